@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json headline metric on the MI355X render path.
+
+Workload (BASELINE.json configs[1], "C2"): 4-channel uint16 1024x1024 tiles (big-endian, as
+ROMIO planes), per-channel window + colour composite to packed ARGB.  One step = one
+omr_render_batch_device call over a batch of tiles already resident in HBM (K1 table build +
+K2 quantize/composite).  Multi-GPU: one process per GPU, each rendering its own batch (tiles
+are independent — no collective on the data path; barrier + max-over-ranks timing only).
+
+Also reported: roofline of K2 (HIP events around every K2 launch on its stream), p50 tile
+latency (device-resident and host-fed), and the reference-CPU proxy (oracle/liboracle.so,
+per-request LUT rebuild + render, on the host cores) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "omero-ms-image-region_amd"))
+
+METRIC = "1024² tiles/sec (whole node) at 1/2/4/8 GPUs; p50 tile latency; HBM GB/s"
+TILE = 1024
+CHANNELS = 4
+BYTES_PER_TILE = TILE * TILE * CHANNELS * 2 + TILE * TILE * 4   # 12,582,912 algorithmic bytes
+HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_batch(torch, batch, unique, device):
+    """[batch][4][1024][1024] big-endian uint16 tiles (int16 storage) + device pointer table."""
+    from omr.synthetic import torch_tiles_u16
+    uniq = torch_tiles_u16(unique, CHANNELS, TILE, TILE, device)
+    uniq = uniq.view(torch.uint8).view(unique, CHANNELS, TILE, TILE, 2).flip(-1).contiguous().view(
+        torch.int16).view(unique, CHANNELS, TILE, TILE)                          # -> big-endian bytes
+    data = torch.empty((batch, CHANNELS, TILE, TILE), dtype=torch.int16, device=device)
+    for t in range(batch):
+        data[t].copy_(uniq[t % unique])
+    plane_bytes = TILE * TILE * 2
+    base = data.data_ptr()
+    table = torch.tensor([[base + (t * CHANNELS + c) * plane_bytes for c in range(CHANNELS)]
+                          for t in range(batch)], dtype=torch.int64, device=device)
+    return data, uniq, table
+
+
+def pmc_traffic(batch):
+    """HBM bytes per K2 launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_render_c2.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d["hbm_bytes_per_tile"] * batch
+    except Exception:
+        return None
+
+
+def cpu_baseline(torch, uniq, seconds, threads):
+    """Reference-CPU proxy on a bounded sample: per-request LUT rebuild + render, thread pool."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import numpy as np
+    import oracle_lib
+    from omr import _lib
+    from omr.synthetic import c2_channels
+    host = uniq.cpu().numpy().view(np.uint16)      # big-endian bytes in uint16 storage
+    tiles = [[np.ascontiguousarray(host[t, c]) for c in range(CHANNELS)] for t in range(host.shape[0])]
+    chans = c2_channels(CHANNELS)
+    n = threads
+    secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
+                                         _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
+                                         n_threads=threads, keep_output=False)
+    n = max(threads, int(n * seconds / max(secs, 1e-3)) // threads * threads)
+    secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
+                                         _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
+                                         n_threads=threads, keep_output=False)
+    return {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "sample": f"{n} C2 tiles (4ch uint16 1024^2 BE, per-request LUT rebuild + composite) "
+                      f"in {secs:.2f} s on {threads} threads (oracle/omr_oracle.c, -O3)"}
+
+
+def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
+    """p50 of one-tile requests: device-resident (HBM in/out) and host-fed (pinned H2D + D2H)."""
+    import numpy as np
+    from omr import _lib
+    dev = data.device
+    out1 = torch.empty((TILE, TILE), dtype=torch.int32, device=dev)
+    planes = [data[0, c] for c in range(CHANNELS)]
+    t_dev = []
+    for i in range(iters + 3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.render_packed_int_device(qdef, chans, planes, _lib.PIXELS_UINT16, TILE, TILE, out1, big_endian=True)
+        ctx.synchronize()
+        if i >= 3:
+            t_dev.append(time.perf_counter() - t0)
+    host = [np.ascontiguousarray(p.cpu().numpy()) for p in planes]
+    t_host = []
+    for i in range(iters + 3):
+        t0 = time.perf_counter()
+        ctx.render_packed_int(qdef, chans, host, _lib.PIXELS_UINT16, TILE, TILE, big_endian=True)
+        if i >= 3:
+            t_host.append(time.perf_counter() - t0)
+    return {"device_resident": round(1e3 * float(np.median(t_dev)), 4),
+            "host_fed": round(1e3 * float(np.median(t_host)), 4)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="tiles per GPU per step")
+    ap.add_argument("--unique", type=int, default=8, help="distinct synthetic tiles per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    import omr
+    from omr import _lib
+    from omr.context import make_bindings, make_qdef
+    from omr.synthetic import c2_channels
+
+    ctx = omr.Context(local_rank)
+    qdef = make_qdef("rgb")
+    chans = c2_channels(CHANNELS)
+    bindings = make_bindings(chans)
+    B = args.batch
+    data, uniq, table = build_batch(torch, B, min(args.unique, B), device)
+    out = torch.empty((B, TILE, TILE), dtype=torch.int32, device=device)
+
+    def step():
+        ctx.render_batch_device(qdef, chans, table, B, _lib.PIXELS_UINT16, TILE, TILE, out,
+                                big_endian=True, bindings=bindings)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    ctx.kernel_timings()
+
+    ctx.enable_kernel_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.enable_kernel_timing(False)
+    k2 = [ms for ms, kind in ctx.kernel_timings() if kind == 2]
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    tiles = world * B * args.steps
+    value = tiles / elapsed
+    k2_ms = sum(k2) / len(k2) if k2 else float("nan")
+    achieved = BYTES_PER_TILE * B / (k2_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(B)
+
+    extra = {}
+    if rank == 0 and world == 1:
+        extra["p50_tile_latency_ms"] = latencies(torch, omr, ctx, qdef, chans, data)
+        if not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            try:
+                extra["cpu_baseline"] = cpu_baseline(torch, uniq, args.cpu_seconds, threads)
+            except Exception as e:  # the baseline is reported, never the target
+                log(f"cpu baseline failed: {e}")
+                extra["cpu_baseline"] = None
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "tiles/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (microscopy-like gamma background + gaussian blobs, seeded)",
+            "config": {
+                "workload": "C2: 4-channel uint16 1024x1024 big-endian tiles -> packed ARGB "
+                            "(per-channel window + colour composite, rgb model), HBM-resident",
+                "tiles_per_gpu_per_step": B,
+                "windows": "0:65535,1755:51199,3218:26623,100:4000",
+                "colors": "0000FF,00FF00,FF0000,FFFFFF",
+                "parallelism": f"dp{world} (independent tile batches per GPU, no collectives)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_render<u16,BE,4ch> (K2)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": BYTES_PER_TILE * B,
+                "avg_launch_ms": round(k2_ms, 5),
+                "launches": len(k2),
+            },
+            "hbm_gbs": round(achieved, 1),
+        }
+        line.update(extra)
+        if "cpu_baseline" not in line:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,271 @@
+/*
+ * omr.h — C ABI of the MI355X-native image-region rendering path.
+ *
+ * This is the drop-in boundary between the reference's Java host code
+ * (omero-ms-image-region's ImageRegionRequestHandler / ShapeMaskRequestHandler)
+ * and hand-written gfx950 HIP kernels.  Every entry point names the reference
+ * call site it replaces.  Paths are relative to
+ *   src/main/java/com/glencoesoftware/omero/ms/image/region/
+ * of the reference.  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * Status codes map onto the reference's HTTP outcomes
+ * (ImageRegionVerticle.java:163-186, ImageRegionMicroserviceVerticle.java:301-304):
+ *   OMR_INVALID_ARGUMENT -> 400 (IllegalArgumentException / ValidationException)
+ *   OMR_NOT_FOUND        -> 404 (handler returned null, e.g. unknown format)
+ *   OMR_QUANTIZATION     -> 500 (QuantizationException, ImageRegionRequestHandler.java:479)
+ *   OMR_DEVICE / OMR_OOM -> 500
+ *
+ * Threading: one omr_ctx per worker thread.  Calls on distinct contexts may run
+ * concurrently; one context must not be called concurrently.  All buffers are
+ * caller-owned.  Unlike the reference (global mutable compression level,
+ * ImageRegionRequestHandler.java:457-460 on a Spring singleton), JPEG quality is
+ * a per-call argument.
+ */
+#ifndef OMR_OMR_H
+#define OMR_OMR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMR_ABI_VERSION 1
+
+typedef int32_t omr_status;
+enum {
+    OMR_OK = 0,
+    OMR_INVALID_ARGUMENT = 1,
+    OMR_NOT_FOUND = 2,
+    OMR_QUANTIZATION = 3,
+    OMR_DEVICE = 4,
+    OMR_OOM = 5,
+    OMR_BUFFER_TOO_SMALL = 6
+};
+
+/* ome.model.enums.PixelsType values the path supports. */
+enum {
+    OMR_PIXELS_INT8 = 0,
+    OMR_PIXELS_UINT8 = 1,
+    OMR_PIXELS_INT16 = 2,
+    OMR_PIXELS_UINT16 = 3,
+    OMR_PIXELS_INT32 = 4,
+    OMR_PIXELS_UINT32 = 5,
+    OMR_PIXELS_FLOAT = 6,
+    OMR_PIXELS_DOUBLE = 7
+};
+
+/* ome.model.enums.Family (ImageRegionVerticle.java:72-76 lists the families). */
+enum {
+    OMR_FAMILY_LINEAR = 0,
+    OMR_FAMILY_POLYNOMIAL = 1,
+    OMR_FAMILY_LOGARITHMIC = 2,
+    OMR_FAMILY_EXPONENTIAL = 3
+};
+
+/* RenderingModel: Renderer.MODEL_GREYSCALE / MODEL_RGB (ImageRegionCtx.java:333-341). */
+enum { OMR_MODEL_GREYSCALE = 0, OMR_MODEL_RGB = 1 };
+
+/* IProjection constants used by ProjectionService.java:75-91. */
+enum { OMR_PROJECTION_MAX = 0, OMR_PROJECTION_MEAN = 1, OMR_PROJECTION_SUM = 2 };
+
+/* QuantumDef + RenderingDef model (ImageRegionRequestHandler.java:262-277). */
+typedef struct omr_quantum_def {
+    int32_t cd_start;        /* 0 */
+    int32_t cd_end;          /* 255 (QuantumFactory.DEPTH_8BIT) */
+    int32_t bit_resolution;  /* 255 */
+    int32_t model;           /* OMR_MODEL_* */
+} omr_quantum_def;
+
+/*
+ * One ChannelBinding as the Renderer sees it after updateSettings
+ * (ImageRegionRequestHandler.java:281-298 defaults, :689-741 request settings).
+ */
+typedef struct omr_channel_binding {
+    int32_t active;           /* Renderer.setActive (:696) */
+    int32_t family;           /* OMR_FAMILY_*; HTTP path is always linear (:285) */
+    double coefficient;       /* curve coefficient k; HTTP path 1.0 (:286) */
+    int32_t noise_reduction;  /* HTTP path false (:287) */
+    int32_t reverse;          /* ReverseIntensityContext in the codomain chain (:725-726) */
+    double input_start;       /* Renderer.setChannelWindow start (:703), float-rounded by ImageRegionCtx.java:313 */
+    double input_end;         /* window end */
+    double global_min;        /* LUT domain = StatsInfo/type range (StatsFactory.initPixelsRange, :290-291) */
+    double global_max;
+    uint8_t rgba[4];          /* Renderer.setRGBA (:712) */
+    const uint8_t* lut;       /* setChannelLookupTable (:708): 768 bytes R[256] G[256] B[256]; NULL = use rgba */
+} omr_channel_binding;
+
+/* RegionDef (omeis.providers.re.data.RegionDef). */
+typedef struct omr_region {
+    int32_t x, y, width, height;
+} omr_region;
+
+typedef struct omr_ctx omr_ctx;
+
+/* ---- context --------------------------------------------------------- */
+int32_t     omr_abi_version(void);
+omr_status  omr_ctx_create(int32_t device_ordinal, omr_ctx** out);
+void        omr_ctx_destroy(omr_ctx* ctx);
+const char* omr_last_error(const omr_ctx* ctx);
+omr_status  omr_ctx_synchronize(omr_ctx* ctx);
+/* Run subsequent device-side calls on a caller-owned hipStream_t (NULL = ctx's own). */
+omr_status  omr_ctx_set_stream(omr_ctx* ctx, void* hip_stream);
+void*       omr_ctx_get_stream(omr_ctx* ctx);
+/*
+ * Kernel timing (perf4j StopWatch analogue, ImageRegionRequestHandler.java:502): when enabled,
+ * every hot-kernel launch (K2 render, K3 projection, K4 JPEG) is bracketed by HIP events on
+ * the stream it is launched on.  omr_ctx_kernel_timings synchronises, writes up to `cap`
+ * per-launch durations in ms (launch order) and clears the record; returns the count.
+ * kind_out (optional) receives 2 = render, 3 = projection, 4 = jpeg per entry.
+ */
+omr_status  omr_ctx_enable_kernel_timing(omr_ctx* ctx, int32_t enable);
+int32_t     omr_ctx_kernel_timings(omr_ctx* ctx, float* ms_out, int32_t* kind_out, int32_t cap);
+/* Pinned host staging (PixelBuffer tile reads land here). */
+void*       omr_pinned_alloc(omr_ctx* ctx, size_t bytes);
+void        omr_pinned_free(omr_ctx* ctx, void* p);
+
+/* ---- render (quantize + codomain + composite + flip) ------------------ */
+/*
+ * Replaces renderer.renderAsPackedInt(planeDef, null)  (ImageRegionRequestHandler.java:559)
+ * followed by flip(buf, sizeX, sizeY, flipH, flipV)      (ImageRegionRequestHandler.java:574-575, :616-642).
+ * planes[c] points at the region of channel c (size_c pointers; NULL allowed for inactive
+ * channels); row_stride is in pixels (0 = width).  big_endian: ROMIO planes are big-endian.
+ * Host memory in and out; synchronous.
+ */
+omr_status omr_render_packed_int(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                 const omr_channel_binding* channels, int32_t size_c,
+                                 const void* const* planes, int64_t row_stride,
+                                 int32_t pixel_type, int32_t big_endian,
+                                 int32_t width, int32_t height,
+                                 int32_t flip_h, int32_t flip_v,
+                                 uint32_t* argb_out);
+
+/* Same, device pointers, asynchronous on the context stream. */
+omr_status omr_render_packed_int_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                        const omr_channel_binding* channels, int32_t size_c,
+                                        const void* const* d_planes, int64_t row_stride,
+                                        int32_t pixel_type, int32_t big_endian,
+                                        int32_t width, int32_t height,
+                                        int32_t flip_h, int32_t flip_v,
+                                        uint32_t* d_argb_out);
+
+/*
+ * Batch of n_tiles same-settings tile requests (one viewer's tiles; the request-level
+ * parallelism of ImageRegionMicroserviceVerticle.java:149-165 coalesced into one launch).
+ * d_plane_ptrs: DEVICE array of n_tiles*size_c device pointers ([tile][channel]).
+ * d_argb_out: device [n_tiles][height][width].  d_status (optional, device int32[n_tiles]):
+ * per-tile OMR_OK / OMR_QUANTIZATION.  Asynchronous on the context stream.
+ */
+omr_status omr_render_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                   const omr_channel_binding* channels, int32_t size_c,
+                                   const void* const* d_plane_ptrs, int32_t n_tiles,
+                                   int64_t row_stride, int32_t pixel_type, int32_t big_endian,
+                                   int32_t width, int32_t height,
+                                   int32_t flip_h, int32_t flip_v,
+                                   uint32_t* d_argb_out, int32_t* d_status);
+
+/*
+ * Standalone output flip of an already-rendered ARGB buffer on the device
+ * (ImageRegionRequestHandler.flip, :616-642).  src and dest must not alias.
+ * Identity (no flip) copies.
+ */
+omr_status omr_flip_argb_device(omr_ctx* ctx, const uint32_t* d_src, uint32_t* d_dest,
+                                int32_t size_x, int32_t size_y, int32_t flip_h, int32_t flip_v);
+/* ShapeMaskRequestHandler.flip(byte[]...) (:128-154), byte-per-pixel. */
+omr_status omr_flip_mask_device(omr_ctx* ctx, const uint8_t* d_src, uint8_t* d_dest,
+                                int32_t size_x, int32_t size_y, int32_t flip_h, int32_t flip_v);
+
+/* ---- Z-projection ------------------------------------------------------ */
+/*
+ * ProjectionService.projectStack(pixels, buf, alg, t, c, stepping, start, end)
+ * (ProjectionService.java:46-120): one channel's stack [size_z][size_y][size_x] -> one plane
+ * of the same pixel type.  Max over z in [start,end] inclusive; mean/sum over [start,end)
+ * (ProjectionService.java:184 vs :271).  Host memory; synchronous.
+ */
+omr_status omr_project_stack(omr_ctx* ctx, const void* stack, int32_t pixel_type,
+                             int32_t big_endian_in, int32_t size_x, int32_t size_y, int32_t size_z,
+                             int32_t algorithm, int32_t start, int32_t end, int32_t stepping,
+                             void* plane_out, int32_t big_endian_out);
+omr_status omr_project_stack_device(omr_ctx* ctx, const void* d_stack, int32_t pixel_type,
+                                    int32_t big_endian_in, int32_t size_x, int32_t size_y,
+                                    int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
+                                    int32_t stepping, void* d_plane_out, int32_t big_endian_out);
+/*
+ * Projection glue + render (ImageRegionRequestHandler.java:506-559): project every active
+ * channel's stack (d_stacks[c], NULL for inactive) and render the full projected plane.
+ * Projected planes stay in HBM (native byte order); output device [size_y][size_x].
+ */
+omr_status omr_render_projected_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                       const omr_channel_binding* channels, int32_t size_c,
+                                       const void* const* d_stacks, int32_t pixel_type,
+                                       int32_t big_endian, int32_t size_x, int32_t size_y,
+                                       int32_t size_z, int32_t algorithm, int32_t start,
+                                       int32_t end, int32_t stepping, int32_t flip_h,
+                                       int32_t flip_v, uint32_t* d_argb_out);
+
+/* ---- encode --------------------------------------------------------------- */
+/* Upper bound of the encoded size (callers size `out` with it). */
+size_t omr_jpeg_max_bytes(int32_t width, int32_t height);
+size_t omr_png_max_bytes(int32_t width, int32_t height, int32_t channels);
+/*
+ * JPEG baseline (JFIF, YCbCr 4:2:0, IJG islow FDCT, Java ImageIO quality scaling,
+ * standard Huffman tables) of the 24-bit RGB view of ARGB pixels
+ * (ImageUtil.createBufferedImage + compressionService.compressToStream,
+ *  ImageRegionRequestHandler.java:576-582).  Quality is per call.
+ * Host ARGB in, host bytes out.
+ */
+omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, int32_t height,
+                           float quality, uint8_t* out, size_t cap, size_t* out_len);
+/* Device ARGB in (e.g. straight from omr_render_*_device), host bytes out. */
+omr_status omr_encode_jpeg_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
+                                  int32_t height, float quality, uint8_t* out, size_t cap,
+                                  size_t* out_len);
+/* Java ImageIO quality -> quantisation tables (natural order), JPEGQTable.getScaledInstance. */
+omr_status omr_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]);
+
+/* PNG RGB8 of ARGB pixels (ImageIO.write(image, "png"), ImageRegionRequestHandler.java:598). */
+omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int32_t height,
+                          uint8_t* out, size_t cap, size_t* out_len);
+omr_status omr_encode_png_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
+                                 int32_t height, uint8_t* out, size_t cap, size_t* out_len);
+
+/* ---- shape mask ------------------------------------------------------------- */
+/*
+ * ShapeMaskRequestHandler.renderShapeMask(Color, byte[], w, h) (:165-207): MSB-first bit mask
+ * (no row padding) -> flip -> 2-entry palette PNG (index 0 transparent, index 1 = rgba).
+ * Deviation: flips at pixel level also when width % 8 == 0 (the reference flips the
+ * still-packed buffer there and fails, :175-181).  Host in/out.
+ */
+omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n_bytes,
+                                     int32_t width, int32_t height, const uint8_t rgba[4],
+                                     int32_t flip_h, int32_t flip_v,
+                                     uint8_t* out, size_t cap, size_t* out_len);
+
+/* ---- host-side request helpers (no device work) ---------------------------------- */
+/* ImageRegionRequestHandler.splitHTMLColor (:865-890), bug-compatible; OMR_INVALID_ARGUMENT = null. */
+omr_status omr_split_html_color(const char* color, int32_t rgba_out[4]);
+/* ShapeMaskRequestHandler.renderShapeMask(Mask) fill colour (:97-106). */
+omr_status omr_shape_mask_fill_color(int32_t has_mask_fill, int32_t mask_fill_color,
+                                     const char* request_color, uint8_t rgba_out[4]);
+/*
+ * getRegionDef + truncateRegionDef + flipRegionDef (ImageRegionRequestHandler.java:789-832,
+ * :751-758, :770-780).  mode: 0 = tile (tile.x/y in tile units, width/height 0 = use
+ * tile_size_*), 1 = region (pixels), 2 = neither (full plane).  level_sizes holds
+ * n_levels (sizeX,sizeY) pairs; resolution < 0 means "not given" (0).
+ */
+omr_status omr_get_region_def(int32_t mode, const omr_region* request, int32_t resolution,
+                              const int32_t* level_sizes, int32_t n_levels,
+                              int32_t tile_size_x, int32_t tile_size_y, int32_t max_tile_length,
+                              int32_t flip_h, int32_t flip_v, omr_region* out);
+/* setResolutionLevel (:840-853): Renderer level = nLevels - resolution - 1. */
+int32_t omr_resolution_level(int32_t n_levels, int32_t resolution);
+/* checkPlaneDef (:651-681): truncate region to the level size. */
+omr_status omr_check_plane_def(omr_region* region, int32_t size_x, int32_t size_y);
+/* LutReader: parse an ImageJ .lut file image (768 B binary, 800 B with header, or text). */
+omr_status omr_parse_lut(const uint8_t* data, size_t n, uint8_t lut_out[768]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMR_OMR_H */

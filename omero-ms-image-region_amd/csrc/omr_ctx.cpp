@@ -1,0 +1,202 @@
+// omr_ctx.cpp — per-worker-thread context: device, stream, workspace, pinned staging.
+// One context per Vert.x worker thread replaces the per-request Renderer construction
+// (ImageRegionRequestHandler.java:436-440) as the unit of state; the reference's only
+// parallelism (worker-verticle instances, ImageRegionMicroserviceVerticle.java:149-165)
+// maps to one context per thread, or one per GPU for batched launches.
+#include "omr_internal.h"
+
+#include <cstdio>
+
+namespace omr {
+
+omr_status fail(Ctx* c, omr_status s, const std::string& msg) {
+    if (c) c->last_error = msg;
+    return s;
+}
+
+omr_status hip_fail(Ctx* c, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(c, e == hipErrorOutOfMemory ? OMR_OOM : OMR_DEVICE, m);
+}
+
+int bytes_per_pixel(int32_t t) {
+    switch (t) {
+    case OMR_PIXELS_INT8: case OMR_PIXELS_UINT8: return 1;
+    case OMR_PIXELS_INT16: case OMR_PIXELS_UINT16: return 2;
+    case OMR_PIXELS_INT32: case OMR_PIXELS_UINT32: case OMR_PIXELS_FLOAT: return 4;
+    case OMR_PIXELS_DOUBLE: return 8;
+    default: return 0;
+    }
+}
+
+omr_status ensure_workspace(Ctx* c, size_t bytes) {
+    if (bytes <= c->ws_cap) return OMR_OK;
+    size_t cap = align_up(bytes + bytes / 4, 1 << 20);
+    if (c->ws) {
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        OMR_HIP(c, hipFree(c->ws));
+        c->ws = nullptr;
+        c->ws_cap = 0;
+    }
+    OMR_HIP(c, hipMalloc(&c->ws, cap));
+    c->ws_cap = cap;
+    return OMR_OK;
+}
+
+omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
+    if (bytes == 0) return OMR_OK;
+    if (bytes > c->pin_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (c->pin[i]) {
+                OMR_HIP(c, hipEventSynchronize(c->pin_ev[i]));
+                OMR_HIP(c, hipHostFree(c->pin[i]));
+                c->pin[i] = nullptr;
+            }
+        }
+        size_t cap = align_up(bytes, 1 << 16);
+        for (int i = 0; i < 2; ++i) OMR_HIP(c, hipHostMalloc(&c->pin[i], cap, hipHostMallocDefault));
+        c->pin_cap = cap;
+    }
+    const int s = c->pin_slot;
+    c->pin_slot ^= 1;
+    OMR_HIP(c, hipEventSynchronize(c->pin_ev[s]));  // previous copy out of this slot is done
+    std::memcpy(c->pin[s], src, bytes);
+    OMR_HIP(c, hipMemcpyAsync(dst, c->pin[s], bytes, hipMemcpyHostToDevice, c->stream));
+    OMR_HIP(c, hipEventRecord(c->pin_ev[s], c->stream));
+    return OMR_OK;
+}
+
+static hipEvent_t pooled_event(Ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+KernelTimer::KernelTimer(Ctx* ctx, int k) : c(ctx), kind(k) {
+    if (!c->timing) return;
+    hipEvent_t start = pooled_event(c);
+    stop = pooled_event(c);
+    if (!start || !stop) { stop = nullptr; return; }
+    (void)hipEventRecord(start, c->stream);
+    c->timed.push_back({start, stop, kind});
+}
+
+KernelTimer::~KernelTimer() {
+    if (stop) (void)hipEventRecord(stop, c->stream);
+}
+
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+int32_t omr_abi_version(void) { return OMR_ABI_VERSION; }
+
+omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
+    if (!out) return OMR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return OMR_DEVICE;
+    if (device_ordinal < 0 || device_ordinal >= n) return OMR_INVALID_ARGUMENT;
+    omr_ctx* c = new omr_ctx();
+    c->device = device_ordinal;
+    hipError_t e = hipSetDevice(device_ordinal);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_flag, 256);
+    if (e == hipSuccess) e = hipMemset(c->d_flag, 0, 256);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming);
+    if (e == hipSuccess) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) c->cu_count = prop.multiProcessorCount;
+    }
+    if (e != hipSuccess) {
+        omr_ctx_destroy(c);
+        return e == hipErrorOutOfMemory ? OMR_OOM : OMR_DEVICE;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return OMR_OK;
+}
+
+omr_status omr_ctx_enable_kernel_timing(omr_ctx* c, int32_t enable) {
+    if (!c) return OMR_INVALID_ARGUMENT;
+    c->timing = enable != 0;
+    return OMR_OK;
+}
+
+int32_t omr_ctx_kernel_timings(omr_ctx* c, float* ms_out, int32_t* kind_out, int32_t cap) {
+    if (!c) return -1;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    int32_t n = 0;
+    for (auto& t : c->timed) {
+        float ms = 0.f;
+        (void)hipEventSynchronize(t.stop);
+        if (hipEventElapsedTime(&ms, t.start, t.stop) != hipSuccess) ms = -1.f;
+        if (n < cap && ms_out) {
+            ms_out[n] = ms;
+            if (kind_out) kind_out[n] = t.kind;
+        }
+        ++n;
+        c->event_pool.push_back(t.start);
+        c->event_pool.push_back(t.stop);
+    }
+    c->timed.clear();
+    return n < cap ? n : cap;
+}
+
+void omr_ctx_destroy(omr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& t : c->timed) { c->event_pool.push_back(t.start); c->event_pool.push_back(t.stop); }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
+        if (c->pin[i]) (void)hipHostFree(c->pin[i]);
+    }
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->d_flag) (void)hipFree(c->d_flag);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* omr_last_error(const omr_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
+
+omr_status omr_ctx_synchronize(omr_ctx* c) {
+    if (!c) return OMR_INVALID_ARGUMENT;
+    OMR_HIP(c, hipStreamSynchronize(c->stream));
+    int32_t flag = 0;
+    OMR_HIP(c, hipMemcpy(&flag, c->d_flag, sizeof(flag), hipMemcpyDeviceToHost));
+    if (flag) {
+        OMR_HIP(c, hipMemsetAsync(c->d_flag, 0, sizeof(flag), c->stream));
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        return fail(c, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");
+    }
+    return OMR_OK;
+}
+
+omr_status omr_ctx_set_stream(omr_ctx* c, void* s) {
+    if (!c) return OMR_INVALID_ARGUMENT;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    return OMR_OK;
+}
+
+void* omr_ctx_get_stream(omr_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+void* omr_pinned_alloc(omr_ctx* c, size_t bytes) {
+    void* p = nullptr;
+    if (!c || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void omr_pinned_free(omr_ctx* c, void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+}  // extern "C"

@@ -1,0 +1,116 @@
+// omr_internal.h — shared definitions of the MI355X image-region library (libomr.so).
+// Host runtime pieces (context, workspace, staging) and the device-side parameter
+// blocks the kernels read.  Reference citations: see include/omr/omr.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "omr/omr.h"
+
+namespace omr {
+
+constexpr int kMaxActive = 32;        // active channels per render call
+constexpr int kBlock = 256;           // threads per workgroup (4 waves)
+constexpr uint32_t kErrBit = 0x80000000u;  // contrib-table entry flag: value outside LUT domain
+
+// Per-active-channel quantization mode.
+enum ChanMode : int32_t {
+    kModeTable8 = 0,   // 8-bit types: quantization+codomain+colour folded into contrib[raw byte]
+    kModeLinear16 = 1, // 16-bit linear: exact double evaluation of the LUT entry, contrib[v]
+    kModeLut16 = 2,    // 16-bit other families / noise reduction: byte LUT gather, contrib[v]
+    kModeEval = 3      // 32-bit int / float / double: per-pixel q(x) in double, contrib[v]
+};
+
+// One active channel as the kernels see it (device memory, read uniformly).
+struct ChanParam {
+    int32_t index;      // channel index into the [tile][size_c] plane table
+    int32_t mode;
+    int32_t lo, hi;     // integer window thresholds: x < lo -> cdStart, x >= hi -> cdEnd
+    int32_t gmin, gmax; // LUT domain (QuantizationException outside)
+    int32_t family, nr;
+    int32_t reverse, has_lut;
+    int32_t second;     // apply the a1*v + cdStart rounding stage (not identity)
+    int32_t pad0;
+    double ws, we, k;   // window, coefficient
+    double ys, a0, a1;  // f(ws), bitRes/(f(we)-f(ws)), (cdEnd-cdStart)/bitRes
+    double dec;         // noise-reduction decile width
+    float ratio[3];     // (c/255f)*(alpha/255f)
+    float pad1;
+    uint64_t lut_off;   // byte offset of this channel's quantization LUT in the workspace
+    uint8_t lut_rgb[768];  // LutReader colours (valid when has_lut)
+};
+
+struct RenderPlan {
+    int32_t n_active;
+    int32_t cd_start, cd_end;
+    int32_t greyscale;
+    ChanParam ch[kMaxActive];
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    // device workspace (grow-only bump arena, reset per call)
+    void* ws = nullptr;
+    size_t ws_cap = 0;
+    // device-side sticky status word (quantization errors of async calls)
+    int32_t* d_flag = nullptr;
+    // pinned staging for parameter blocks (2-slot ring)
+    void* pin[2] = {nullptr, nullptr};
+    size_t pin_cap = 0;
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    int pin_slot = 0;
+    int cu_count = 256;
+    // kernel timing (omr_ctx_enable_kernel_timing)
+    bool timing = false;
+    struct Timed { hipEvent_t start, stop; int kind; };
+    std::vector<Timed> timed;
+    std::vector<hipEvent_t> event_pool;
+};
+
+// Bracket one hot-kernel launch with events when timing is enabled.
+struct KernelTimer {
+    Ctx* c;
+    int kind;
+    hipEvent_t stop = nullptr;
+    KernelTimer(Ctx* ctx, int k);
+    ~KernelTimer();
+};
+
+omr_status fail(Ctx* c, omr_status s, const std::string& msg);
+omr_status hip_fail(Ctx* c, hipError_t e, const char* what);
+// Ensure the workspace holds at least `bytes`; invalidates previous contents.
+omr_status ensure_workspace(Ctx* c, size_t bytes);
+// Copy `bytes` from host `src` to device `dst` through the pinned ring (async on ctx stream).
+omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes);
+int bytes_per_pixel(int32_t pixel_type);
+// K3 launch over up to 32 stacks (omr_project.hip).
+omr_status validate_projection_args(Ctx* c, int32_t pixel_type, int32_t size_x, int32_t size_y,
+                                    int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
+                                    int32_t stepping);
+omr_status enqueue_projection(Ctx* c, const void* const* d_stacks, void* const* d_outs, int n,
+                              int32_t pixel_type, int32_t be_in, int32_t size_x, int32_t size_y,
+                              int32_t algorithm, int32_t start, int32_t end, int32_t stepping,
+                              int32_t be_out);
+
+#define OMR_HIP(ctx, expr)                                          \
+    do {                                                            \
+        hipError_t _e = (expr);                                     \
+        if (_e != hipSuccess) return ::omr::hip_fail((ctx), _e, #expr); \
+    } while (0)
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace omr
+
+struct omr_ctx : omr::Ctx {};

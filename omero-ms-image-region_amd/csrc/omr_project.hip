@@ -1,0 +1,336 @@
+// omr_project.hip — K3 Z-projection and the standalone flip kernels.
+//
+// K3 replaces ProjectionService.projectStack (ProjectionService.java:46-120) with
+// projectStackMax (:176-199) and projectStackMeanOrSum (:259-291).  Each lane owns a
+// 16-byte column chunk of the XY plane and walks z with several loads in flight, so the
+// Z-stack streams through HBM exactly once (coalesced rows; no transposition).
+// The flips replace ImageRegionRequestHandler.flip (:616-642) and
+// ShapeMaskRequestHandler.flip (:128-154) for callers holding an already-rendered buffer.
+#include "omr_device.h"
+
+namespace omr {
+
+constexpr int kMaxStacks = 32;
+
+struct K3Args {
+    const uint8_t* stacks[kMaxStacks];
+    uint8_t* outs[kMaxStacks];
+    int32_t n_stacks;
+    int32_t start, end, stepping;
+    int64_t plane;        // pixels per plane
+    uint32_t chunks;      // chunks per plane
+};
+
+template <typename T> struct Raw;
+template <> struct Raw<int8_t> { using U = uint8_t; };
+template <> struct Raw<uint8_t> { using U = uint8_t; };
+template <> struct Raw<int16_t> { using U = uint16_t; };
+template <> struct Raw<uint16_t> { using U = uint16_t; };
+template <> struct Raw<int32_t> { using U = uint32_t; };
+template <> struct Raw<uint32_t> { using U = uint32_t; };
+template <> struct Raw<float> { using U = uint32_t; };
+template <> struct Raw<double> { using U = uint64_t; };
+
+template <typename U>
+__device__ __forceinline__ U bswap_any(U v) {
+    if constexpr (sizeof(U) == 1) return v;
+    else if constexpr (sizeof(U) == 2) return (U)(((v & 0xFF) << 8) | (v >> 8));
+    else if constexpr (sizeof(U) == 4) return bswap32(v);
+    else return ((uint64_t)bswap32((uint32_t)v) << 32) | bswap32((uint32_t)(v >> 32));
+}
+
+template <typename T, bool BE>
+__device__ __forceinline__ T load_px(const uint8_t* p) {
+    using U = typename Raw<T>::U;
+    U u = *reinterpret_cast<const U*>(p);
+    if constexpr (BE) u = bswap_any<U>(u);
+    T t;
+    __builtin_memcpy(&t, &u, sizeof(T));
+    return t;
+}
+
+template <typename T, bool BE>
+__device__ __forceinline__ void store_px(uint8_t* p, T t) {
+    using U = typename Raw<T>::U;
+    U u;
+    __builtin_memcpy(&u, &t, sizeof(T));
+    if constexpr (BE) u = bswap_any<U>(u);
+    *reinterpret_cast<U*>(p) = u;
+}
+
+template <typename T> __device__ __forceinline__ double type_max() {
+    if constexpr (std::is_same<T, int8_t>::value) return 127.0;
+    else if constexpr (std::is_same<T, uint8_t>::value) return 255.0;
+    else if constexpr (std::is_same<T, int16_t>::value) return 32767.0;
+    else if constexpr (std::is_same<T, uint16_t>::value) return 65535.0;
+    else if constexpr (std::is_same<T, int32_t>::value) return 2147483647.0;
+    else if constexpr (std::is_same<T, uint32_t>::value) return 4294967295.0;
+    else if constexpr (std::is_same<T, float>::value) return 3.4028234663852886e38;
+    else return 1.7976931348623157e308;
+}
+
+__device__ __forceinline__ int32_t java_d2i(double d) {
+    if (d != d) return 0;
+    if (d >= 2147483647.0) return INT32_MAX;
+    if (d <= -2147483648.0) return INT32_MIN;
+    return (int32_t)d;
+}
+__device__ __forceinline__ int64_t java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+// PixelData.setPixelValue narrowing (S9 in oracle/omr_oracle.c).
+template <typename T> __device__ __forceinline__ T narrow(double v) {
+    if constexpr (std::is_same<T, float>::value) return (float)v;
+    else if constexpr (std::is_same<T, double>::value) return v;
+    else if constexpr (std::is_same<T, uint32_t>::value) return (uint32_t)java_d2l(v);
+    else return (T)java_d2i(v);
+}
+
+// Accumulator: exact integer sum for integer types (== Java's double sum, every partial
+// sum < 2^53), double for float types (same order as the reference loop).
+template <typename T> struct Acc { using type = double; };
+template <> struct Acc<int8_t> { using type = int64_t; };
+template <> struct Acc<uint8_t> { using type = int64_t; };
+template <> struct Acc<int16_t> { using type = int64_t; };
+template <> struct Acc<uint16_t> { using type = int64_t; };
+template <> struct Acc<int32_t> { using type = int64_t; };
+template <> struct Acc<uint32_t> { using type = int64_t; };
+
+template <typename T, bool BEI, bool BEO, int ALG>
+__global__ void __launch_bounds__(kBlock) k_project(K3Args A) {
+    constexpr int V = sizeof(T) >= 8 ? 2 : 16 / (int)sizeof(T);   // pixels per lane (16 B)
+    const int s = blockIdx.y;
+    const uint8_t* __restrict__ stack = A.stacks[s];
+    uint8_t* __restrict__ out = A.outs[s];
+    const int64_t plane_bytes = A.plane * (int64_t)sizeof(T);
+    for (uint32_t c = blockIdx.x * kBlock + threadIdx.x; c < A.chunks; c += gridDim.x * kBlock) {
+        const int64_t px0 = (int64_t)c * V;
+        const int nv = (int)min<int64_t>(V, A.plane - px0);
+        if (ALG == OMR_PROJECTION_MAX) {
+            T best[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) best[j] = (T)0;
+            const uint8_t* p = stack + (int64_t)A.start * plane_bytes + px0 * (int64_t)sizeof(T);
+            const int64_t step = plane_bytes * A.stepping;
+            if (nv == V) {
+                int z = A.start;
+#pragma unroll 4
+                for (; z <= A.end; z += A.stepping, p += step) {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {
+                        const T v = load_px<T, BEI>(p + j * sizeof(T));
+                        if (v > best[j]) best[j] = v;   // stackValue > projectedValue (:187)
+                    }
+                }
+            } else {
+                for (int z = A.start; z <= A.end; z += A.stepping, p += step)
+                    for (int j = 0; j < nv; ++j) {
+                        const T v = load_px<T, BEI>(p + j * sizeof(T));
+                        if (v > best[j]) best[j] = v;
+                    }
+            }
+            for (int j = 0; j < nv; ++j) store_px<T, BEO>(out + (px0 + j) * sizeof(T), best[j]);
+        } else {
+            using AT = typename Acc<T>::type;
+            AT sum[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) sum[j] = 0;
+            int count = 0;
+            const uint8_t* p = stack + (int64_t)A.start * plane_bytes + px0 * (int64_t)sizeof(T);
+            const int64_t step = plane_bytes * A.stepping;
+            if (nv == V) {
+#pragma unroll 4
+                for (int z = A.start; z < A.end; z += A.stepping, p += step) {
+#pragma unroll
+                    for (int j = 0; j < V; ++j) sum[j] += (AT)load_px<T, BEI>(p + j * sizeof(T));
+                    ++count;
+                }
+            } else {
+                for (int z = A.start; z < A.end; z += A.stepping, p += step) {
+                    for (int j = 0; j < nv; ++j) sum[j] += (AT)load_px<T, BEI>(p + j * sizeof(T));
+                    ++count;
+                }
+            }
+            const double pmax = type_max<T>();
+            for (int j = 0; j < nv; ++j) {
+                double v = (double)sum[j];
+                if (ALG == OMR_PROJECTION_MEAN) v = v / (double)count;
+                if (v > pmax) v = pmax;
+                store_px<T, BEO>(out + (px0 + j) * sizeof(T), narrow<T>(v));
+            }
+        }
+    }
+}
+
+template <typename T, bool BEI, bool BEO>
+static hipError_t launch_project_alg(const K3Args& a, int alg, dim3 grid, hipStream_t s) {
+    switch (alg) {
+    case OMR_PROJECTION_MAX: hipLaunchKernelGGL((k_project<T, BEI, BEO, OMR_PROJECTION_MAX>), grid, dim3(kBlock), 0, s, a); break;
+    case OMR_PROJECTION_MEAN: hipLaunchKernelGGL((k_project<T, BEI, BEO, OMR_PROJECTION_MEAN>), grid, dim3(kBlock), 0, s, a); break;
+    default: hipLaunchKernelGGL((k_project<T, BEI, BEO, OMR_PROJECTION_SUM>), grid, dim3(kBlock), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_project_t(const K3Args& a, int alg, bool bei, bool beo, dim3 grid, hipStream_t s) {
+    if (bei) return beo ? launch_project_alg<T, true, true>(a, alg, grid, s) : launch_project_alg<T, true, false>(a, alg, grid, s);
+    return beo ? launch_project_alg<T, false, true>(a, alg, grid, s) : launch_project_alg<T, false, false>(a, alg, grid, s);
+}
+
+// Validation exactly as ProjectionService.java:53-64 / :154-161 / :140-144 / :88-90.
+static omr_status validate_projection(Ctx* ctx, int32_t pixel_type, int32_t size_x, int32_t size_y,
+                                      int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
+                                      int32_t stepping) {
+    if (!bytes_per_pixel(pixel_type)) return fail(ctx, OMR_INVALID_ARGUMENT, "unsupported pixel type");
+    if (size_x < 0 || size_y < 0 || size_z <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "bad stack dimensions");
+    if (start < 0 || end < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "Z interval value cannot be negative.");
+    if (start >= size_z || end >= size_z)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "Z interval value cannot be >= " + std::to_string(size_z));
+    if (stepping <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "stepping: " + std::to_string(stepping) + " <= 0");
+    if (algorithm < OMR_PROJECTION_MAX || algorithm > OMR_PROJECTION_SUM)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "Unknown algorithm: " + std::to_string(algorithm));
+    return OMR_OK;
+}
+
+omr_status enqueue_projection(Ctx* ctx, const void* const* d_stacks, void* const* d_outs, int n,
+                              int32_t pixel_type, int32_t be_in, int32_t size_x, int32_t size_y,
+                              int32_t algorithm, int32_t start, int32_t end, int32_t stepping,
+                              int32_t be_out) {
+    if (n <= 0) return OMR_OK;
+    if (n > kMaxStacks) return fail(ctx, OMR_INVALID_ARGUMENT, "more than 32 stacks per launch");
+    K3Args a;
+    std::memset(&a, 0, sizeof(a));
+    for (int i = 0; i < n; ++i) {
+        a.stacks[i] = static_cast<const uint8_t*>(d_stacks[i]);
+        a.outs[i] = static_cast<uint8_t*>(d_outs[i]);
+    }
+    a.n_stacks = n;
+    a.start = start;
+    a.end = end;
+    a.stepping = stepping;
+    a.plane = (int64_t)size_x * size_y;
+    if (a.plane == 0) return OMR_OK;
+    const int bpp = bytes_per_pixel(pixel_type);
+    const int v = bpp >= 8 ? 2 : 16 / bpp;
+    const int64_t chunks = (a.plane + v - 1) / v;
+    if (chunks >= (1ll << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "plane too large");
+    a.chunks = (uint32_t)chunks;
+    const int64_t bx = std::min<int64_t>((chunks + kBlock - 1) / kBlock, (int64_t)ctx->cu_count * 8);
+    const dim3 grid((unsigned)bx, (unsigned)n);
+    const bool bi = be_in != 0, bo = be_out != 0;
+    hipError_t e;
+    KernelTimer timer(ctx, 3);
+    switch (pixel_type) {
+    case OMR_PIXELS_INT8: e = launch_project_t<int8_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_UINT8: e = launch_project_t<uint8_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_INT16: e = launch_project_t<int16_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_UINT16: e = launch_project_t<uint16_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_INT32: e = launch_project_t<int32_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_UINT32: e = launch_project_t<uint32_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    case OMR_PIXELS_FLOAT: e = launch_project_t<float>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    default: e = launch_project_t<double>(a, algorithm, bi, bo, grid, ctx->stream); break;
+    }
+    OMR_HIP(ctx, e);
+    return OMR_OK;
+}
+
+omr_status validate_projection_args(Ctx* ctx, int32_t pixel_type, int32_t size_x, int32_t size_y,
+                                    int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
+                                    int32_t stepping) {
+    return validate_projection(ctx, pixel_type, size_x, size_y, size_z, algorithm, start, end, stepping);
+}
+
+// ------------------------------------------------------------------------------- flips
+template <typename T>
+__global__ void __launch_bounds__(kBlock) k_flip(const T* __restrict__ src, T* __restrict__ dst, int W,
+                                                 int H, int fh, int fv, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+        const int oy = fv ? H - 1 - y : y, ox = fh ? W - 1 - x : x;
+        dst[(int64_t)oy * W + ox] = src[i];
+    }
+}
+
+template <typename T>
+static omr_status flip_device(Ctx* ctx, const T* src, T* dst, int32_t W, int32_t H, int32_t fh, int32_t fv) {
+    if (!fh && !fv) {
+        if (W > 0 && H > 0 && src && dst && src != dst)
+            OMR_HIP(ctx, hipMemcpyAsync(dst, src, sizeof(T) * (size_t)W * H, hipMemcpyDeviceToDevice, ctx->stream));
+        return OMR_OK;
+    }
+    if (!src) return fail(ctx, OMR_INVALID_ARGUMENT, "Attempted to flip null image");
+    if (W == 0 || H == 0) return fail(ctx, OMR_INVALID_ARGUMENT, "Attempted to flip image with 0 size");
+    if (W < 0 || H < 0 || !dst || src == dst) return fail(ctx, OMR_INVALID_ARGUMENT, "bad flip arguments");
+    const int64_t n = (int64_t)W * H;
+    const int grid = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, (int64_t)ctx->cu_count * 8);
+    hipLaunchKernelGGL(k_flip<T>, dim3(grid), dim3(kBlock), 0, ctx->stream, src, dst, W, H, fh ? 1 : 0, fv ? 1 : 0, n);
+    OMR_HIP(ctx, hipGetLastError());
+    return OMR_OK;
+}
+
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+omr_status omr_flip_argb_device(omr_ctx* ctx, const uint32_t* d_src, uint32_t* d_dest, int32_t size_x,
+                                int32_t size_y, int32_t flip_h, int32_t flip_v) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    return flip_device<uint32_t>(ctx, d_src, d_dest, size_x, size_y, flip_h, flip_v);
+}
+
+omr_status omr_flip_mask_device(omr_ctx* ctx, const uint8_t* d_src, uint8_t* d_dest, int32_t size_x,
+                                int32_t size_y, int32_t flip_h, int32_t flip_v) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    return flip_device<uint8_t>(ctx, d_src, d_dest, size_x, size_y, flip_h, flip_v);
+}
+
+omr_status omr_project_stack_device(omr_ctx* ctx, const void* d_stack, int32_t pixel_type,
+                                    int32_t big_endian_in, int32_t size_x, int32_t size_y,
+                                    int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
+                                    int32_t stepping, void* d_plane_out, int32_t big_endian_out) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = validate_projection(ctx, pixel_type, size_x, size_y, size_z, algorithm, start, end, stepping);
+    if (st) return st;
+    if (!d_stack || !d_plane_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack or output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const void* s[1] = {d_stack};
+    void* o[1] = {d_plane_out};
+    return enqueue_projection(ctx, s, o, 1, pixel_type, big_endian_in, size_x, size_y, algorithm, start,
+                              end, stepping, big_endian_out);
+}
+
+omr_status omr_project_stack(omr_ctx* ctx, const void* stack, int32_t pixel_type, int32_t big_endian_in,
+                             int32_t size_x, int32_t size_y, int32_t size_z, int32_t algorithm,
+                             int32_t start, int32_t end, int32_t stepping, void* plane_out,
+                             int32_t big_endian_out) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = validate_projection(ctx, pixel_type, size_x, size_y, size_z, algorithm, start, end, stepping);
+    if (st) return st;
+    if (!stack || !plane_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack or output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const int bpp = bytes_per_pixel(pixel_type);
+    const size_t plane = (size_t)size_x * size_y * bpp;
+    const size_t in_bytes = plane * size_z;
+    st = ensure_workspace(ctx, align_up(in_bytes, 256) + align_up(plane, 256));
+    if (st) return st;
+    uint8_t* d_in = static_cast<uint8_t*>(ctx->ws);
+    uint8_t* d_out = d_in + align_up(in_bytes, 256);
+    OMR_HIP(ctx, hipMemcpyAsync(d_in, stack, in_bytes, hipMemcpyHostToDevice, ctx->stream));
+    const void* s[1] = {d_in};
+    void* o[1] = {d_out};
+    st = enqueue_projection(ctx, s, o, 1, pixel_type, big_endian_in, size_x, size_y, algorithm, start, end,
+                            stepping, big_endian_out);
+    if (st) return st;
+    OMR_HIP(ctx, hipMemcpyAsync(plane_out, d_out, plane, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return OMR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,670 @@
+// omr_render.hip — K1 (per-request tables) and K2 (quantize + codomain + composite + flip).
+//
+// Replaces, per tile request:
+//   renderer.renderAsPackedInt(planeDef, null)   ImageRegionRequestHandler.java:559
+//     (upstream omeis Renderer: QuantumStrategy LUT, CodomainChain, HSB/GreyScale strategy)
+//   flip(buf, sizeX, sizeY, flipH, flipV)         ImageRegionRequestHandler.java:574-575, :616-642
+// Semantics: SEMANTICS TABLE in oracle/omr_oracle.c (the parity checker).
+//
+// Design:
+//  * K1 folds everything that depends only on the quantized value v — reverse intensity,
+//    channel colour or .lut table, greyscale — into a 256-entry table per active channel
+//    whose entries pack (r,g,b) contributions as 10-bit fields.  For 8-bit pixel types the
+//    quantization LUT is folded in as well (table indexed by the raw byte).
+//  * K2 streams the channel planes once (16 B per lane per channel), quantizes each pixel
+//    (16-bit linear: exact double evaluation of the LUT entry, no 64 KiB LUT gather;
+//    other families: byte LUT gather; float/32-bit: per-pixel double q(x)), sums the
+//    channel contributions from LDS with plain integer adds, clamps and packs ARGB, and
+//    writes it at the flipped position (the flip costs nothing).  HBM-bound.
+#include "omr_device.h"
+
+namespace omr {
+
+// ------------------------------------------------------------------------------- K1
+__device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey) {
+    const int vv = p.reverse ? ((cde - v + cds) & 0xFF) : v;
+    if (grey) return ((uint32_t)vv << 20) | ((uint32_t)vv << 10) | (uint32_t)vv;
+    uint32_t r, g, b;
+    if (p.has_lut) {
+        r = p.lut_rgb[vv]; g = p.lut_rgb[256 + vv]; b = p.lut_rgb[512 + vv];
+    } else {
+        r = (uint32_t)(int)(p.ratio[0] * (float)vv);
+        g = (uint32_t)(int)(p.ratio[1] * (float)vv);
+        b = (uint32_t)(int)(p.ratio[2] * (float)vv);
+    }
+    return (r << 20) | (g << 10) | b;
+}
+
+// grid: n_active blocks x 256 threads.  Table8 channels are indexed by the raw byte.
+__global__ void __launch_bounds__(256) k_build_contrib(const RenderPlan* __restrict__ plan,
+                                                       uint32_t* __restrict__ contrib, int is_signed8) {
+    const int a = blockIdx.x;
+    const ChanParam& p = plan->ch[a];
+    const int t = threadIdx.x;
+    const int cds = plan->cd_start, cde = plan->cd_end;
+    uint32_t e;
+    if (p.mode == kModeTable8) {
+        const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
+        if (value < p.gmin || value > p.gmax) {
+            e = kErrBit;
+        } else {
+            const int v = quantize_eval((double)value, p, cds, cde);
+            e = pack_contrib(p, v, cds, cde, plan->greyscale);
+        }
+    } else {
+        e = pack_contrib(p, t, cds, cde, plan->greyscale);
+    }
+    contrib[a * 256 + t] = e;
+}
+
+// grid: (ceil(n/256), n_active); builds the byte LUT of every kModeLut16 channel.
+__global__ void __launch_bounds__(256) k_build_lut(const RenderPlan* __restrict__ plan,
+                                                   uint8_t* __restrict__ ws_base) {
+    const ChanParam& p = plan->ch[blockIdx.y];
+    if (p.mode != kModeLut16) return;
+    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        ws_base[p.lut_off + i] = (uint8_t)quantize_eval((double)(p.gmin + i), p, plan->cd_start, plan->cd_end);
+}
+
+// ------------------------------------------------------------------------------- K2
+struct K2Args {
+    const RenderPlan* plan;
+    const void* const* planes;  // [n_tiles][size_c]
+    const uint8_t* ws_base;     // quantization LUTs live here (ChanParam::lut_off)
+    const uint32_t* contrib;    // [n_active][256]
+    uint32_t* out;              // [n_tiles][H][W]
+    int32_t* status;            // optional per-tile status
+    int32_t* flag;              // sticky error word
+    int64_t row_stride;         // pixels
+    int32_t size_c, n_tiles, width, height;
+    int32_t flip_h, flip_v;
+    uint32_t total;             // work items (chunks of VEC pixels)
+    FastDiv cpt, cpr;           // chunks per tile, chunks per row
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Raw chunk of VEC pixels of BPP bytes.
+template <int BPP, int VEC>
+struct Chunk {
+    static constexpr int kBytes = BPP * VEC;
+    static constexpr int kDw = kBytes >= 4 ? kBytes / 4 : 1;
+    uint32_t dw[kDw];
+};
+
+template <int BPP, int VEC>
+__device__ __forceinline__ void load_chunk(Chunk<BPP, VEC>& c, const uint8_t* p) {
+    constexpr int B = BPP * VEC;
+    if constexpr (B == 16) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        c.dw[0] = v[0]; c.dw[1] = v[1]; c.dw[2] = v[2]; c.dw[3] = v[3];
+    } else if constexpr (B == 8) {
+        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+        c.dw[0] = v[0]; c.dw[1] = v[1];
+    } else if constexpr (B == 4) {
+        c.dw[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else if constexpr (B == 2) {
+        c.dw[0] = *reinterpret_cast<const uint16_t*>(p);
+    } else {
+        c.dw[0] = *p;
+    }
+}
+
+// Integer value of pixel j (8/16-bit types).
+template <int BPP, int VEC, bool BE, bool SIGNED>
+__device__ __forceinline__ int pixel_int(const Chunk<BPP, VEC>& c, int j) {
+    if constexpr (BPP == 1) {
+        const uint32_t b = (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
+        return SIGNED ? (int)(int8_t)b : (int)b;
+    } else {
+        uint32_t d = c.dw[j >> 1];
+        if constexpr (BE) d = bswap16x2(d);
+        const uint32_t h = (j & 1) ? (d >> 16) : (d & 0xFFFF);
+        return SIGNED ? (int)(int16_t)h : (int)h;
+    }
+}
+
+// Raw byte index of pixel j (8-bit types: contrib table index).
+template <int VEC, bool SIGNED>
+__device__ __forceinline__ uint32_t byte_index(const Chunk<1, VEC>& c, int j) {
+    const uint32_t b = (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
+    return SIGNED ? (b ^ 0x80u) : b;
+}
+
+// Double value of pixel j (32/64-bit types).
+template <int BPP, int VEC, bool BE, int PT>
+__device__ __forceinline__ double pixel_double(const Chunk<BPP, VEC>& c, int j) {
+    if constexpr (BPP == 4) {
+        uint32_t d = c.dw[j];
+        if constexpr (BE) d = bswap32(d);
+        if constexpr (PT == OMR_PIXELS_FLOAT) return (double)__uint_as_float(d);
+        else if constexpr (PT == OMR_PIXELS_INT32) return (double)(int32_t)d;
+        else return (double)d;
+    } else {
+        uint32_t lo = c.dw[2 * j], hi = c.dw[2 * j + 1];
+        if constexpr (BE) { const uint32_t t = bswap32(lo); lo = bswap32(hi); hi = t; }
+        return __hiloint2double((int)hi, (int)lo);
+    }
+}
+
+__device__ __forceinline__ uint32_t clamp_fields(uint32_t a) {
+    const uint32_t r = min(a >> 20, 255u), g = min((a >> 10) & 1023u, 255u), b = min(a & 1023u, 255u);
+    return (r << 20) | (g << 10) | b;
+}
+
+// Quantized value of a 16-bit pixel: exact LUT entry (linear) or LUT gather.
+__device__ __forceinline__ uint32_t quant16(int x, const ChanParam& p, const uint8_t* ws_base,
+                                            int cds8, int cde8, int cds, bool& err) {
+    if (x < p.gmin || x > p.gmax) { err = true; return 0; }
+    if (p.mode == kModeLut16) return ws_base[p.lut_off + (uint32_t)(x - p.gmin)];
+    if (x < p.lo) return (uint32_t)cds8;
+    if (x >= p.hi) return (uint32_t)cde8;
+    const double d = p.a0 * ((double)x - p.ws);
+    int v = (d == 0x1.fffffffffffffp-2) ? 0 : (int)floor(d + 0.5);
+    if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);
+    return (uint32_t)v & 0xFFu;
+}
+
+// NA > 0: fixed active-channel count (fully unrolled, all loads issued up front).
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA>
+__global__ void __launch_bounds__(kBlock) k_render(K2Args A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
+    const RenderPlan* __restrict__ plan = A.plan;
+    const int na = NA > 0 ? NA : plan->n_active;
+    for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.contrib[i];
+    __syncthreads();
+    const int cds = plan->cd_start, cds8 = plan->cd_start & 0xFF, cde8 = plan->cd_end & 0xFF;
+    const int W = A.width, H = A.height;
+    const uint32_t cpr = A.cpr.d;
+    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < A.total; g += gridDim.x * kBlock) {
+        const uint32_t tile = fdiv(g, A.cpt);
+        const uint32_t rem = g - tile * A.cpt.d;
+        const uint32_t row = fdiv(rem, A.cpr);
+        const uint32_t cc = rem - row * cpr;
+        const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
+        uint32_t acc[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) acc[j] = 0;
+        uint32_t err_bits = 0;
+        bool err = false;
+        constexpr int NL = NA > 0 ? NA : 1;
+        Chunk<BPP, VEC> ck[NL];
+        if constexpr (NA > 0) {
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const uint8_t* base = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + plan->ch[a].index]);
+                load_chunk<BPP, VEC>(ck[a], base + in_off);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < na; ++a) {
+            const ChanParam& p = plan->ch[a];
+            Chunk<BPP, VEC>& c = ck[NA > 0 ? a : 0];
+            if constexpr (NA == 0) {
+                const uint8_t* base = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + p.index]);
+                load_chunk<BPP, VEC>(c, base + in_off);
+            }
+            const uint32_t* tab = s_contrib + a * 256;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) {
+                uint32_t e;
+                if constexpr (BPP == 1) {
+                    e = tab[byte_index<VEC, SIGNED>(c, j)];
+                    err_bits |= e;
+                    e &= ~kErrBit;
+                } else if constexpr (BPP == 2) {
+                    const int x = pixel_int<BPP, VEC, BE, SIGNED>(c, j);
+                    e = tab[quant16(x, p, A.ws_base, cds8, cde8, cds, err)];
+                } else {
+                    const double x = pixel_double<BPP, VEC, BE, PT>(c, j);
+                    e = tab[quantize_eval(x, p, plan->cd_start, plan->cd_end)];
+                }
+                acc[j] += e;
+                if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
+            }
+        }
+        if ((err_bits & kErrBit) || err) {
+            atomicOr(A.flag, 1);
+            if (A.status) A.status[tile] = OMR_QUANTIZATION;
+        }
+        uint32_t px[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            const uint32_t c = clamp_fields(acc[j]);
+            px[j] = 0xFF000000u | ((c >> 4) & 0xFF0000u) | ((c >> 2) & 0xFF00u) | (c & 0xFFu);
+        }
+        const uint32_t orow = A.flip_v ? (uint32_t)H - 1 - row : row;
+        const uint32_t ocol = A.flip_h ? (uint32_t)W - (cc + 1) * VEC : cc * VEC;
+        uint32_t* o = A.out + (int64_t)tile * W * H + (int64_t)orow * W + ocol;
+        if (A.flip_h) {
+#pragma unroll
+            for (int j = 0; j < VEC / 2; ++j) { const uint32_t t = px[j]; px[j] = px[VEC - 1 - j]; px[VEC - 1 - j] = t; }
+        }
+        if constexpr (VEC % 4 == 0) {
+#pragma unroll
+            for (int j = 0; j < VEC; j += 4)
+                *reinterpret_cast<uint4*>(o + j) = make_uint4(px[j], px[j + 1], px[j + 2], px[j + 3]);
+        } else if constexpr (VEC == 2) {
+            *reinterpret_cast<uint2*>(o) = make_uint2(px[0], px[1]);
+        } else {
+            o[0] = px[0];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------- host side
+struct PreparedPlan {
+    RenderPlan plan;
+    size_t plan_bytes = 0;
+    int n_lut = 0;
+    size_t lut_bytes = 0;
+};
+
+static double host_family_map(int family, double x, double k) {
+    switch (family) {
+    case OMR_FAMILY_POLYNOMIAL: return pow(x, k);
+    case OMR_FAMILY_LOGARITHMIC: return x > 0 ? log(x) : 0.0;
+    case OMR_FAMILY_EXPONENTIAL: return exp(pow(x, k));
+    default: return x;
+    }
+}
+
+static int32_t ceil_to_i32(double v) {
+    if (v != v) return INT32_MIN;
+    const double c = ceil(v);
+    if (c <= -2147483647.0) return -2147483647;
+    if (c >= 2147483647.0) return 2147483647;
+    return (int32_t)c;
+}
+
+static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch,
+                               int32_t size_c, int32_t pixel_type, PreparedPlan& pp) {
+    if (!q) return fail(ctx, OMR_INVALID_ARGUMENT, "null quantum def");
+    if (size_c < 0 || (size_c > 0 && !ch)) return fail(ctx, OMR_INVALID_ARGUMENT, "bad channel bindings");
+    if (q->bit_resolution <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "bit resolution must be > 0");
+    if (q->model != OMR_MODEL_GREYSCALE && q->model != OMR_MODEL_RGB)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "unknown rendering model");
+    const int bpp = bytes_per_pixel(pixel_type);
+    if (!bpp) return fail(ctx, OMR_INVALID_ARGUMENT, "unsupported pixel type");
+    RenderPlan& P = pp.plan;
+    std::memset(&P, 0, sizeof(P));
+    P.cd_start = q->cd_start;
+    P.cd_end = q->cd_end;
+    P.greyscale = q->model == OMR_MODEL_GREYSCALE;
+    int na = 0;
+    size_t lut_off = 0;
+    for (int c = 0; c < size_c; ++c) {
+        if (!ch[c].active) continue;
+        if (P.greyscale && na == 1) break;   // GreyScaleStrategy renders the first active channel (S8)
+        if (na == kMaxActive) return fail(ctx, OMR_INVALID_ARGUMENT, "more than 32 active channels");
+        const omr_channel_binding& b = ch[c];
+        if (b.family < OMR_FAMILY_LINEAR || b.family > OMR_FAMILY_EXPONENTIAL)
+            return fail(ctx, OMR_INVALID_ARGUMENT, "unknown family");
+        ChanParam& p = P.ch[na];
+        p.index = c;
+        p.family = b.family;
+        p.nr = b.noise_reduction != 0;
+        p.reverse = b.reverse != 0;
+        p.has_lut = b.lut != nullptr;
+        if (b.lut) std::memcpy(p.lut_rgb, b.lut, 768);
+        p.ws = b.input_start;
+        p.we = b.input_end;
+        p.k = b.coefficient;
+        p.ys = host_family_map(b.family, p.ws, p.k);
+        const double ye = host_family_map(b.family, p.we, p.k);
+        p.a0 = (double)q->bit_resolution / (ye - p.ys);
+        p.a1 = (double)(q->cd_end - q->cd_start) / (double)q->bit_resolution;
+        p.dec = (p.we - p.ws) / 10.0;
+        p.second = !(p.a1 == 1.0 && q->cd_start == 0);
+        p.lo = ceil_to_i32(p.ws);
+        p.hi = ceil_to_i32(p.we);
+        if (p.we != p.we) p.hi = INT32_MAX;
+        const float alpha = (float)b.rgba[3] / 255.0f;
+        for (int k = 0; k < 3; ++k) p.ratio[k] = ((float)b.rgba[k] / 255.0f) * alpha;
+        if (bpp <= 2) {
+            const double gmin = std::trunc(b.global_min), gmax = std::trunc(b.global_max);
+            if (!(gmin == gmin) || !(gmax == gmax) || gmax < gmin || gmin < -2147483648.0 || gmax > 2147483647.0)
+                return fail(ctx, OMR_INVALID_ARGUMENT, "bad LUT domain (global min/max)");
+            p.gmin = (int32_t)gmin;
+            p.gmax = (int32_t)gmax;
+            if (bpp == 1) {
+                p.mode = kModeTable8;
+            } else {
+                const bool fast = b.family == OMR_FAMILY_LINEAR && !p.nr && std::isfinite(p.ws) &&
+                                  std::isfinite(p.a0) && std::fabs(p.a0) < 1e300 && !p.second &&
+                                  q->bit_resolution <= 65535;
+                const bool fast2 = b.family == OMR_FAMILY_LINEAR && !p.nr && std::isfinite(p.ws) &&
+                                   std::isfinite(p.a0) && std::fabs(p.a0) < 1e300 && std::isfinite(p.a1) &&
+                                   q->bit_resolution <= 65535;
+                p.mode = (fast || fast2) ? kModeLinear16 : kModeLut16;
+                if (p.mode == kModeLut16) {
+                    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
+                    if (n > (1 << 24)) return fail(ctx, OMR_INVALID_ARGUMENT, "LUT domain too large");
+                    p.lut_off = lut_off;
+                    lut_off += align_up((size_t)n, 256);
+                    pp.n_lut++;
+                }
+            }
+        } else {
+            p.mode = kModeEval;
+            p.gmin = INT32_MIN;
+            p.gmax = INT32_MAX;
+        }
+        ++na;
+    }
+    P.n_active = na;
+    pp.plan_bytes = offsetof(RenderPlan, ch) + sizeof(ChanParam) * (size_t)(na > 0 ? na : 1);
+    pp.lut_bytes = lut_off;
+    return OMR_OK;
+}
+
+// Workspace layout for one render launch: [plan][contrib][luts][extra...]
+struct RenderLayout {
+    size_t plan_off = 0, contrib_off = 0, lut_off = 0, extra_off = 0, total = 0;
+};
+
+static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
+    RenderLayout L;
+    L.plan_off = 0;
+    L.contrib_off = align_up(sizeof(RenderPlan), 256);
+    L.lut_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
+    L.extra_off = L.lut_off + align_up(pp.lut_bytes, 256);
+    L.total = L.extra_off + extra;
+    return L;
+}
+
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT>
+static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_t s) {
+    const size_t lds = (size_t)(na > 0 ? na : 1) * 256 * 4;
+    switch (na) {
+    case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    default: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 0>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+template <int BPP, int VEC, bool BE>
+static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int grid, hipStream_t s) {
+    if constexpr (BPP == 1) {
+        return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8>(a, na, grid, s)
+                                     : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8>(a, na, grid, s);
+    } else if constexpr (BPP == 2) {
+        return pt == OMR_PIXELS_INT16 ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16>(a, na, grid, s)
+                                      : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16>(a, na, grid, s);
+    } else if constexpr (BPP == 4) {
+        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT>(a, na, grid, s);
+        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32>(a, na, grid, s);
+        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32>(a, na, grid, s);
+    } else {
+        return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE>(a, na, grid, s);
+    }
+}
+
+template <int BPP, int VEC>
+static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int grid, hipStream_t s) {
+    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, grid, s) : launch_render_pt<BPP, VEC, false>(a, pt, na, grid, s);
+}
+
+// Enqueue K1 + K2 for a batch whose plane pointer table is already on the device.
+static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type, int32_t big_endian,
+                                 const void* const* d_plane_ptrs, int32_t size_c, int32_t n_tiles,
+                                 int64_t row_stride, int32_t width, int32_t height, int32_t flip_h,
+                                 int32_t flip_v, uint32_t* d_out, int32_t* d_status, bool aligned,
+                                 const RenderLayout& L) {
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
+    uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
+    uint8_t* d_luts = ws + L.lut_off;
+    // LUT offsets are relative to the LUT region; make them workspace-relative for K2.
+    for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off += L.lut_off;
+    omr_status st = stage_h2d(ctx, d_plan, &pp.plan, pp.plan_bytes);
+    for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off -= L.lut_off;
+    if (st != OMR_OK) return st;
+    const int na = pp.plan.n_active;
+    if (na > 0) {
+        hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
+                           pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
+        OMR_HIP(ctx, hipGetLastError());
+        if (pp.n_lut > 0) {
+            hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan, ws);
+            OMR_HIP(ctx, hipGetLastError());
+        }
+    }
+    (void)d_luts;
+    const int bpp = bytes_per_pixel(pixel_type);
+    const int vec = aligned ? (bpp <= 2 ? 8 : 16 / bpp) : 1;
+    const uint64_t cpr = (uint64_t)width / vec;
+    const uint64_t cpt = cpr * (uint64_t)height;
+    const uint64_t total = cpt * (uint64_t)n_tiles;
+    if (total == 0) return OMR_OK;
+    if (total >= (1ull << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "batch too large for one launch");
+    K2Args a;
+    a.plan = d_plan;
+    a.planes = d_plane_ptrs;
+    a.ws_base = ws;
+    a.contrib = d_contrib;
+    a.out = d_out;
+    a.status = d_status;
+    a.flag = ctx->d_flag;
+    a.row_stride = row_stride;
+    a.size_c = size_c;
+    a.n_tiles = n_tiles;
+    a.width = width;
+    a.height = height;
+    a.flip_h = flip_h ? 1 : 0;
+    a.flip_v = flip_v ? 1 : 0;
+    a.total = (uint32_t)total;
+    a.cpt = make_fastdiv((uint32_t)cpt);
+    a.cpr = make_fastdiv((uint32_t)cpr);
+    const uint64_t blocks_needed = (total + kBlock - 1) / kBlock;
+    const int grid = (int)std::min<uint64_t>(blocks_needed, (uint64_t)ctx->cu_count * 8);
+    hipError_t e;
+    const bool be = big_endian != 0;
+    KernelTimer timer(ctx, 2);
+    if (aligned) {
+        switch (bpp) {
+        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, grid, ctx->stream); break;
+        }
+    } else {
+        switch (bpp) {
+        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
+        }
+    }
+    OMR_HIP(ctx, e);
+    return OMR_OK;
+}
+
+static bool vec_aligned(int bpp, int32_t width, int64_t row_stride) {
+    const int vec = bpp <= 2 ? 8 : 16 / bpp;
+    return width % vec == 0 && row_stride % vec == 0;
+}
+
+static omr_status check_dims(Ctx* ctx, int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                             int64_t& row_stride) {
+    if (width < 0 || height < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "negative region size");
+    if ((flip_h || flip_v) && (width == 0 || height == 0))
+        return fail(ctx, OMR_INVALID_ARGUMENT, "Attempted to flip image with 0 size");
+    if (row_stride == 0) row_stride = width;
+    if (row_stride < width) return fail(ctx, OMR_INVALID_ARGUMENT, "row stride smaller than width");
+    return OMR_OK;
+}
+
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+omr_status omr_render_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                   const omr_channel_binding* channels, int32_t size_c,
+                                   const void* const* d_plane_ptrs, int32_t n_tiles,
+                                   int64_t row_stride, int32_t pixel_type, int32_t big_endian,
+                                   int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                                   uint32_t* d_argb_out, int32_t* d_status) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (n_tiles < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "negative tile count");
+    omr_status st = check_dims(ctx, width, height, flip_h, flip_v, row_stride);
+    if (st) return st;
+    PreparedPlan pp;
+    st = prepare_plan(ctx, qdef, channels, size_c, pixel_type, pp);
+    if (st) return st;
+    if (n_tiles == 0 || width == 0 || height == 0) return OMR_OK;
+    if (pp.plan.n_active > 0 && !d_plane_ptrs) return fail(ctx, OMR_INVALID_ARGUMENT, "null plane table");
+    if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const RenderLayout L = layout_for(pp, 0);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    if (d_status) OMR_HIP(ctx, hipMemsetAsync(d_status, 0, sizeof(int32_t) * (size_t)n_tiles, ctx->stream));
+    const int bpp = bytes_per_pixel(pixel_type);
+    return enqueue_render(ctx, pp, pixel_type, big_endian, d_plane_ptrs, size_c, n_tiles, row_stride,
+                          width, height, flip_h, flip_v, d_argb_out, d_status,
+                          vec_aligned(bpp, width, row_stride), L);
+}
+
+omr_status omr_render_packed_int_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                        const omr_channel_binding* channels, int32_t size_c,
+                                        const void* const* d_planes, int64_t row_stride,
+                                        int32_t pixel_type, int32_t big_endian, int32_t width,
+                                        int32_t height, int32_t flip_h, int32_t flip_v,
+                                        uint32_t* d_argb_out) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = check_dims(ctx, width, height, flip_h, flip_v, row_stride);
+    if (st) return st;
+    PreparedPlan pp;
+    st = prepare_plan(ctx, qdef, channels, size_c, pixel_type, pp);
+    if (st) return st;
+    if (width == 0 || height == 0) return OMR_OK;
+    for (int a = 0; a < pp.plan.n_active; ++a)
+        if (!d_planes || !d_planes[pp.plan.ch[a].index]) return fail(ctx, OMR_INVALID_ARGUMENT, "null plane for active channel");
+    if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const size_t ptr_bytes = sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1);
+    const RenderLayout L = layout_for(pp, align_up(ptr_bytes, 256));
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    const void** d_ptrs = reinterpret_cast<const void**>(static_cast<uint8_t*>(ctx->ws) + L.extra_off);
+    std::vector<const void*> ptrs(size_c > 0 ? size_c : 1, nullptr);
+    for (int c = 0; c < size_c; ++c) ptrs[c] = d_planes ? d_planes[c] : nullptr;
+    st = stage_h2d(ctx, d_ptrs, ptrs.data(), ptr_bytes);
+    if (st) return st;
+    const int bpp = bytes_per_pixel(pixel_type);
+    bool aligned = vec_aligned(bpp, width, row_stride);
+    for (int c = 0; c < size_c && aligned; ++c)
+        if (ptrs[c] && (reinterpret_cast<uintptr_t>(ptrs[c]) % 16)) aligned = false;
+    if (reinterpret_cast<uintptr_t>(d_argb_out) % 16) aligned = false;
+    return enqueue_render(ctx, pp, pixel_type, big_endian, d_ptrs, size_c, 1, row_stride, width, height,
+                          flip_h, flip_v, d_argb_out, nullptr, aligned, L);
+}
+
+omr_status omr_render_packed_int(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                 const omr_channel_binding* channels, int32_t size_c,
+                                 const void* const* planes, int64_t row_stride, int32_t pixel_type,
+                                 int32_t big_endian, int32_t width, int32_t height, int32_t flip_h,
+                                 int32_t flip_v, uint32_t* argb_out) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = check_dims(ctx, width, height, flip_h, flip_v, row_stride);
+    if (st) return st;
+    PreparedPlan pp;
+    st = prepare_plan(ctx, qdef, channels, size_c, pixel_type, pp);
+    if (st) return st;
+    if (width == 0 || height == 0) return OMR_OK;
+    for (int a = 0; a < pp.plan.n_active; ++a)
+        if (!planes || !planes[pp.plan.ch[a].index]) return fail(ctx, OMR_INVALID_ARGUMENT, "null plane for active channel");
+    if (!argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const int bpp = bytes_per_pixel(pixel_type);
+    const size_t plane_bytes = align_up((size_t)width * height * bpp, 256);
+    const size_t out_bytes = align_up((size_t)width * height * 4, 256);
+    const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1), 256);
+    const int na = pp.plan.n_active;
+    const RenderLayout L = layout_for(pp, ptr_bytes + plane_bytes * (size_t)na + out_bytes);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    const void** d_ptrs = reinterpret_cast<const void**>(ws + L.extra_off);
+    uint8_t* d_planes = ws + L.extra_off + ptr_bytes;
+    uint32_t* d_out = reinterpret_cast<uint32_t*>(d_planes + plane_bytes * (size_t)na);
+    std::vector<const void*> ptrs(size_c > 0 ? size_c : 1, nullptr);
+    for (int a = 0; a < na; ++a) {
+        const int c = pp.plan.ch[a].index;
+        uint8_t* dst = d_planes + plane_bytes * (size_t)a;
+        ptrs[c] = dst;
+        OMR_HIP(ctx, hipMemcpy2DAsync(dst, (size_t)width * bpp, planes[c], (size_t)row_stride * bpp,
+                                      (size_t)width * bpp, height, hipMemcpyHostToDevice, ctx->stream));
+    }
+    st = stage_h2d(ctx, d_ptrs, ptrs.data(), sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1));
+    if (st) return st;
+    st = enqueue_render(ctx, pp, pixel_type, big_endian, d_ptrs, size_c, 1, width, width, height, flip_h,
+                        flip_v, d_out, nullptr, vec_aligned(bpp, width, width), L);
+    if (st) return st;
+    OMR_HIP(ctx, hipMemcpyAsync(argb_out, d_out, (size_t)width * height * 4, hipMemcpyDeviceToHost, ctx->stream));
+    return omr_ctx_synchronize(ctx);
+}
+
+}  // extern "C"
+
+extern "C" omr_status omr_render_projected_device(
+    omr_ctx* ctx, const omr_quantum_def* qdef, const omr_channel_binding* channels, int32_t size_c,
+    const void* const* d_stacks, int32_t pixel_type, int32_t big_endian, int32_t size_x, int32_t size_y,
+    int32_t size_z, int32_t algorithm, int32_t start, int32_t end, int32_t stepping, int32_t flip_h,
+    int32_t flip_v, uint32_t* d_argb_out) {
+    // ImageRegionRequestHandler.java:506-559: project every active channel (full plane, the
+    // tile/region is dropped, :556-557), then render the projected planes at z=0,t=0.
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = validate_projection_args(ctx, pixel_type, size_x, size_y, size_z, algorithm, start, end, stepping);
+    if (st) return st;
+    int64_t row_stride = size_x;
+    st = check_dims(ctx, size_x, size_y, flip_h, flip_v, row_stride);
+    if (st) return st;
+    PreparedPlan pp;
+    st = prepare_plan(ctx, qdef, channels, size_c, pixel_type, pp);
+    if (st) return st;
+    if (size_x == 0 || size_y == 0) return OMR_OK;
+    const int na = pp.plan.n_active;
+    for (int a = 0; a < na; ++a)
+        if (!d_stacks || !d_stacks[pp.plan.ch[a].index]) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack for active channel");
+    if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const int bpp = bytes_per_pixel(pixel_type);
+    const size_t plane_bytes = align_up((size_t)size_x * size_y * bpp, 256);
+    const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1), 256);
+    const RenderLayout L = layout_for(pp, ptr_bytes + plane_bytes * (size_t)na);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    const void** d_ptrs = reinterpret_cast<const void**>(ws + L.extra_off);
+    uint8_t* d_planes = ws + L.extra_off + ptr_bytes;
+    std::vector<const void*> ptrs(size_c > 0 ? size_c : 1, nullptr);
+    std::vector<const void*> srcs;
+    std::vector<void*> dsts;
+    for (int a = 0; a < na; ++a) {
+        const int c = pp.plan.ch[a].index;
+        uint8_t* dst = d_planes + plane_bytes * (size_t)a;
+        ptrs[c] = dst;
+        srcs.push_back(d_stacks[c]);
+        dsts.push_back(dst);
+    }
+    for (size_t i = 0; i < srcs.size(); i += 32) {
+        const int n = (int)std::min<size_t>(32, srcs.size() - i);
+        st = enqueue_projection(ctx, srcs.data() + i, dsts.data() + i, n, pixel_type, big_endian, size_x,
+                                size_y, algorithm, start, end, stepping, 0);
+        if (st) return st;
+    }
+    st = stage_h2d(ctx, d_ptrs, ptrs.data(), sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1));
+    if (st) return st;
+    const bool aligned = vec_aligned(bpp, size_x, size_x) && (reinterpret_cast<uintptr_t>(d_argb_out) % 16 == 0);
+    return enqueue_render(ctx, pp, pixel_type, 0, d_ptrs, size_c, 1, size_x, size_x, size_y, flip_h, flip_v,
+                          d_argb_out, nullptr, aligned, L);
+}

@@ -1,0 +1,18 @@
+"""omr — MI355X-native image-region rendering (Python side of the drop-in).
+
+Layers:
+  _lib      ctypes binding of libomr.so (the C ABI in include/omr/omr.h)
+  context   Context: one per worker thread / GPU (device, stream, workspace)
+  renderer  Renderer facade mirroring the omeis Renderer calls the reference makes
+            (ImageRegionRequestHandler.java:436-440, :689-741, :559)
+  request   ImageRegionCtx / ShapeMaskCtx parsing and the handler glue
+            (ImageRegionCtx.java, ImageRegionRequestHandler.java, ShapeMaskRequestHandler.java)
+"""
+from . import _lib
+from ._lib import OmrError
+from .context import Context
+from .renderer import (ChannelSettings, Renderer, ReverseIntensityContext, create_rendering_def,
+                       flip, split_html_color)
+
+__all__ = ["_lib", "OmrError", "Context", "Renderer", "ChannelSettings", "ReverseIntensityContext",
+           "create_rendering_def", "flip", "split_html_color"]

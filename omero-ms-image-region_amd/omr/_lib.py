@@ -1,0 +1,134 @@
+"""ctypes binding of libomr.so (include/omr/omr.h).
+
+This is the ONLY way Python reaches the product path; there is no CPU fallback.
+If libomr.so is missing, importing this module raises immediately.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libomr.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libomr.so not found at {LIB_PATH}: build it with `make -C omero-ms-image-region_amd` "
+        "(or __graft_entry__.build()); there is no fallback path")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+# ---- enums (omr.h) ----------------------------------------------------------------------
+OK, INVALID_ARGUMENT, NOT_FOUND, QUANTIZATION, DEVICE, OOM, BUFFER_TOO_SMALL = range(7)
+STATUS_NAMES = {0: "OK", 1: "INVALID_ARGUMENT", 2: "NOT_FOUND", 3: "QUANTIZATION", 4: "DEVICE",
+                5: "OOM", 6: "BUFFER_TOO_SMALL"}
+PIXELS_INT8, PIXELS_UINT8, PIXELS_INT16, PIXELS_UINT16, PIXELS_INT32, PIXELS_UINT32, \
+    PIXELS_FLOAT, PIXELS_DOUBLE = range(8)
+FAMILY_LINEAR, FAMILY_POLYNOMIAL, FAMILY_LOGARITHMIC, FAMILY_EXPONENTIAL = range(4)
+MODEL_GREYSCALE, MODEL_RGB = 0, 1
+PROJECTION_MAX, PROJECTION_MEAN, PROJECTION_SUM = 0, 1, 2
+
+PIXEL_TYPE_NAMES = {"int8": PIXELS_INT8, "uint8": PIXELS_UINT8, "int16": PIXELS_INT16,
+                    "uint16": PIXELS_UINT16, "int32": PIXELS_INT32, "uint32": PIXELS_UINT32,
+                    "float": PIXELS_FLOAT, "double": PIXELS_DOUBLE}
+BYTES_PER_PIXEL = {PIXELS_INT8: 1, PIXELS_UINT8: 1, PIXELS_INT16: 2, PIXELS_UINT16: 2,
+                   PIXELS_INT32: 4, PIXELS_UINT32: 4, PIXELS_FLOAT: 4, PIXELS_DOUBLE: 8}
+
+
+class QuantumDef(ctypes.Structure):
+    _fields_ = [("cd_start", ctypes.c_int32), ("cd_end", ctypes.c_int32),
+                ("bit_resolution", ctypes.c_int32), ("model", ctypes.c_int32)]
+
+
+class ChannelBinding(ctypes.Structure):
+    _fields_ = [("active", ctypes.c_int32), ("family", ctypes.c_int32),
+                ("coefficient", ctypes.c_double), ("noise_reduction", ctypes.c_int32),
+                ("reverse", ctypes.c_int32), ("input_start", ctypes.c_double),
+                ("input_end", ctypes.c_double), ("global_min", ctypes.c_double),
+                ("global_max", ctypes.c_double), ("rgba", ctypes.c_uint8 * 4),
+                ("lut", ctypes.POINTER(ctypes.c_uint8))]
+
+
+class Region(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_sz = ctypes.c_size_t
+_f32 = ctypes.c_float
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_QD = ctypes.POINTER(QuantumDef)
+_CB = ctypes.POINTER(ChannelBinding)
+
+_SIGS = {
+    "omr_abi_version": (_i32, []),
+    "omr_ctx_create": (_i32, [_i32, ctypes.POINTER(_vp)]),
+    "omr_ctx_destroy": (None, [_vp]),
+    "omr_last_error": (ctypes.c_char_p, [_vp]),
+    "omr_ctx_synchronize": (_i32, [_vp]),
+    "omr_ctx_set_stream": (_i32, [_vp, _vp]),
+    "omr_ctx_get_stream": (_vp, [_vp]),
+    "omr_ctx_enable_kernel_timing": (_i32, [_vp, _i32]),
+    "omr_ctx_kernel_timings": (_i32, [_vp, _vp, _vp, _i32]),
+    "omr_pinned_alloc": (_vp, [_vp, _sz]),
+    "omr_pinned_free": (None, [_vp, _vp]),
+    "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
+                                     _i32, _vp]),
+    "omr_render_packed_int_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32,
+                                            _i32, _i32, _vp]),
+    "omr_render_batch_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _i32,
+                                       _i32, _i32, _vp, _vp]),
+    "omr_flip_argb_device": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32]),
+    "omr_flip_mask_device": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32]),
+    "omr_project_stack": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                 _vp, _i32]),
+    "omr_project_stack_device": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                        _i32, _vp, _i32]),
+    "omr_render_projected_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32,
+                                           _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "omr_jpeg_max_bytes": (_sz, [_i32, _i32]),
+    "omr_png_max_bytes": (_sz, [_i32, _i32, _i32]),
+    "omr_encode_jpeg": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_encode_jpeg_device": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_jpeg_quant_tables": (_i32, [_f32, _vp, _vp]),
+    "omr_encode_png": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_encode_png_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_render_shape_mask_png": (_i32, [_vp, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp, _sz,
+                                         ctypes.POINTER(_sz)]),
+    "omr_split_html_color": (_i32, [ctypes.c_char_p, ctypes.POINTER(_i32)]),
+    "omr_shape_mask_fill_color": (_i32, [_i32, _i32, ctypes.c_char_p, _vp]),
+    "omr_get_region_def": (_i32, [_i32, ctypes.POINTER(Region), _i32, ctypes.POINTER(_i32), _i32,
+                                  _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(Region)]),
+    "omr_resolution_level": (_i32, [_i32, _i32]),
+    "omr_check_plane_def": (_i32, [ctypes.POINTER(Region), _i32, _i32]),
+    "omr_parse_lut": (_i32, [_vp, _sz, _vp]),
+}
+
+MISSING = []
+for _name, (_res, _args) in _SIGS.items():
+    try:
+        _fn = getattr(lib, _name)
+    except AttributeError:
+        MISSING.append(_name)
+        continue
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = [n for n in _SIGS if n not in MISSING]
+
+
+class OmrError(RuntimeError):
+    def __init__(self, status, message=""):
+        self.status = status
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+
+
+def check(status, ctx=None):
+    if status != OK:
+        msg = ""
+        if ctx is not None:
+            raw = lib.omr_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise OmrError(status, msg)
+    return status

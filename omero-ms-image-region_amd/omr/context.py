@@ -1,0 +1,221 @@
+"""Context: Python handle on one omr_ctx (device + stream + workspace).
+
+Host arrays are numpy; device buffers are torch tensors on the context's GPU (torch is
+only used as the device-memory allocator — all compute runs in libomr.so kernels).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import lib, check
+
+
+def _ptr(a):
+    """Address of a numpy array, torch tensor, bytes-like or int."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    raise TypeError(f"cannot take the address of {type(a)}")
+
+
+def make_bindings(channels):
+    """ChannelBinding[] from a list of dicts / ChannelSettings; keeps LUT buffers alive."""
+    n = len(channels)
+    arr = (_lib.ChannelBinding * max(n, 1))()
+    keep = []
+    for i, ch in enumerate(channels):
+        d = ch if isinstance(ch, dict) else ch.as_dict()
+        b = arr[i]
+        b.active = int(bool(d.get("active", True)))
+        b.family = int(d.get("family", _lib.FAMILY_LINEAR))
+        b.coefficient = float(d.get("coefficient", 1.0))
+        b.noise_reduction = int(bool(d.get("noise_reduction", False)))
+        b.reverse = int(bool(d.get("reverse", False)))
+        b.input_start = float(d["input_start"])
+        b.input_end = float(d["input_end"])
+        b.global_min = float(d.get("global_min", 0.0))
+        b.global_max = float(d.get("global_max", 0.0))
+        rgba = d.get("rgba", (255, 0, 0, 255))
+        for k in range(4):
+            b.rgba[k] = int(rgba[k])
+        lut = d.get("lut")
+        if lut is not None:
+            buf = np.ascontiguousarray(np.asarray(lut, dtype=np.uint8).reshape(768))
+            keep.append(buf)
+            b.lut = buf.ctypes.data_as(_lib._u8p)
+        else:
+            b.lut = None
+    return arr, keep
+
+
+def make_qdef(model, cd_start=0, cd_end=255, bit_resolution=255):
+    q = _lib.QuantumDef()
+    q.cd_start, q.cd_end, q.bit_resolution = cd_start, cd_end, bit_resolution
+    q.model = _lib.MODEL_RGB if model in (_lib.MODEL_RGB, "rgb", "c") else _lib.MODEL_GREYSCALE
+    return q
+
+
+class Context:
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        st = lib.omr_ctx_create(int(device), ctypes.byref(h))
+        if st != _lib.OK:
+            raise _lib.OmrError(st, f"omr_ctx_create(device={device}) failed")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib.omr_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def stream(self):
+        return lib.omr_ctx_get_stream(self.h)
+
+    def set_stream(self, stream_ptr):
+        check(lib.omr_ctx_set_stream(self.h, stream_ptr), self.h)
+
+    def synchronize(self):
+        check(lib.omr_ctx_synchronize(self.h), self.h)
+
+    def enable_kernel_timing(self, enable=True):
+        check(lib.omr_ctx_enable_kernel_timing(self.h, int(enable)), self.h)
+
+    def kernel_timings(self, cap=1 << 16):
+        """[(ms, kind)] of the timed hot-kernel launches since the last call (kind 2 render,
+        3 projection, 4 jpeg); synchronises the stream."""
+        ms = np.zeros(cap, np.float32)
+        kind = np.zeros(cap, np.int32)
+        n = lib.omr_ctx_kernel_timings(self.h, ms.ctypes.data, kind.ctypes.data, cap)
+        if n < 0:
+            raise _lib.OmrError(_lib.DEVICE, "kernel timing query failed")
+        return list(zip(ms[:n].tolist(), kind[:n].tolist()))
+
+    def last_error(self):
+        raw = lib.omr_last_error(self.h)
+        return raw.decode() if raw else ""
+
+    # ---- render -----------------------------------------------------------------------
+    def render_packed_int(self, qdef, channels, planes, pixel_type, width, height,
+                          big_endian=False, flip_h=False, flip_v=False, row_stride=0):
+        arr, keep = make_bindings(channels)
+        ptrs = (ctypes.c_void_p * max(len(planes), 1))(*[_ptr(p) for p in planes])
+        out = np.empty((height, width), dtype=np.uint32)
+        check(lib.omr_render_packed_int(self.h, ctypes.byref(qdef), arr, len(channels), ptrs,
+                                        row_stride, pixel_type, int(big_endian), width, height,
+                                        int(flip_h), int(flip_v), out.ctypes.data), self.h)
+        return out
+
+    def render_packed_int_device(self, qdef, channels, planes, pixel_type, width, height, out,
+                                 big_endian=False, flip_h=False, flip_v=False, row_stride=0):
+        arr, keep = make_bindings(channels)
+        ptrs = (ctypes.c_void_p * max(len(planes), 1))(*[_ptr(p) for p in planes])
+        check(lib.omr_render_packed_int_device(self.h, ctypes.byref(qdef), arr, len(channels),
+                                               ptrs, row_stride, pixel_type, int(big_endian),
+                                               width, height, int(flip_h), int(flip_v),
+                                               _ptr(out)), self.h)
+        return out
+
+    def render_batch_device(self, qdef, channels, d_plane_ptrs, n_tiles, pixel_type, width, height,
+                            out, status=None, big_endian=False, flip_h=False, flip_v=False,
+                            row_stride=0, bindings=None):
+        if bindings is None:
+            bindings = make_bindings(channels)
+        arr, keep = bindings
+        check(lib.omr_render_batch_device(self.h, ctypes.byref(qdef), arr, len(channels),
+                                          _ptr(d_plane_ptrs), n_tiles, row_stride, pixel_type,
+                                          int(big_endian), width, height, int(flip_h),
+                                          int(flip_v), _ptr(out), _ptr(status)), self.h)
+        return out
+
+    def flip_argb_device(self, src, dst, width, height, flip_h, flip_v):
+        check(lib.omr_flip_argb_device(self.h, _ptr(src), _ptr(dst), width, height, int(flip_h),
+                                       int(flip_v)), self.h)
+
+    def flip_mask_device(self, src, dst, width, height, flip_h, flip_v):
+        check(lib.omr_flip_mask_device(self.h, _ptr(src), _ptr(dst), width, height, int(flip_h),
+                                       int(flip_v)), self.h)
+
+    # ---- projection --------------------------------------------------------------------
+    def project_stack(self, stack, pixel_type, size_x, size_y, size_z, algorithm, start, end,
+                      stepping=1, big_endian_in=False, big_endian_out=False):
+        bpp = _lib.BYTES_PER_PIXEL[pixel_type]
+        out = np.empty(size_x * size_y * bpp, dtype=np.uint8)
+        check(lib.omr_project_stack(self.h, _ptr(stack), pixel_type, int(big_endian_in), size_x,
+                                    size_y, size_z, algorithm, start, end, stepping,
+                                    out.ctypes.data, int(big_endian_out)), self.h)
+        return out
+
+    def project_stack_device(self, stack, pixel_type, size_x, size_y, size_z, algorithm, start,
+                             end, out, stepping=1, big_endian_in=False, big_endian_out=False):
+        check(lib.omr_project_stack_device(self.h, _ptr(stack), pixel_type, int(big_endian_in),
+                                           size_x, size_y, size_z, algorithm, start, end,
+                                           stepping, _ptr(out), int(big_endian_out)), self.h)
+        return out
+
+    def render_projected_device(self, qdef, channels, stacks, pixel_type, size_x, size_y, size_z,
+                                algorithm, start, end, out, stepping=1, big_endian=False,
+                                flip_h=False, flip_v=False):
+        arr, keep = make_bindings(channels)
+        ptrs = (ctypes.c_void_p * max(len(stacks), 1))(*[_ptr(s) for s in stacks])
+        check(lib.omr_render_projected_device(self.h, ctypes.byref(qdef), arr, len(channels), ptrs,
+                                              pixel_type, int(big_endian), size_x, size_y, size_z,
+                                              algorithm, start, end, stepping, int(flip_h),
+                                              int(flip_v), _ptr(out)), self.h)
+        return out
+
+    # ---- encode ------------------------------------------------------------------------
+    def _encode(self, fn, src, *args, cap):
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_size_t(0)
+        check(fn(self.h, _ptr(src), *args, out.ctypes.data, cap, ctypes.byref(n)), self.h)
+        return out[:n.value].tobytes()
+
+    def encode_jpeg(self, argb, width, height, quality):
+        argb = np.ascontiguousarray(argb, dtype=np.uint32)
+        return self._encode(lib.omr_encode_jpeg, argb, width, height, float(quality),
+                            cap=lib.omr_jpeg_max_bytes(width, height))
+
+    def encode_jpeg_device(self, d_argb, width, height, quality):
+        return self._encode(lib.omr_encode_jpeg_device, d_argb, width, height, float(quality),
+                            cap=lib.omr_jpeg_max_bytes(width, height))
+
+    def encode_png(self, argb, width, height):
+        argb = np.ascontiguousarray(argb, dtype=np.uint32)
+        return self._encode(lib.omr_encode_png, argb, width, height,
+                            cap=lib.omr_png_max_bytes(width, height, 3))
+
+    def encode_png_device(self, d_argb, width, height):
+        return self._encode(lib.omr_encode_png_device, d_argb, width, height,
+                            cap=lib.omr_png_max_bytes(width, height, 3))
+
+    def render_shape_mask_png(self, bits, width, height, rgba, flip_h=False, flip_v=False):
+        bits = np.frombuffer(bytes(bits), dtype=np.uint8).copy()
+        col = (ctypes.c_uint8 * 4)(*[int(v) for v in rgba])
+        cap = lib.omr_png_max_bytes(width, height, 1)
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_size_t(0)
+        check(lib.omr_render_shape_mask_png(self.h, bits.ctypes.data if bits.size else None,
+                                            bits.size, width, height, col, int(flip_h),
+                                            int(flip_v), out.ctypes.data, cap, ctypes.byref(n)),
+              self.h)
+        return out[:n.value].tobytes()

@@ -1,0 +1,262 @@
+"""Parity of the HIP render path (K1+K2 through the C ABI) against the CPU restatement.
+
+Bar (BASELINE.json north_star): packed ARGB bit-exact for integer pixel types; float32 and
+transcendental families (log/exp/poly LUTs built on the device) within +-1 code value per
+channel contribution.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from omr import _lib
+from omr.renderer import f32
+from omr.synthetic import C2_COLORS, C2_WINDOWS, c2_channels, tile_u16
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to("cuda")
+
+
+def host_render(ctx, channels, planes, pt, w, h, **kw):
+    q = O.make_qdef(kw.pop("model", "rgb"))
+    return ctx.render_packed_int(q, channels, planes, pt, w, h, **kw)
+
+
+def assert_argb_close(got, exp, tol):
+    if tol == 0:
+        np.testing.assert_array_equal(got, exp)
+        return
+    g = got.view(np.uint8).astype(int)
+    e = exp.view(np.uint8).astype(int)
+    assert np.abs(g - e).max() <= tol, f"max diff {np.abs(g - e).max()}"
+
+
+@pytest.mark.parametrize("be", [False, True])
+@pytest.mark.parametrize("flip", [(False, False), (True, False), (False, True), (True, True)])
+def test_c2_u16_four_channel_bit_exact(ctx, be, flip):
+    h, w = 96, 128
+    planes = tile_u16(0, 4, h, w)
+    src = [O.np.ascontiguousarray(p.astype(">u2") if be else p) for p in planes]
+    chans = c2_channels(4)
+    st, exp = O.render(chans, src, _lib.PIXELS_UINT16, w, h, big_endian=be, flip_h=flip[0], flip_v=flip[1])
+    assert st == 0
+    got = host_render(ctx, chans, src, _lib.PIXELS_UINT16, w, h, big_endian=be, flip_h=flip[0], flip_v=flip[1])
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_u16_uniform_every_lut_entry(ctx):
+    h, w = 256, 256   # 65536 pixels: every uint16 value once per channel
+    rng = np.random.default_rng(7)
+    planes = [rng.permutation(65536).astype(np.uint16).reshape(h, w) for _ in range(4)]
+    chans = c2_channels(4)
+    for c, (s, e) in enumerate([(0.0, 65535.0), (1755.0, 51199.0), (3218.5, 26623.25), (65534.0, 65535.0)]):
+        chans[c]["input_start"], chans[c]["input_end"] = f32(s), f32(e)
+    st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h)
+    assert st == 0
+    np.testing.assert_array_equal(host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h), exp)
+
+
+@pytest.mark.parametrize("pt,dtype,lo,hi", [
+    (_lib.PIXELS_UINT8, np.uint8, 0, 255), (_lib.PIXELS_INT8, np.int8, -128, 127),
+    (_lib.PIXELS_INT16, np.int16, -32768, 32767), (_lib.PIXELS_UINT16, np.uint16, 0, 65535)])
+@pytest.mark.parametrize("model", ["rgb", "greyscale"])
+def test_integer_types_windows_reverse(ctx, pt, dtype, lo, hi, model):
+    h, w = 40, 72
+    rng = np.random.default_rng(11)
+    planes = [rng.integers(lo, hi + 1, size=(h, w)).astype(dtype) for _ in range(3)]
+    span = hi - lo
+    chans = [
+        {"input_start": f32(lo + 0.1 * span), "input_end": f32(lo + 0.8 * span), "global_min": lo,
+         "global_max": hi, "rgba": (255, 128, 7, 255), "reverse": True},
+        {"input_start": f32(lo), "input_end": f32(hi), "global_min": lo, "global_max": hi,
+         "rgba": (0, 255, 0, 200)},
+        {"input_start": f32(lo + 0.33 * span), "input_end": f32(lo + 0.34 * span), "global_min": lo,
+         "global_max": hi, "rgba": (255, 255, 255, 255)},
+    ]
+    for be in (False, True):
+        src = [p.astype(p.dtype.newbyteorder(">")) if be else p for p in planes]
+        st, exp = O.render(chans, src, pt, w, h, model=model, big_endian=be)
+        assert st == 0
+        got = host_render(ctx, chans, src, pt, w, h, model=model, big_endian=be)
+        np.testing.assert_array_equal(got, exp)
+
+
+def test_lut_colour_inactive_and_ragged_width(ctx):
+    h, w = 33, 37   # width % 8 != 0 -> scalar path
+    planes = tile_u16(3, 3, h, w)
+    lut = np.concatenate([np.arange(256), 255 - np.arange(256), (np.arange(256) * 7) % 256]).astype(np.uint8)
+    chans = c2_channels(3)
+    chans[1]["active"] = False
+    chans[2]["lut"] = lut
+    for flip in [(False, False), (True, True)]:
+        st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, flip_h=flip[0], flip_v=flip[1])
+        got = host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h, flip_h=flip[0], flip_v=flip[1])
+        np.testing.assert_array_equal(got, exp)
+
+
+def test_region_of_larger_plane_row_stride(ctx):
+    H, W = 64, 100
+    planes = tile_u16(5, 2, H, W)
+    x0, y0, w, h = 12, 9, 64, 40
+    chans = c2_channels(2)
+    regions = [np.ascontiguousarray(p[y0:y0 + h, x0:x0 + w]) for p in planes]
+    st, exp = O.render(chans, regions, _lib.PIXELS_UINT16, w, h)
+    views = [p[y0:, x0:] for p in planes]   # base pointer at the region start
+    import ctypes
+    q = O.make_qdef("rgb")
+    arr, keep = O.make_bindings(chans)
+    ptrs = (ctypes.c_void_p * 2)(*[v.__array_interface__["data"][0] for v in views])
+    out = np.empty((h, w), np.uint32)
+    assert _lib.lib.omr_render_packed_int(ctx.h, ctypes.byref(q), arr, 2, ptrs, W, _lib.PIXELS_UINT16, 0,
+                                          w, h, 0, 0, out.ctypes.data) == 0
+    np.testing.assert_array_equal(out, exp)
+
+
+@pytest.mark.parametrize("family,k", [(_lib.FAMILY_POLYNOMIAL, 2.0), (_lib.FAMILY_POLYNOMIAL, 0.5),
+                                      (_lib.FAMILY_LOGARITHMIC, 1.0), (_lib.FAMILY_EXPONENTIAL, 0.25)])
+def test_u16_nonlinear_families_lut_path(ctx, family, k):
+    h, w = 64, 64
+    planes = tile_u16(9, 2, h, w, uniform=True)
+    chans = c2_channels(2)
+    for c in chans:
+        c["family"], c["coefficient"] = family, k
+    st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h)
+    got = host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h)
+    assert_argb_close(got, exp, tol=2)
+    assert np.mean(got == exp) > 0.99
+
+
+def test_noise_reduction_linear_exact(ctx):
+    h, w = 64, 64
+    planes = tile_u16(10, 2, h, w, uniform=True)
+    chans = c2_channels(2)
+    chans[0]["noise_reduction"] = True
+    st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h)
+    np.testing.assert_array_equal(host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h), exp)
+
+
+def test_c5_float32_log_poly_reverse_lut(ctx):
+    h, w = 64, 96
+    rng = np.random.default_rng(SEED := 20261015 + 5)
+    planes = [rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32),
+              (rng.normal(0, 300, size=(h, w))).astype(np.float32),
+              rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32)]
+    lut = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
+    chans = []
+    for i, p in enumerate(planes):
+        lo, hi = np.percentile(p, 1), np.percentile(p, 99)
+        chans.append({"input_start": f32(lo), "input_end": f32(hi), "rgba": C2_COLORS[i]})
+    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
+    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
+    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=lut)
+    for be in (False, True):
+        src = [p.astype(">f4") if be else p for p in planes]
+        st, exp = O.render(chans, src, _lib.PIXELS_FLOAT, w, h, big_endian=be)
+        assert st == 0
+        got = host_render(ctx, chans, src, _lib.PIXELS_FLOAT, w, h, big_endian=be)
+        assert_argb_close(got, exp, tol=3)
+
+
+def test_float_linear_and_int32_double_exact(ctx):
+    h, w = 32, 48
+    rng = np.random.default_rng(3)
+    cases = [(_lib.PIXELS_FLOAT, rng.normal(100, 50, (h, w)).astype(np.float32)),
+             (_lib.PIXELS_DOUBLE, rng.normal(100, 50, (h, w))),
+             (_lib.PIXELS_INT32, rng.integers(-1000, 1000, (h, w)).astype(np.int32)),
+             (_lib.PIXELS_UINT32, rng.integers(0, 3_000_000_000, (h, w), dtype=np.uint64).astype(np.uint32))]
+    for pt, p in cases:
+        lo, hi = np.percentile(p, 5), np.percentile(p, 95)
+        chans = [{"input_start": f32(lo), "input_end": f32(hi), "rgba": (10, 200, 255, 255), "reverse": True}]
+        for be in (False, True):
+            src = [p.astype(p.dtype.newbyteorder(">")) if be else p]
+            st, exp = O.render(chans, src, pt, w, h, big_endian=be)
+            np.testing.assert_array_equal(host_render(ctx, chans, src, pt, w, h, big_endian=be), exp)
+
+
+def test_greyscale_first_active_only_and_no_active(ctx):
+    h, w = 16, 24
+    planes = tile_u16(2, 3, h, w)
+    chans = c2_channels(3)
+    chans[0]["active"] = False
+    st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, model="greyscale")
+    np.testing.assert_array_equal(host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h, model="greyscale"), exp)
+    for c in chans:
+        c["active"] = False
+    for model in ("rgb", "greyscale"):
+        st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, model=model)
+        got = host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h, model=model)
+        np.testing.assert_array_equal(got, exp)
+        assert (got == 0xFF000000).all()
+
+
+def test_quantization_exception_outside_lut_domain(ctx):
+    h, w = 8, 16
+    p = np.full((h, w), 1000, np.uint16)
+    p[3, 5] = 60000
+    chans = [{"input_start": 0.0, "input_end": 50000.0, "global_min": 0, "global_max": 50000, "rgba": (255, 0, 0, 255)}]
+    st, _ = O.render(chans, [p], _lib.PIXELS_UINT16, w, h)
+    assert st == _lib.QUANTIZATION
+    with pytest.raises(_lib.OmrError) as ei:
+        host_render(ctx, chans, [p], _lib.PIXELS_UINT16, w, h)
+    assert ei.value.status == _lib.QUANTIZATION
+    # context is usable again afterwards
+    p[3, 5] = 7
+    st, exp = O.render(chans, [p], _lib.PIXELS_UINT16, w, h)
+    np.testing.assert_array_equal(host_render(ctx, chans, [p], _lib.PIXELS_UINT16, w, h), exp)
+
+
+def test_batch_device_per_tile_status_and_results(ctx):
+    import torch
+    h, w, n = 64, 64, 5
+    chans = c2_channels(4)
+    for c in chans:
+        c["global_max"] = 60000.0
+    tiles = [tile_u16(100 + t, 4, h, w) for t in range(n)]
+    tiles[3][1][0, 0] = 65000          # outside [0, 60000] -> QuantizationException for tile 3
+    big = [[p.astype(">u2") for p in t] for t in tiles]
+    dbufs = [[dev(p) for p in t] for t in big]
+    table = torch.tensor([[b.data_ptr() for b in t] for t in dbufs], dtype=torch.int64, device="cuda")
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda")
+    status = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ctx.render_batch_device(O.make_qdef("rgb"), chans, table, n, _lib.PIXELS_UINT16, w, h, out, status,
+                            big_endian=True, flip_h=True)
+    with pytest.raises(_lib.OmrError):
+        ctx.synchronize()
+    st = status.cpu().numpy()
+    assert list(st) == [0, 0, 0, _lib.QUANTIZATION, 0]
+    got = out.cpu().numpy().view(np.uint32)
+    for t in range(n):
+        if t == 3:
+            continue
+        s, exp = O.render(chans, big[t], _lib.PIXELS_UINT16, w, h, big_endian=True, flip_h=True)
+        np.testing.assert_array_equal(got[t], exp)
+
+
+def test_device_api_matches_host_api(ctx):
+    import torch
+    h, w = 128, 256
+    planes = [p.astype(">u2") for p in tile_u16(42, 4, h, w)]
+    chans = c2_channels(4)
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+    ctx.render_packed_int_device(O.make_qdef("rgb"), chans, [dev(p) for p in planes], _lib.PIXELS_UINT16, w, h,
+                                 out, big_endian=True, flip_v=True)
+    ctx.synchronize()
+    st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, big_endian=True, flip_v=True)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+
+
+def test_invalid_arguments(ctx):
+    chans = c2_channels(1)
+    p = np.zeros((4, 4), np.uint16)
+    with pytest.raises(_lib.OmrError) as ei:
+        host_render(ctx, chans, [p], _lib.PIXELS_UINT16, 0, 4, flip_h=True)
+    assert ei.value.status == _lib.INVALID_ARGUMENT
+    with pytest.raises(_lib.OmrError):
+        host_render(ctx, chans, [None], _lib.PIXELS_UINT16, 4, 4)
+    with pytest.raises(_lib.OmrError):
+        host_render(ctx, chans, [p], 99, 4, 4)
+    # zero-size region without a flip renders nothing and succeeds (renderAsPackedInt -> int[0])
+    assert host_render(ctx, chans, [p], _lib.PIXELS_UINT16, 0, 0).size == 0
