@@ -126,11 +126,11 @@ __device__ __forceinline__ int pixel_int(const Chunk<BPP, VEC>& c, int j) {
     }
 }
 
-// Raw byte index of pixel j (8-bit types: contrib table index).
+// Raw byte of pixel j (8-bit types: the contrib table is indexed by the raw byte; K1
+// decodes the signed value of int8 entries).
 template <int VEC, bool SIGNED>
 __device__ __forceinline__ uint32_t byte_index(const Chunk<1, VEC>& c, int j) {
-    const uint32_t b = (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
-    return SIGNED ? (b ^ 0x80u) : b;
+    return (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
 }
 
 // Double value of pixel j (32/64-bit types).

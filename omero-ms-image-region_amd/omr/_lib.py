@@ -14,6 +14,14 @@ if not os.path.exists(LIB_PATH):
         f"libomr.so not found at {LIB_PATH}: build it with `make -C omero-ms-image-region_amd` "
         "(or __graft_entry__.build()); there is no fallback path")
 
+# One HIP runtime per process: torch-ROCm bundles its own libamdhip64.so.7 (same soname as
+# /opt/rocm's).  Loading torch first makes libomr.so bind to that already-loaded runtime
+# instead of pulling in a second HIP/HSA runtime that would fight over the device.
+try:
+    import torch  # noqa: F401
+except Exception:  # no torch: libomr.so uses /opt/rocm's runtime (the Java/FFI case)
+    pass
+
 lib = ctypes.CDLL(LIB_PATH)
 
 # ---- enums (omr.h) ----------------------------------------------------------------------

@@ -214,7 +214,7 @@ def test_batch_device_per_tile_status_and_results(ctx):
     chans = c2_channels(4)
     for c in chans:
         c["global_max"] = 60000.0
-    tiles = [tile_u16(100 + t, 4, h, w) for t in range(n)]
+    tiles = [[np.minimum(p, 50000) for p in tile_u16(100 + t, 4, h, w)] for t in range(n)]
     tiles[3][1][0, 0] = 65000          # outside [0, 60000] -> QuantizationException for tile 3
     big = [[p.astype(">u2") for p in t] for t in tiles]
     dbufs = [[dev(p) for p in t] for t in big]
