@@ -1,0 +1,128 @@
+"""K3 Z-projection and the flip kernels on the GPU vs the CPU restatement.
+
+Projection: ProjectionService.java:46-317 (bit-exact for every pixel type: integer sums are
+exact, float sums keep the reference's z order in double).  Flips: the reference's index-oracle
+tests (ImageRegionRequestHandlerTest.java:69-200, ShapeMaskRequestHandlerTest.java:84-215).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from omr import _lib, flip
+from omr.synthetic import c2_channels, microscopy_u16
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [(_lib.PIXELS_UINT8, np.uint8), (_lib.PIXELS_INT8, np.int8), (_lib.PIXELS_UINT16, np.uint16),
+         (_lib.PIXELS_INT16, np.int16), (_lib.PIXELS_UINT32, np.uint32), (_lib.PIXELS_INT32, np.int32),
+         (_lib.PIXELS_FLOAT, np.float32), (_lib.PIXELS_DOUBLE, np.float64)]
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).to("cuda")
+
+
+def rand_stack(dtype, z, h, w, seed):
+    rng = np.random.default_rng(seed)
+    if np.issubdtype(dtype, np.floating):
+        return (rng.normal(0, 1e4, (z, h, w))).astype(dtype)
+    info = np.iinfo(dtype)
+    return rng.integers(info.min, info.max, (z, h, w), endpoint=True, dtype=np.int64).astype(dtype)
+
+
+@pytest.mark.parametrize("pt,dtype", TYPES)
+@pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM])
+def test_projection_bit_exact_all_types(ctx, pt, dtype, alg):
+    z, h, w = 7, 9, 13                                     # ragged plane (117 px)
+    stack = rand_stack(dtype, z, h, w, 100 + pt)
+    for (start, end, step, bi, bo) in [(0, 6, 1, False, False), (1, 5, 2, True, True), (3, 3, 1, True, False),
+                                       (0, 6, 3, False, True)]:
+        src = stack.astype(stack.dtype.newbyteorder(">")) if bi else stack
+        st, exp = O.project(src, pt, w, h, z, alg, start, end, step, be_in=bi, be_out=bo)
+        assert st == 0
+        got = ctx.project_stack(src, pt, w, h, z, alg, start, end, step, big_endian_in=bi, big_endian_out=bo)
+        np.testing.assert_array_equal(got, exp, err_msg=f"{start},{end},{step},{bi},{bo}")
+
+
+def test_projection_device_api_and_validation(ctx):
+    import torch
+    z, h, w = 64, 128, 256
+    stack = rand_stack(np.uint16, z, h, w, 5)
+    d = dev(stack.astype(">u2"))
+    out = torch.empty(h * w * 2, dtype=torch.uint8, device="cuda")
+    ctx.project_stack_device(d, _lib.PIXELS_UINT16, w, h, z, _lib.PROJECTION_MEAN, 0, z - 1, out,
+                             big_endian_in=True)
+    ctx.synchronize()
+    st, exp = O.project(stack.astype(">u2"), _lib.PIXELS_UINT16, w, h, z, _lib.PROJECTION_MEAN, 0, z - 1, be_in=True)
+    np.testing.assert_array_equal(out.cpu().numpy(), exp)
+    for start, end, step, alg in [(-1, 2, 1, 0), (0, z, 1, 0), (z, 0, 1, 0), (0, 3, 0, 0), (0, 3, 1, 9)]:
+        with pytest.raises(_lib.OmrError) as ei:
+            ctx.project_stack(stack, _lib.PIXELS_UINT16, w, h, z, alg, start, end, step)
+        assert ei.value.status == _lib.INVALID_ARGUMENT
+
+
+@pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN])
+def test_c3_projection_then_composite_full_size(ctx, alg):
+    """BASELINE config C3: 3-channel uint16 512x512x64 Z-stack -> max/mean projection -> composite.
+    Default bounds 0..63 (ImageRegionRequestHandler.java:511-516): mean skips the last plane."""
+    import torch
+    z, h, w = 64, 512, 512
+    rng = np.random.default_rng(20261015 + 3)
+    base = [microscopy_u16(h, w, rng) for _ in range(3)]
+    stacks = [np.stack([np.clip(b.astype(np.int64) + rng.integers(-500, 500, (h, w)), 0, 65535).astype(np.uint16)
+                        for _ in range(z)]) for b in base]
+    be = [s.astype(">u2") for s in stacks]
+    chans = c2_channels(3)
+    projected = []
+    for s in be:
+        st, p = O.project(s, _lib.PIXELS_UINT16, w, h, z, alg, 0, z - 1, be_in=True, be_out=True)
+        assert st == 0
+        projected.append(p.view(">u2").reshape(h, w))
+    st, exp = O.render(chans, projected, _lib.PIXELS_UINT16, w, h, big_endian=True)
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+    ctx.render_projected_device(O.make_qdef("rgb"), chans, [dev(s) for s in be], _lib.PIXELS_UINT16, w, h, z,
+                                alg, 0, z - 1, out, big_endian=True)
+    ctx.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
+
+
+# ---- flips: ported index-oracle tests on the device kernels ------------------------------
+@pytest.mark.parametrize("w,h", [(4, 4), (5, 5), (7, 4), (4, 7), (7, 1), (1, 7), (1, 1)])
+def test_flip_argb_index_oracle(ctx, w, h):
+    import torch
+    src = torch.arange(w * h, dtype=torch.int32, device="cuda")
+    for fh, fv in [(False, True), (True, False), (True, True)]:
+        f = flip(ctx, src, w, h, fh, fv).cpu().numpy()
+        for n in range(w * h):
+            nc = w - 1 - n % w if fh else n % w
+            nr = h - 1 - n // w if fv else n // w
+            assert f[nr * w + nc] == n
+    assert flip(ctx, src, w, h, False, False) is src           # no flip returns src
+
+
+@pytest.mark.parametrize("w,h", [(4, 4), (5, 5), (7, 4), (4, 7), (7, 1), (1, 7), (1, 1)])
+def test_flip_mask_index_oracle(ctx, w, h):
+    import torch
+    src = torch.arange(w * h, dtype=torch.uint8, device="cuda")
+    dst = torch.empty_like(src)
+    for fh, fv in [(False, True), (True, False), (True, True)]:
+        ctx.flip_mask_device(src, dst, w, h, fh, fv)
+        f = dst.cpu().numpy()
+        for n in range(w * h):
+            nc = w - 1 - n % w if fh else n % w
+            nr = h - 1 - n // w if fv else n // w
+            assert f[nr * w + nc] == n
+
+
+def test_flip_errors(ctx):
+    import torch
+    with pytest.raises(ValueError):
+        flip(ctx, None, 4, 4, True, True)                          # testFlipNullImage
+    src = torch.ones(1, dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        flip(ctx, src, 0, 4, True, True)                           # testFlipZeroXImage
+    with pytest.raises(ValueError):
+        flip(ctx, src, 4, 0, True, True)                           # testFlipZeroYImage
+    with pytest.raises(_lib.OmrError):
+        ctx.flip_argb_device(None, src, 4, 4, True, True)
