@@ -68,10 +68,25 @@ __global__ void __launch_bounds__(256) k_build_lut(const RenderPlan* __restrict_
 }
 
 // ------------------------------------------------------------------------------- K2
+// Per-active-channel parameters K2 reads from the kernarg segment (scalar loads, no
+// per-pixel memory traffic for settings).
+struct K2Chan {
+    int32_t index;      // plane-table column (channel index)
+    int32_t mode;       // kModeTable8 / kModeLinear16 / kModeLut16 / kModeEval
+    int32_t lo, hi;     // window thresholds for integer x: x < lo -> cdStart, x >= hi -> cdEnd
+    int32_t gmin, gmax; // LUT domain
+    int32_t check;      // pixel values may fall outside [gmin, gmax] (QuantizationException)
+    int32_t second;     // the a1*v + cdStart rounding stage is not the identity
+    double ws, a0, a1;
+    uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
+};
+
+enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3 };
+
 struct K2Args {
-    const RenderPlan* plan;
+    const RenderPlan* plan;     // full plan in HBM (eval mode reads the family parameters)
     const void* const* planes;  // [n_tiles][size_c]
-    const uint8_t* ws_base;     // quantization LUTs live here (ChanParam::lut_off)
+    const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
     uint32_t* out;              // [n_tiles][H][W]
     int32_t* status;            // optional per-tile status
@@ -79,8 +94,11 @@ struct K2Args {
     int64_t row_stride;         // pixels
     int32_t size_c, n_tiles, width, height;
     int32_t flip_h, flip_v;
+    int32_t n_active, cd_start, cd_end, cds8, cde8;
+    int32_t tile_uniform;       // chunks per tile % 64 == 0: the tile index is wave-uniform
     uint32_t total;             // work items (chunks of VEC pixels)
     FastDiv cpt, cpr;           // chunks per tile, chunks per row
+    K2Chan ch[kMaxActive];
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -112,23 +130,18 @@ __device__ __forceinline__ void load_chunk(Chunk<BPP, VEC>& c, const uint8_t* p)
     }
 }
 
-// Integer value of pixel j (8/16-bit types).
-template <int BPP, int VEC, bool BE, bool SIGNED>
-__device__ __forceinline__ int pixel_int(const Chunk<BPP, VEC>& c, int j) {
-    if constexpr (BPP == 1) {
-        const uint32_t b = (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
-        return SIGNED ? (int)(int8_t)b : (int)b;
-    } else {
-        uint32_t d = c.dw[j >> 1];
-        if constexpr (BE) d = bswap16x2(d);
-        const uint32_t h = (j & 1) ? (d >> 16) : (d & 0xFFFF);
-        return SIGNED ? (int)(int16_t)h : (int)h;
-    }
+// Integer value of pixel j (16-bit types).
+template <int VEC, bool BE, bool SIGNED>
+__device__ __forceinline__ int pixel16(const Chunk<2, VEC>& c, int j) {
+    uint32_t d = c.dw[j >> 1];
+    if constexpr (BE) d = bswap16x2(d);
+    const uint32_t h = (j & 1) ? (d >> 16) : (d & 0xFFFF);
+    return SIGNED ? (int)(int16_t)h : (int)h;
 }
 
 // Raw byte of pixel j (8-bit types: the contrib table is indexed by the raw byte; K1
 // decodes the signed value of int8 entries).
-template <int VEC, bool SIGNED>
+template <int VEC>
 __device__ __forceinline__ uint32_t byte_index(const Chunk<1, VEC>& c, int j) {
     return (c.dw[j >> 2] >> (8 * (j & 3))) & 0xFF;
 }
@@ -154,72 +167,102 @@ __device__ __forceinline__ uint32_t clamp_fields(uint32_t a) {
     return (r << 20) | (g << 10) | b;
 }
 
-// Quantized value of a 16-bit pixel: exact LUT entry (linear) or LUT gather.
-__device__ __forceinline__ uint32_t quant16(int x, const ChanParam& p, const uint8_t* ws_base,
-                                            int cds8, int cde8, int cds, bool& err) {
-    if (x < p.gmin || x > p.gmax) { err = true; return 0; }
-    if (p.mode == kModeLut16) return ws_base[p.lut_off + (uint32_t)(x - p.gmin)];
-    if (x < p.lo) return (uint32_t)cds8;
-    if (x >= p.hi) return (uint32_t)cde8;
+// Exact LUT entry of a 16-bit pixel for the linear family, branch-free:
+// v = round(a0*(x - ws)) (Java Math.round), window ends by integer compare.
+__device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, int cds8, int cde8) {
     const double d = p.a0 * ((double)x - p.ws);
-    int v = (d == 0x1.fffffffffffffp-2) ? 0 : (int)floor(d + 0.5);
-    if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);
+    int v = __double2int_rz(floor(d + 0.5));          // exact in the window (d in [0, bitRes])
+    v = (d == 0x1.fffffffffffffp-2) ? 0 : v;
+    if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);   // uniform branch
+    v = x < p.lo ? cds8 : v;
+    v = x >= p.hi ? cde8 : v;
     return (uint32_t)v & 0xFFu;
 }
 
+// General q(x) in double (float / 32-bit types): Java semantics, selects instead of branches.
+__device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds, int cde) {
+    const double f = family_map(p.family, x, p.k);
+    const double a = p.a0 * (f - p.ys);
+    double r = floor(a + 0.5);
+    r = (a == 0x1.fffffffffffffp-2 || r != r) ? 0.0 : r;
+    r = fmin(fmax(r, -9223372036854775808.0), 9223372036854775808.0);   // (double)(long) round
+    uint32_t v = (uint32_t)(java_round_d(p.a1 * r + (double)cds) & 0xFF);
+    const bool lo = x < p.ws || (p.nr && x < p.ws + p.dec);
+    const bool hi = x >= p.we || (p.nr && x >= p.we - p.dec);
+    v = hi && !(x < p.ws) ? (uint32_t)(cde & 0xFF) : v;
+    v = lo ? (uint32_t)(cds & 0xFF) : v;
+    return v;
+}
+
 // NA > 0: fixed active-channel count (fully unrolled, all loads issued up front).
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA>
-__global__ void __launch_bounds__(kBlock) k_render(K2Args A) {
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
+__global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
-    const RenderPlan* __restrict__ plan = A.plan;
-    const int na = NA > 0 ? NA : plan->n_active;
+    const int na = NA > 0 ? NA : A.n_active;
     for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.contrib[i];
     __syncthreads();
-    const int cds = plan->cd_start, cds8 = plan->cd_start & 0xFF, cde8 = plan->cd_end & 0xFF;
+    const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
     const int W = A.width, H = A.height;
-    const uint32_t cpr = A.cpr.d;
+    const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
+    constexpr int NL = NA > 0 ? NA : 1;
+    const uint8_t* base[NL];
+    uint32_t cur_tile = 0xFFFFFFFFu;
     for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < A.total; g += gridDim.x * kBlock) {
-        const uint32_t tile = fdiv(g, A.cpt);
-        const uint32_t rem = g - tile * A.cpt.d;
+        uint32_t tile = fdiv(g, A.cpt);
+        if (A.tile_uniform) tile = __builtin_amdgcn_readfirstlane(tile);
+        const uint32_t rem = g - tile * cptd;
         const uint32_t row = fdiv(rem, A.cpr);
         const uint32_t cc = rem - row * cpr;
         const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
+        if constexpr (NA > 0) {
+            if (tile != cur_tile) {
+#pragma unroll
+                for (int a = 0; a < NA; ++a)
+                    base[a] = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + A.ch[a].index]);
+                cur_tile = tile;
+            }
+        }
         uint32_t acc[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[j] = 0;
         uint32_t err_bits = 0;
         bool err = false;
-        constexpr int NL = NA > 0 ? NA : 1;
         Chunk<BPP, VEC> ck[NL];
         if constexpr (NA > 0) {
 #pragma unroll
-            for (int a = 0; a < NA; ++a) {
-                const uint8_t* base = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + plan->ch[a].index]);
-                load_chunk<BPP, VEC>(ck[a], base + in_off);
-            }
+            for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(ck[a], base[a] + in_off);
         }
 #pragma unroll
-        for (int a = 0; a < na; ++a) {
-            const ChanParam& p = plan->ch[a];
+        for (int a = 0; a < (NA > 0 ? NA : kMaxActive); ++a) {
+            if (NA == 0 && a >= na) break;
+            const K2Chan& p = A.ch[a];
             Chunk<BPP, VEC>& c = ck[NA > 0 ? a : 0];
             if constexpr (NA == 0) {
-                const uint8_t* base = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + p.index]);
-                load_chunk<BPP, VEC>(c, base + in_off);
+                const uint8_t* b = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + p.index]);
+                load_chunk<BPP, VEC>(c, b + in_off);
             }
             const uint32_t* tab = s_contrib + a * 256;
 #pragma unroll
             for (int j = 0; j < VEC; ++j) {
                 uint32_t e;
-                if constexpr (BPP == 1) {
-                    e = tab[byte_index<VEC, SIGNED>(c, j)];
+                if constexpr (MODE == kK2Table8) {
+                    e = tab[byte_index<VEC>(c, j)];
                     err_bits |= e;
                     e &= ~kErrBit;
-                } else if constexpr (BPP == 2) {
-                    const int x = pixel_int<BPP, VEC, BE, SIGNED>(c, j);
-                    e = tab[quant16(x, p, A.ws_base, cds8, cde8, cds, err)];
+                } else if constexpr (MODE == kK2Linear16 || MODE == kK2Mixed16) {
+                    const int x = pixel16<VEC, BE, SIGNED>(c, j);
+                    if (p.check) err |= (x < p.gmin) | (x > p.gmax);
+                    uint32_t v;
+                    if (MODE == kK2Linear16 || p.mode == kModeLinear16) {
+                        v = linear16(x, p, cds, cds8, cde8);
+                    } else {
+                        const int xi = min(max(x, p.gmin), p.gmax);
+                        v = A.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
+                    }
+                    e = tab[v];
                 } else {
                     const double x = pixel_double<BPP, VEC, BE, PT>(c, j);
-                    e = tab[quantize_eval(x, p, plan->cd_start, plan->cd_end)];
+                    e = tab[eval_q(x, A.plan->ch[a], A.cd_start, A.cd_end)];
                 }
                 acc[j] += e;
                 if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
@@ -375,39 +418,53 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
     return L;
 }
 
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT>
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_t s) {
     const size_t lds = (size_t)(na > 0 ? na : 1) * 256 * 4;
     switch (na) {
-    case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    default: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 0>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    default: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 0, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
     }
     return hipGetLastError();
 }
 
 template <int BPP, int VEC, bool BE>
-static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int grid, hipStream_t s) {
+static hipError_t launch_render_pt(const K2Args& a, int pt, int na, bool all_linear, int grid, hipStream_t s) {
     if constexpr (BPP == 1) {
-        return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8>(a, na, grid, s)
-                                     : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8>(a, na, grid, s);
+        return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8, kK2Table8>(a, na, grid, s)
+                                     : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8, kK2Table8>(a, na, grid, s);
     } else if constexpr (BPP == 2) {
-        return pt == OMR_PIXELS_INT16 ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16>(a, na, grid, s)
-                                      : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16>(a, na, grid, s);
+        if (pt == OMR_PIXELS_INT16)
+            return all_linear ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Linear16>(a, na, grid, s)
+                              : launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Mixed16>(a, na, grid, s);
+        return all_linear ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, s)
+                          : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, s);
     } else if constexpr (BPP == 4) {
-        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT>(a, na, grid, s);
-        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32>(a, na, grid, s);
-        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32>(a, na, grid, s);
+        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, s);
+        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, s);
+        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, s);
     } else {
-        return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE>(a, na, grid, s);
+        return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE, kK2Eval>(a, na, grid, s);
     }
 }
 
 template <int BPP, int VEC>
-static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int grid, hipStream_t s) {
-    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, grid, s) : launch_render_pt<BPP, VEC, false>(a, pt, na, grid, s);
+static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, bool all_linear, int grid, hipStream_t s) {
+    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, all_linear, grid, s)
+              : launch_render_pt<BPP, VEC, false>(a, pt, na, all_linear, grid, s);
+}
+
+static void type_bounds(int32_t t, double& lo, double& hi) {
+    switch (t) {
+    case OMR_PIXELS_INT8: lo = -128; hi = 127; break;
+    case OMR_PIXELS_UINT8: lo = 0; hi = 255; break;
+    case OMR_PIXELS_INT16: lo = -32768; hi = 32767; break;
+    case OMR_PIXELS_UINT16: lo = 0; hi = 65535; break;
+    default: lo = 0; hi = 0; break;
+    }
 }
 
 // Enqueue K1 + K2 for a batch whose plane pointer table is already on the device.
@@ -444,6 +501,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     if (total == 0) return OMR_OK;
     if (total >= (1ull << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "batch too large for one launch");
     K2Args a;
+    std::memset(&a, 0, sizeof(a));
     a.plan = d_plan;
     a.planes = d_plane_ptrs;
     a.ws_base = ws;
@@ -458,9 +516,35 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.height = height;
     a.flip_h = flip_h ? 1 : 0;
     a.flip_v = flip_v ? 1 : 0;
+    a.n_active = na;
+    a.cd_start = pp.plan.cd_start;
+    a.cd_end = pp.plan.cd_end;
+    a.cds8 = pp.plan.cd_start & 0xFF;
+    a.cde8 = pp.plan.cd_end & 0xFF;
+    a.tile_uniform = (cpt % 64) == 0 ? 1 : 0;
     a.total = (uint32_t)total;
     a.cpt = make_fastdiv((uint32_t)cpt);
     a.cpr = make_fastdiv((uint32_t)cpr);
+    bool all_linear = true;
+    double tlo, thi;
+    type_bounds(pixel_type, tlo, thi);
+    for (int i = 0; i < na; ++i) {
+        const ChanParam& c = pp.plan.ch[i];
+        K2Chan& k = a.ch[i];
+        k.index = c.index;
+        k.mode = c.mode;
+        k.lo = c.lo;
+        k.hi = c.hi;
+        k.gmin = c.gmin;
+        k.gmax = c.gmax;
+        k.check = (bpp <= 2 && (c.gmin > tlo || c.gmax < thi)) ? 1 : 0;
+        k.second = c.second;
+        k.ws = c.ws;
+        k.a0 = c.a0;
+        k.a1 = c.a1;
+        k.lut_off = c.lut_off + L.lut_off;
+        if (c.mode != kModeLinear16) all_linear = false;
+    }
     const uint64_t blocks_needed = (total + kBlock - 1) / kBlock;
     const int grid = (int)std::min<uint64_t>(blocks_needed, (uint64_t)ctx->cu_count * 8);
     hipError_t e;
@@ -468,17 +552,17 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     KernelTimer timer(ctx, 2);
     if (aligned) {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
         }
     } else {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
         }
     }
     OMR_HIP(ctx, e);
