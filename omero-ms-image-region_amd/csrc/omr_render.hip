@@ -81,7 +81,7 @@ struct K2Chan {
     uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
 };
 
-enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3 };
+enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3, kK2Fast16 = 4 };
 
 struct K2Args {
     const RenderPlan* plan;     // full plan in HBM (eval mode reads the family parameters)
@@ -95,7 +95,7 @@ struct K2Args {
     int32_t size_c, n_tiles, width, height;
     int32_t flip_h, flip_v;
     int32_t n_active, cd_start, cd_end, cds8, cde8;
-    int32_t tile_uniform;       // chunks per tile % 64 == 0: the tile index is wave-uniform
+    int32_t tile_uniform;       // every block lies inside one tile (chunks per tile % block chunks == 0)
     uint32_t total;             // work items (chunks of VEC pixels)
     FastDiv cpt, cpr;           // chunks per tile, chunks per row
     K2Chan ch[kMaxActive];
@@ -116,10 +116,10 @@ template <int BPP, int VEC>
 __device__ __forceinline__ void load_chunk(Chunk<BPP, VEC>& c, const uint8_t* p) {
     constexpr int B = BPP * VEC;
     if constexpr (B == 16) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        const u32x4 v = *reinterpret_cast<const u32x4*>(p);
         c.dw[0] = v[0]; c.dw[1] = v[1]; c.dw[2] = v[2]; c.dw[3] = v[3];
     } else if constexpr (B == 8) {
-        const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p));
+        const u32x2 v = *reinterpret_cast<const u32x2*>(p);
         c.dw[0] = v[0]; c.dw[1] = v[1];
     } else if constexpr (B == 4) {
         c.dw[0] = *reinterpret_cast<const uint32_t*>(p);
@@ -179,6 +179,16 @@ __device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, in
     return (uint32_t)v & 0xFFu;
 }
 
+// Default QuantumDef (cd 0..255, bitRes 255), window start < end, and no window pixel at
+// Java's 0.49999999999999994 special case (checked on the host): round(a0*(x - ws)) clamped
+// to [0,255] equals the LUT entry for every x (below the window d < 0 -> 0, above it
+// d >= 255 -> 255), so the window compares fold into one med3.
+__device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
+    const double d = p.a0 * ((double)x - p.ws);
+    const int v = __double2int_rz(floor(d + 0.5));
+    return (uint32_t)min(max(v, 0), 255);
+}
+
 // General q(x) in double (float / 32-bit types): Java semantics, selects instead of branches.
 __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds, int cde) {
     const double f = family_map(p.family, x, p.k);
@@ -194,49 +204,72 @@ __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds
     return v;
 }
 
-// NA > 0: fixed active-channel count (fully unrolled, all loads issued up front).
+constexpr int kCPT = 2;   // chunks per thread of the fixed-channel-count kernels
+
+// One full (non-persistent) grid: block b owns chunks [b*256*CPT, (b+1)*256*CPT), thread t the
+// chunks b*256*CPT + k*256 + t.  Every channel load of every chunk is issued before any compute
+// (CPT*NA 16-B loads in flight per lane); plain loads (measured faster than non-temporal here,
+// tools/probe_stream.hip).  NA == 0: runtime channel count, one chunk per thread, clamp per add.
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
 __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
+    constexpr int CPT = NA > 0 ? kCPT : 1;
+    constexpr int NL = NA > 0 ? NA : 1;
     const int na = NA > 0 ? NA : A.n_active;
     for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.contrib[i];
-    __syncthreads();
     const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
     const int W = A.width, H = A.height;
     const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
-    constexpr int NL = NA > 0 ? NA : 1;
-    const uint8_t* base[NL];
-    uint32_t cur_tile = 0xFFFFFFFFu;
-    for (uint32_t g = blockIdx.x * kBlock + threadIdx.x; g < A.total; g += gridDim.x * kBlock) {
-        uint32_t tile = fdiv(g, A.cpt);
-        if (A.tile_uniform) tile = __builtin_amdgcn_readfirstlane(tile);
-        const uint32_t rem = g - tile * cptd;
-        const uint32_t row = fdiv(rem, A.cpr);
-        const uint32_t cc = rem - row * cpr;
-        const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
-        if constexpr (NA > 0) {
-            if (tile != cur_tile) {
+    const uint32_t g0 = blockIdx.x * (kBlock * CPT);
+    uint32_t btile = 0;
+    if (A.tile_uniform) btile = fdiv(g0, A.cpt);          // whole block inside one tile (scalar)
+    const uint8_t* ubase[NL];
+    if (NA > 0 && A.tile_uniform) {
 #pragma unroll
-                for (int a = 0; a < NA; ++a)
-                    base[a] = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + A.ch[a].index]);
-                cur_tile = tile;
+        for (int a = 0; a < NL; ++a)
+            ubase[a] = static_cast<const uint8_t*>(A.planes[(int64_t)btile * A.size_c + A.ch[a].index]);
+    }
+    uint32_t gk[CPT], tk[CPT], rk[CPT], ck_[CPT];
+    Chunk<BPP, VEC> ck[CPT][NL];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        const uint32_t g = g0 + k * kBlock + threadIdx.x;
+        gk[k] = g;
+        const uint32_t t = A.tile_uniform ? btile : fdiv(g, A.cpt);
+        const uint32_t rem = g - t * cptd;
+        const uint32_t r = fdiv(rem, A.cpr);
+        tk[k] = t;
+        rk[k] = r;
+        ck_[k] = rem - r * cpr;
+        if constexpr (NA > 0) {
+            if (g < A.total) {
+                const int64_t off = ((int64_t)r * A.row_stride + (int64_t)ck_[k] * VEC) * BPP;
+#pragma unroll
+                for (int a = 0; a < NA; ++a) {
+                    const uint8_t* b = A.tile_uniform ? ubase[a]
+                        : static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
+                    load_chunk<BPP, VEC>(ck[k][a], b + off);
+                }
             }
         }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        const uint32_t g = gk[k];
+        if (g >= A.total) continue;
+        const uint32_t tile = tk[k], row = rk[k], cc = ck_[k];
+        const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
         uint32_t acc[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) acc[j] = 0;
         uint32_t err_bits = 0;
         bool err = false;
-        Chunk<BPP, VEC> ck[NL];
-        if constexpr (NA > 0) {
-#pragma unroll
-            for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(ck[a], base[a] + in_off);
-        }
 #pragma unroll
         for (int a = 0; a < (NA > 0 ? NA : kMaxActive); ++a) {
             if (NA == 0 && a >= na) break;
             const K2Chan& p = A.ch[a];
-            Chunk<BPP, VEC>& c = ck[NA > 0 ? a : 0];
+            Chunk<BPP, VEC>& c = ck[k][NA > 0 ? a : 0];
             if constexpr (NA == 0) {
                 const uint8_t* b = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + p.index]);
                 load_chunk<BPP, VEC>(c, b + in_off);
@@ -249,11 +282,13 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
                     e = tab[byte_index<VEC>(c, j)];
                     err_bits |= e;
                     e &= ~kErrBit;
-                } else if constexpr (MODE == kK2Linear16 || MODE == kK2Mixed16) {
+                } else if constexpr (MODE == kK2Fast16 || MODE == kK2Linear16 || MODE == kK2Mixed16) {
                     const int x = pixel16<VEC, BE, SIGNED>(c, j);
                     if (p.check) err |= (x < p.gmin) | (x > p.gmax);
                     uint32_t v;
-                    if (MODE == kK2Linear16 || p.mode == kModeLinear16) {
+                    if constexpr (MODE == kK2Fast16) {
+                        v = fast16(x, p);
+                    } else if (MODE == kK2Linear16 || p.mode == kModeLinear16) {
                         v = linear16(x, p, cds, cds8, cde8);
                     } else {
                         const int xi = min(max(x, p.gmin), p.gmax);
@@ -432,16 +467,19 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_
 }
 
 template <int BPP, int VEC, bool BE>
-static hipError_t launch_render_pt(const K2Args& a, int pt, int na, bool all_linear, int grid, hipStream_t s) {
+static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, int grid, hipStream_t s) {
     if constexpr (BPP == 1) {
         return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8, kK2Table8>(a, na, grid, s)
                                      : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8, kK2Table8>(a, na, grid, s);
     } else if constexpr (BPP == 2) {
-        if (pt == OMR_PIXELS_INT16)
-            return all_linear ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Linear16>(a, na, grid, s)
-                              : launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Mixed16>(a, na, grid, s);
-        return all_linear ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, s)
-                          : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, s);
+        if (pt == OMR_PIXELS_INT16) {
+            if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Fast16>(a, na, grid, s);
+            return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Linear16>(a, na, grid, s)
+                                         : launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Mixed16>(a, na, grid, s);
+        }
+        if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Fast16>(a, na, grid, s);
+        return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, s)
+                                     : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, s);
     } else if constexpr (BPP == 4) {
         if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, s);
         if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, s);
@@ -452,9 +490,24 @@ static hipError_t launch_render_pt(const K2Args& a, int pt, int na, bool all_lin
 }
 
 template <int BPP, int VEC>
-static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, bool all_linear, int grid, hipStream_t s) {
-    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, all_linear, grid, s)
-              : launch_render_pt<BPP, VEC, false>(a, pt, na, all_linear, grid, s);
+static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int mode16, int grid, hipStream_t s) {
+    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, mode16, grid, s)
+              : launch_render_pt<BPP, VEC, false>(a, pt, na, mode16, grid, s);
+}
+
+// kK2Fast16 preconditions (see fast16): default codomain, increasing window, finite slope,
+// and no integer x in the window with a0*(x - ws) == 0.49999999999999994 (Java's
+// Math.round special case, where floor(d + 0.5) would differ).
+static bool fast_linear_ok(const ChanParam& c, const RenderPlan& P) {
+    if (P.cd_start != 0 || P.cd_end != 255 || c.second || !(c.we > c.ws) || !(c.a0 > 0) || !std::isfinite(c.a0))
+        return false;
+    const double x0 = std::floor(c.ws + 0.5 / c.a0);
+    for (double x = x0 - 3; x <= x0 + 3; x += 1.0) {
+        if (x < c.lo || x >= c.hi) continue;
+        const double d = c.a0 * (x - c.ws);
+        if (d == 0x1.fffffffffffffp-2) return false;
+    }
+    return true;
 }
 
 static void type_bounds(int32_t t, double& lo, double& hi) {
@@ -521,11 +574,12 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cd_end = pp.plan.cd_end;
     a.cds8 = pp.plan.cd_start & 0xFF;
     a.cde8 = pp.plan.cd_end & 0xFF;
-    a.tile_uniform = (cpt % 64) == 0 ? 1 : 0;
+    const int cpt_thread = (na >= 1 && na <= 4) ? kCPT : 1;
+    a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.total = (uint32_t)total;
     a.cpt = make_fastdiv((uint32_t)cpt);
     a.cpr = make_fastdiv((uint32_t)cpr);
-    bool all_linear = true;
+    bool all_linear = true, all_fast = true;
     double tlo, thi;
     type_bounds(pixel_type, tlo, thi);
     for (int i = 0; i < na; ++i) {
@@ -544,25 +598,27 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         k.a1 = c.a1;
         k.lut_off = c.lut_off + L.lut_off;
         if (c.mode != kModeLinear16) all_linear = false;
+        if (!(c.mode == kModeLinear16 && fast_linear_ok(c, pp.plan))) all_fast = false;
     }
-    const uint64_t blocks_needed = (total + kBlock - 1) / kBlock;
-    const int grid = (int)std::min<uint64_t>(blocks_needed, (uint64_t)ctx->cu_count * 8);
+    const int mode16 = all_fast ? kK2Fast16 : all_linear ? kK2Linear16 : kK2Mixed16;
+    const uint64_t per_block = (uint64_t)kBlock * cpt_thread;
+    const int grid = (int)((total + per_block - 1) / per_block);
     hipError_t e;
     const bool be = big_endian != 0;
     KernelTimer timer(ctx, 2);
     if (aligned) {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
         }
     } else {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, all_linear, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
         }
     }
     OMR_HIP(ctx, e);
