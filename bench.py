@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="tiles per GPU per step")
     ap.add_argument("--unique", type=int, default=8, help="distinct synthetic tiles per GPU")
+    ap.add_argument("--addr", choices=["strided", "table"], default="strided",
+                    help="batch descriptor: regular [tile][channel] layout or device pointer table")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -144,9 +146,16 @@ def main():
     data, uniq, table = build_batch(torch, B, min(args.unique, B), device)
     out = torch.empty((B, TILE, TILE), dtype=torch.int32, device=device)
 
+    plane_bytes = TILE * TILE * 2
+
     def step():
-        ctx.render_batch_device(qdef, chans, table, B, _lib.PIXELS_UINT16, TILE, TILE, out,
-                                big_endian=True, bindings=bindings)
+        if args.addr == "strided":
+            ctx.render_batch_strided_device(qdef, chans, data, CHANNELS * plane_bytes, plane_bytes, B,
+                                            _lib.PIXELS_UINT16, TILE, TILE, out, big_endian=True,
+                                            bindings=bindings)
+        else:
+            ctx.render_batch_device(qdef, chans, table, B, _lib.PIXELS_UINT16, TILE, TILE, out,
+                                    big_endian=True, bindings=bindings)
 
     for _ in range(args.warmup):
         step()
@@ -211,6 +220,7 @@ def main():
                 "windows": "0:65535,1755:51199,3218:26623,100:4000",
                 "colors": "0000FF,00FF00,FF0000,FFFFFF",
                 "parallelism": f"dp{world} (independent tile batches per GPU, no collectives)",
+                "batch_descriptor": args.addr,
             },
             "roofline": {
                 "bound": "hbm",

@@ -166,6 +166,20 @@ omr_status omr_render_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
                                    uint32_t* d_argb_out, int32_t* d_status);
 
 /*
+ * Same batch with the planes laid out regularly in device memory (e.g. a pyramid level kept
+ * resident as [tile][channel][y][x]): plane(t, c) = d_base + t*tile_stride_bytes +
+ * c*channel_stride_bytes.  No pointer table; otherwise identical to omr_render_batch_device.
+ */
+omr_status omr_render_batch_strided_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                           const omr_channel_binding* channels, int32_t size_c,
+                                           const void* d_base, int64_t tile_stride_bytes,
+                                           int64_t channel_stride_bytes, int32_t n_tiles,
+                                           int64_t row_stride, int32_t pixel_type, int32_t big_endian,
+                                           int32_t width, int32_t height,
+                                           int32_t flip_h, int32_t flip_v,
+                                           uint32_t* d_argb_out, int32_t* d_status);
+
+/*
  * Standalone output flip of an already-rendered ARGB buffer on the device
  * (ImageRegionRequestHandler.flip, :616-642).  src and dest must not alias.
  * Identity (no flip) copies.

@@ -85,7 +85,10 @@ enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3,
 
 struct K2Args {
     const RenderPlan* plan;     // full plan in HBM (eval mode reads the family parameters)
-    const void* const* planes;  // [n_tiles][size_c]
+    const void* const* planes;  // [n_tiles][size_c] (pointer-table batches)
+    const uint8_t* sbase;       // strided batches: plane(t, c) = sbase + t*tile_stride + c*chan_stride
+    int64_t tile_stride, chan_stride;
+    int32_t strided;
     const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
     uint32_t* out;              // [n_tiles][H][W]
@@ -112,21 +115,28 @@ struct Chunk {
     uint32_t dw[kDw];
 };
 
+// Plane pointers arrive as generic pointers (pointer table / strided base); loading through
+// the global address space gives global_load_* instead of flat_load_*, whose shared
+// vmcnt/lgkmcnt accounting forced a full wait between the channel loads.
+#define OMR_GLOBAL __attribute__((address_space(1)))
+template <typename T> __device__ __forceinline__ const OMR_GLOBAL T* gload_ptr(const void* p) { return (const OMR_GLOBAL T*)(p); }
+template <typename T> __device__ __forceinline__ OMR_GLOBAL T* gstore_ptr(void* p) { return (OMR_GLOBAL T*)(p); }
+
 template <int BPP, int VEC>
 __device__ __forceinline__ void load_chunk(Chunk<BPP, VEC>& c, const uint8_t* p) {
     constexpr int B = BPP * VEC;
     if constexpr (B == 16) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+        const u32x4 v = *gload_ptr<u32x4>(p);
         c.dw[0] = v[0]; c.dw[1] = v[1]; c.dw[2] = v[2]; c.dw[3] = v[3];
     } else if constexpr (B == 8) {
-        const u32x2 v = *reinterpret_cast<const u32x2*>(p);
+        const u32x2 v = *gload_ptr<u32x2>(p);
         c.dw[0] = v[0]; c.dw[1] = v[1];
     } else if constexpr (B == 4) {
-        c.dw[0] = *reinterpret_cast<const uint32_t*>(p);
+        c.dw[0] = *gload_ptr<uint32_t>(p);
     } else if constexpr (B == 2) {
-        c.dw[0] = *reinterpret_cast<const uint16_t*>(p);
+        c.dw[0] = *gload_ptr<uint16_t>(p);
     } else {
-        c.dw[0] = *p;
+        c.dw[0] = *gload_ptr<uint8_t>(p);
     }
 }
 
@@ -216,43 +226,53 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
     constexpr int CPT = NA > 0 ? kCPT : 1;
     constexpr int NL = NA > 0 ? NA : 1;
     const int na = NA > 0 ? NA : A.n_active;
-    for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.contrib[i];
     const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
     const int W = A.width, H = A.height;
     const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
     const uint32_t g0 = blockIdx.x * (kBlock * CPT);
     uint32_t btile = 0;
     if (A.tile_uniform) btile = fdiv(g0, A.cpt);          // whole block inside one tile (scalar)
+    auto plane_base = [&](uint32_t t, int a) -> const uint8_t* {
+        if (A.strided) return A.sbase + (int64_t)t * A.tile_stride + (int64_t)A.ch[a].index * A.chan_stride;
+        return static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
+    };
     const uint8_t* ubase[NL];
     if (NA > 0 && A.tile_uniform) {
 #pragma unroll
-        for (int a = 0; a < NL; ++a)
-            ubase[a] = static_cast<const uint8_t*>(A.planes[(int64_t)btile * A.size_c + A.ch[a].index]);
+        for (int a = 0; a < NL; ++a) ubase[a] = plane_base(btile, a);
     }
     uint32_t gk[CPT], tk[CPT], rk[CPT], ck_[CPT];
     Chunk<BPP, VEC> ck[CPT][NL];
+    const uint8_t* pb[CPT][NL];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-        const uint32_t g = g0 + k * kBlock + threadIdx.x;
-        gk[k] = g;
+        gk[k] = g0 + k * kBlock + threadIdx.x;
+        const uint32_t g = min(gk[k], A.total - 1);   // tail lanes load a valid chunk, store nothing
         const uint32_t t = A.tile_uniform ? btile : fdiv(g, A.cpt);
         const uint32_t rem = g - t * cptd;
         const uint32_t r = fdiv(rem, A.cpr);
         tk[k] = t;
         rk[k] = r;
         ck_[k] = rem - r * cpr;
-        if constexpr (NA > 0) {
-            if (g < A.total) {
-                const int64_t off = ((int64_t)r * A.row_stride + (int64_t)ck_[k] * VEC) * BPP;
+    }
+    if constexpr (NA > 0) {
+        // 1) every plane pointer (scalar when the block sits in one tile), 2) every pixel load
+        //    back to back: no wait between the channel loads.
 #pragma unroll
-                for (int a = 0; a < NA; ++a) {
-                    const uint8_t* b = A.tile_uniform ? ubase[a]
-                        : static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
-                    load_chunk<BPP, VEC>(ck[k][a], b + off);
-                }
-            }
+        for (int k = 0; k < CPT; ++k)
+#pragma unroll
+            for (int a = 0; a < NA; ++a) pb[k][a] = A.tile_uniform ? ubase[a] : plane_base(tk[k], a);
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+            const int64_t off = ((int64_t)rk[k] * A.row_stride + (int64_t)ck_[k] * VEC) * BPP;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(ck[k][a], pb[k][a] + off);
         }
     }
+    // Contribution tables -> LDS, issued after the pixel loads so their latencies overlap
+    // (one 16-byte load per lane for up to 4 channels; a single wait).
+    for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
+        *reinterpret_cast<uint4*>(s_contrib + i) = *reinterpret_cast<const uint4*>(A.contrib + i);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -271,8 +291,7 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
             const K2Chan& p = A.ch[a];
             Chunk<BPP, VEC>& c = ck[k][NA > 0 ? a : 0];
             if constexpr (NA == 0) {
-                const uint8_t* b = static_cast<const uint8_t*>(A.planes[(int64_t)tile * A.size_c + p.index]);
-                load_chunk<BPP, VEC>(c, b + in_off);
+                load_chunk<BPP, VEC>(c, plane_base(tile, a) + in_off);
             }
             const uint32_t* tab = s_contrib + a * 256;
 #pragma unroll
@@ -315,7 +334,7 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
         }
         const uint32_t orow = A.flip_v ? (uint32_t)H - 1 - row : row;
         const uint32_t ocol = A.flip_h ? (uint32_t)W - (cc + 1) * VEC : cc * VEC;
-        uint32_t* o = A.out + (int64_t)tile * W * H + (int64_t)orow * W + ocol;
+        OMR_GLOBAL uint32_t* o = gstore_ptr<uint32_t>(A.out + (int64_t)tile * W * H + (int64_t)orow * W + ocol);
         if (A.flip_h) {
 #pragma unroll
             for (int j = 0; j < VEC / 2; ++j) { const uint32_t t = px[j]; px[j] = px[VEC - 1 - j]; px[VEC - 1 - j] = t; }
@@ -323,9 +342,9 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
         if constexpr (VEC % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < VEC; j += 4)
-                *reinterpret_cast<uint4*>(o + j) = make_uint4(px[j], px[j + 1], px[j + 2], px[j + 3]);
+                *(OMR_GLOBAL u32x4*)(o + j) = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
         } else if constexpr (VEC == 2) {
-            *reinterpret_cast<uint2*>(o) = make_uint2(px[0], px[1]);
+            *(OMR_GLOBAL u32x2*)(o) = u32x2{px[0], px[1]};
         } else {
             o[0] = px[0];
         }
@@ -521,11 +540,16 @@ static void type_bounds(int32_t t, double& lo, double& hi) {
 }
 
 // Enqueue K1 + K2 for a batch whose plane pointer table is already on the device.
+struct Strided {
+    const void* base;
+    int64_t tile_stride, chan_stride;   // bytes
+};
+
 static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type, int32_t big_endian,
                                  const void* const* d_plane_ptrs, int32_t size_c, int32_t n_tiles,
                                  int64_t row_stride, int32_t width, int32_t height, int32_t flip_h,
                                  int32_t flip_v, uint32_t* d_out, int32_t* d_status, bool aligned,
-                                 const RenderLayout& L) {
+                                 const RenderLayout& L, const Strided* strided = nullptr) {
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
     uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
@@ -557,6 +581,12 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     std::memset(&a, 0, sizeof(a));
     a.plan = d_plan;
     a.planes = d_plane_ptrs;
+    if (strided) {
+        a.strided = 1;
+        a.sbase = static_cast<const uint8_t*>(strided->base);
+        a.tile_stride = strided->tile_stride;
+        a.chan_stride = strided->chan_stride;
+    }
     a.ws_base = ws;
     a.contrib = d_contrib;
     a.out = d_out;
@@ -671,6 +701,37 @@ omr_status omr_render_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
     return enqueue_render(ctx, pp, pixel_type, big_endian, d_plane_ptrs, size_c, n_tiles, row_stride,
                           width, height, flip_h, flip_v, d_argb_out, d_status,
                           vec_aligned(bpp, width, row_stride), L);
+}
+
+omr_status omr_render_batch_strided_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                           const omr_channel_binding* channels, int32_t size_c,
+                                           const void* d_base, int64_t tile_stride_bytes,
+                                           int64_t channel_stride_bytes, int32_t n_tiles,
+                                           int64_t row_stride, int32_t pixel_type, int32_t big_endian,
+                                           int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                                           uint32_t* d_argb_out, int32_t* d_status) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (n_tiles < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "negative tile count");
+    omr_status st = check_dims(ctx, width, height, flip_h, flip_v, row_stride);
+    if (st) return st;
+    PreparedPlan pp;
+    st = prepare_plan(ctx, qdef, channels, size_c, pixel_type, pp);
+    if (st) return st;
+    if (n_tiles == 0 || width == 0 || height == 0) return OMR_OK;
+    if (pp.plan.n_active > 0 && !d_base) return fail(ctx, OMR_INVALID_ARGUMENT, "null batch base");
+    if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const RenderLayout L = layout_for(pp, 0);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    if (d_status) OMR_HIP(ctx, hipMemsetAsync(d_status, 0, sizeof(int32_t) * (size_t)n_tiles, ctx->stream));
+    const int bpp = bytes_per_pixel(pixel_type);
+    const bool aligned = vec_aligned(bpp, width, row_stride) && reinterpret_cast<uintptr_t>(d_base) % 16 == 0 &&
+                         tile_stride_bytes % 16 == 0 && channel_stride_bytes % 16 == 0 &&
+                         reinterpret_cast<uintptr_t>(d_argb_out) % 16 == 0;
+    const Strided sd{d_base, tile_stride_bytes, channel_stride_bytes};
+    return enqueue_render(ctx, pp, pixel_type, big_endian, nullptr, size_c, n_tiles, row_stride, width, height,
+                          flip_h, flip_v, d_argb_out, d_status, aligned, L, &sd);
 }
 
 omr_status omr_render_packed_int_device(omr_ctx* ctx, const omr_quantum_def* qdef,

@@ -87,6 +87,8 @@ _SIGS = {
                                             _i32, _i32, _vp]),
     "omr_render_batch_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _i32,
                                        _i32, _i32, _vp, _vp]),
+    "omr_render_batch_strided_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i64, _i32, _i64, _i32, _i32,
+                                               _i32, _i32, _i32, _i32, _vp, _vp]),
     "omr_flip_argb_device": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32]),
     "omr_flip_mask_device": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32]),
     "omr_project_stack": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32,

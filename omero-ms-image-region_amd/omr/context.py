@@ -147,6 +147,20 @@ class Context:
                                           int(flip_v), _ptr(out), _ptr(status)), self.h)
         return out
 
+    def render_batch_strided_device(self, qdef, channels, d_base, tile_stride, channel_stride, n_tiles,
+                                    pixel_type, width, height, out, status=None, big_endian=False,
+                                    flip_h=False, flip_v=False, row_stride=0, bindings=None):
+        """Batch whose planes sit at d_base + t*tile_stride + c*channel_stride (bytes)."""
+        if bindings is None:
+            bindings = make_bindings(channels)
+        arr, keep = bindings
+        check(lib.omr_render_batch_strided_device(self.h, ctypes.byref(qdef), arr, len(channels),
+                                                  _ptr(d_base), tile_stride, channel_stride, n_tiles,
+                                                  row_stride, pixel_type, int(big_endian), width,
+                                                  height, int(flip_h), int(flip_v), _ptr(out),
+                                                  _ptr(status)), self.h)
+        return out
+
     def flip_argb_device(self, src, dst, width, height, flip_h, flip_v):
         check(lib.omr_flip_argb_device(self.h, _ptr(src), _ptr(dst), width, height, int(flip_h),
                                        int(flip_v)), self.h)

@@ -59,6 +59,29 @@ def test_u16_uniform_every_lut_entry(ctx):
     np.testing.assert_array_equal(host_render(ctx, chans, planes, _lib.PIXELS_UINT16, w, h), exp)
 
 
+@pytest.mark.parametrize("pt", [_lib.PIXELS_UINT16, _lib.PIXELS_INT16])
+@pytest.mark.parametrize("windows", [
+    [(60000.3, 60010.7), (65000.5, 65001.25), (-5.0, 3.0), (0.0, 1.0)],          # steep: many skipped values
+    [(12.25, 65535.0), (-70000.0, 70000.0), (30000.0, 30000.5), (1.0, 65536.0)],
+    [(-32768.0, 32767.0), (-100.5, -99.75), (32000.0, 40000.0), (-40000.0, -32000.0)],
+])
+def test_16bit_every_index_fast_path_windows(ctx, pt, windows):
+    """Every raw 16-bit value through windows that stress the fp32 estimate + exact-proof path."""
+    h, w = 256, 256
+    rng = np.random.default_rng(99)
+    raw = [rng.permutation(65536).astype(np.uint16).reshape(h, w) for _ in range(4)]
+    planes = [r.view(np.int16) if pt == _lib.PIXELS_INT16 else r for r in raw]
+    lo, hi = (-32768, 32767) if pt == _lib.PIXELS_INT16 else (0, 65535)
+    chans = c2_channels(4)
+    for c, (s, e) in enumerate(windows):
+        chans[c].update(input_start=f32(s), input_end=f32(e), global_min=lo, global_max=hi)
+    for be in (False, True):
+        src = [p.astype(p.dtype.newbyteorder(">")) if be else p for p in planes]
+        st, exp = O.render(chans, src, pt, w, h, big_endian=be)
+        assert st == 0
+        np.testing.assert_array_equal(host_render(ctx, chans, src, pt, w, h, big_endian=be), exp)
+
+
 @pytest.mark.parametrize("pt,dtype,lo,hi", [
     (_lib.PIXELS_UINT8, np.uint8, 0, 255), (_lib.PIXELS_INT8, np.int8, -128, 127),
     (_lib.PIXELS_INT16, np.int16, -32768, 32767), (_lib.PIXELS_UINT16, np.uint16, 0, 65535)])
@@ -232,6 +255,24 @@ def test_batch_device_per_tile_status_and_results(ctx):
         if t == 3:
             continue
         s, exp = O.render(chans, big[t], _lib.PIXELS_UINT16, w, h, big_endian=True, flip_h=True)
+        np.testing.assert_array_equal(got[t], exp)
+
+
+def test_batch_strided_matches_table(ctx):
+    import torch
+    h, w, n = 48, 64, 6
+    chans = c2_channels(3)
+    tiles = [[p.astype(">u2") for p in tile_u16(200 + t, 3, h, w)] for t in range(n)]
+    raw = b"".join(p.tobytes() for t in tiles for p in t)             # big-endian bytes, [tile][chan]
+    data = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to("cuda")
+    plane = h * w * 2
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda")
+    ctx.render_batch_strided_device(O.make_qdef("rgb"), chans, data, 3 * plane, plane, n, _lib.PIXELS_UINT16, w, h,
+                                    out, big_endian=True, flip_v=True)
+    ctx.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    for t in range(n):
+        st, exp = O.render(chans, tiles[t], _lib.PIXELS_UINT16, w, h, big_endian=True, flip_v=True)
         np.testing.assert_array_equal(got[t], exp)
 
 
