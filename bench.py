@@ -112,14 +112,16 @@ def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="tiles per GPU per step")
     ap.add_argument("--unique", type=int, default=8, help="distinct synthetic tiles per GPU")
     ap.add_argument("--addr", choices=["strided", "table"], default="strided",
                     help="batch descriptor: regular [tile][channel] layout or device pointer table")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the single-tile latency probe (profiling runs: batch launches only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,7 +192,8 @@ def main():
 
     extra = {}
     if rank == 0 and world == 1:
-        extra["p50_tile_latency_ms"] = latencies(torch, omr, ctx, qdef, chans, data)
+        if not args.no_latency:
+            extra["p50_tile_latency_ms"] = latencies(torch, omr, ctx, qdef, chans, data)
         if not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             try:
