@@ -14,6 +14,7 @@
  *   OMR_NOT_FOUND        -> 404 (handler returned null, e.g. unknown format)
  *   OMR_QUANTIZATION     -> 500 (QuantizationException, ImageRegionRequestHandler.java:479)
  *   OMR_DEVICE / OMR_OOM -> 500
+ *   OMR_INTERNAL         -> 500 (unchecked exceptions the reference would throw: NPE, CCE, ...)
  *
  * Threading: one omr_ctx per worker thread.  Calls on distinct contexts may run
  * concurrently; one context must not be called concurrently.  All buffers are
@@ -41,7 +42,8 @@ enum {
     OMR_QUANTIZATION = 3,
     OMR_DEVICE = 4,
     OMR_OOM = 5,
-    OMR_BUFFER_TOO_SMALL = 6
+    OMR_BUFFER_TOO_SMALL = 6,
+    OMR_INTERNAL = 7          /* NPE / ClassCastException / IndexOutOfBounds in the reference -> 500 */
 };
 
 /* ome.model.enums.PixelsType values the path supports. */
@@ -244,6 +246,16 @@ omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int
 omr_status omr_encode_png_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
                                  int32_t height, uint8_t* out, size_t cap, size_t* out_len);
 
+/*
+ * TIFF of the 24-bit RGB view (TIFFImageWriter branch, ImageRegionRequestHandler.java:584-596):
+ * baseline uncompressed big-endian RGB, 8-bit samples, >= 8 KiB strips.  Host writer.
+ */
+size_t omr_tiff_max_bytes(int32_t width, int32_t height);
+omr_status omr_encode_tiff(omr_ctx* ctx, const uint32_t* argb, int32_t width, int32_t height,
+                           uint8_t* out, size_t cap, size_t* out_len);
+omr_status omr_encode_tiff_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
+                                  int32_t height, uint8_t* out, size_t cap, size_t* out_len);
+
 /* ---- shape mask ------------------------------------------------------------- */
 /*
  * ShapeMaskRequestHandler.renderShapeMask(Color, byte[], w, h) (:165-207): MSB-first bit mask
@@ -278,6 +290,87 @@ int32_t omr_resolution_level(int32_t n_levels, int32_t resolution);
 omr_status omr_check_plane_def(omr_region* region, int32_t size_x, int32_t size_y);
 /* LutReader: parse an ImageJ .lut file image (768 B binary, 800 B with header, or text). */
 omr_status omr_parse_lut(const uint8_t* data, size_t n, uint8_t lut_out[768]);
+
+/* ---- request decode + renderer settings (omr_request.cpp; host only) -------------------- */
+#define OMR_MAX_REQUEST_CHANNELS 64
+/* per-channel entry of omr_image_region_ctx.map_reverse (the `maps` JSON list) */
+enum { OMR_MAP_NONE = 0, OMR_MAP_REVERSE = 1, OMR_MAP_NULL = 2, OMR_MAP_BAD = 3 };
+
+/*
+ * ImageRegionCtx (ImageRegionCtx.java:44-109) after assignParams (:127-153).  has_* / -1 encode
+ * Java nulls.  windows are the Float values (:313-314); colors[i] is the raw `$...` string
+ * (HTML colour or a *.lut name).
+ */
+typedef struct omr_image_region_ctx {
+    int64_t image_id;
+    int32_t z, t;
+    int32_t has_tile;          /* tile: x/y in tile units, width/height 0 for the short form */
+    omr_region tile;
+    int32_t has_resolution, resolution;
+    int32_t has_region;
+    omr_region region;
+    int32_t n_channels;        /* -1: no 'c' parameter (channels == null) */
+    int32_t channels[OMR_MAX_REQUEST_CHANNELS];      /* signed 1-based, negative = inactive */
+    int32_t window_set[OMR_MAX_REQUEST_CHANNELS];    /* 0: Float[2]{null,null} */
+    float windows[OMR_MAX_REQUEST_CHANNELS][2];
+    int32_t color_set[OMR_MAX_REQUEST_CHANNELS];     /* 0: colour null */
+    char colors[OMR_MAX_REQUEST_CHANNELS][64];
+    int32_t model;             /* -1 null, OMR_MODEL_GREYSCALE ("g"), OMR_MODEL_RGB ("c") */
+    int32_t has_quality;
+    float quality;
+    int32_t inverted_axis;     /* -1 null, 0/1 (parsed, unused, :93-97) */
+    int32_t projection;        /* -1 null, OMR_PROJECTION_* */
+    int32_t has_projection_start, projection_start;
+    int32_t has_projection_end, projection_end;
+    int32_t n_maps;            /* -1: no `maps` parameter */
+    int32_t map_reverse[OMR_MAX_REQUEST_CHANNELS];   /* OMR_MAP_* per list element */
+    int32_t flip_h, flip_v;
+    char format[16];           /* default "jpeg" */
+    char cache_key[17];        /* Guava sipHash24 hex of the sorted parameters (:165-177) */
+} omr_image_region_ctx;
+
+/* ShapeMaskCtx (ShapeMaskCtx.java:38-81). */
+typedef struct omr_shape_mask_ctx {
+    int64_t shape_id;
+    int32_t has_color;
+    char color[64];
+    int32_t flip_h, flip_v;
+    char cache_key[128];       /* "ome.model.roi.Mask:<id>:<color>" (:77-81) */
+} omr_shape_mask_ctx;
+
+/*
+ * new ImageRegionCtx(params, key) (ImageRegionCtx.java:122-153).  names/values: the request's
+ * MultiMap entries in insertion order (case-insensitive names, first value wins).
+ * OMR_INVALID_ARGUMENT = IllegalArgumentException (400); OMR_INTERNAL = an unchecked exception
+ * the reference does not catch (500).  err (optional) receives the message.
+ */
+omr_status omr_image_region_ctx_parse(const char* const* names, const char* const* values, int32_t n,
+                                      omr_image_region_ctx* out, char* err, size_t err_cap);
+/* new ShapeMaskCtx(params, key) (ShapeMaskCtx.java:61-72); bad shapeId -> OMR_INTERNAL (500). */
+omr_status omr_shape_mask_ctx_parse(const char* const* names, const char* const* values, int32_t n,
+                                    omr_shape_mask_ctx* out, char* err, size_t err_cap);
+
+/* LutProviderImpl (LutProviderImpl.java:29-75): *.lut files under root, keyed by basename. */
+typedef struct omr_lut_provider omr_lut_provider;
+omr_status     omr_lut_provider_create(const char* root, omr_lut_provider** out);
+void           omr_lut_provider_destroy(omr_lut_provider* p);
+int32_t        omr_lut_provider_count(const omr_lut_provider* p);
+omr_status     omr_lut_provider_add(omr_lut_provider* p, const char* name, const uint8_t lut_rgb768[768]);
+/* 768-byte R[256] G[256] B[256] table owned by the provider, or NULL (getLutReaders -> null). */
+const uint8_t* omr_lut_provider_get(const omr_lut_provider* p, const char* name);
+
+/* createRenderingDef (ImageRegionRequestHandler.java:258-300) for size_c channels. */
+omr_status omr_create_rendering_def(int32_t pixel_type, int32_t size_c, omr_quantum_def* qdef,
+                                    omr_channel_binding* channels);
+/*
+ * updateSettings (ImageRegionRequestHandler.java:689-741) applied to a rendering def: active
+ * flags, windows, colours or LUTs (luts may be NULL), reverse-intensity maps, model.
+ * Reference failures (null channels / window / colour / model, short lists, bad maps entries)
+ * return OMR_INTERNAL (500).
+ */
+omr_status omr_update_settings(const omr_image_region_ctx* ctx, int32_t size_c, omr_quantum_def* qdef,
+                               omr_channel_binding* channels, const omr_lut_provider* luts,
+                               char* err, size_t err_cap);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,10 @@ from ._lib import OmrError
 from .context import Context
 from .renderer import (ChannelSettings, Renderer, ReverseIntensityContext, create_rendering_def,
                        flip, split_html_color)
+from .request import (ImageRegionCtx, ImageRegionRequestHandler, InMemoryPixelBuffer, LutProvider,
+                      RequestError, ShapeMaskCtx, ShapeMaskRequestHandler)
 
 __all__ = ["_lib", "OmrError", "Context", "Renderer", "ChannelSettings", "ReverseIntensityContext",
-           "create_rendering_def", "flip", "split_html_color"]
+           "create_rendering_def", "flip", "split_html_color", "ImageRegionCtx",
+           "ImageRegionRequestHandler", "InMemoryPixelBuffer", "LutProvider", "RequestError",
+           "ShapeMaskCtx", "ShapeMaskRequestHandler"]

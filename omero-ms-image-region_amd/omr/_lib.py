@@ -25,9 +25,14 @@ except Exception:  # no torch: libomr.so uses /opt/rocm's runtime (the Java/FFI 
 lib = ctypes.CDLL(LIB_PATH)
 
 # ---- enums (omr.h) ----------------------------------------------------------------------
-OK, INVALID_ARGUMENT, NOT_FOUND, QUANTIZATION, DEVICE, OOM, BUFFER_TOO_SMALL = range(7)
+OK, INVALID_ARGUMENT, NOT_FOUND, QUANTIZATION, DEVICE, OOM, BUFFER_TOO_SMALL, INTERNAL = range(8)
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARGUMENT", 2: "NOT_FOUND", 3: "QUANTIZATION", 4: "DEVICE",
-                5: "OOM", 6: "BUFFER_TOO_SMALL"}
+                5: "OOM", 6: "BUFFER_TOO_SMALL", 7: "INTERNAL"}
+# HTTP status the reference answers with for each outcome
+HTTP_STATUS = {OK: 200, INVALID_ARGUMENT: 400, NOT_FOUND: 404, QUANTIZATION: 500, DEVICE: 500,
+               OOM: 500, BUFFER_TOO_SMALL: 500, INTERNAL: 500}
+MAX_REQUEST_CHANNELS = 64
+MAP_NONE, MAP_REVERSE, MAP_NULL, MAP_BAD = range(4)
 PIXELS_INT8, PIXELS_UINT8, PIXELS_INT16, PIXELS_UINT16, PIXELS_INT32, PIXELS_UINT32, \
     PIXELS_FLOAT, PIXELS_DOUBLE = range(8)
 FAMILY_LINEAR, FAMILY_POLYNOMIAL, FAMILY_LOGARITHMIC, FAMILY_EXPONENTIAL = range(4)
@@ -58,6 +63,33 @@ class ChannelBinding(ctypes.Structure):
 class Region(ctypes.Structure):
     _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+_NCH = 64
+
+
+class ImageRegionCtxStruct(ctypes.Structure):
+    _fields_ = [("image_id", ctypes.c_int64), ("z", ctypes.c_int32), ("t", ctypes.c_int32),
+                ("has_tile", ctypes.c_int32), ("tile", Region),
+                ("has_resolution", ctypes.c_int32), ("resolution", ctypes.c_int32),
+                ("has_region", ctypes.c_int32), ("region", Region),
+                ("n_channels", ctypes.c_int32), ("channels", ctypes.c_int32 * _NCH),
+                ("window_set", ctypes.c_int32 * _NCH), ("windows", (ctypes.c_float * 2) * _NCH),
+                ("color_set", ctypes.c_int32 * _NCH), ("colors", (ctypes.c_char * 64) * _NCH),
+                ("model", ctypes.c_int32), ("has_quality", ctypes.c_int32),
+                ("quality", ctypes.c_float), ("inverted_axis", ctypes.c_int32),
+                ("projection", ctypes.c_int32), ("has_projection_start", ctypes.c_int32),
+                ("projection_start", ctypes.c_int32), ("has_projection_end", ctypes.c_int32),
+                ("projection_end", ctypes.c_int32), ("n_maps", ctypes.c_int32),
+                ("map_reverse", ctypes.c_int32 * _NCH), ("flip_h", ctypes.c_int32),
+                ("flip_v", ctypes.c_int32), ("format", ctypes.c_char * 16),
+                ("cache_key", ctypes.c_char * 17)]
+
+
+class ShapeMaskCtxStruct(ctypes.Structure):
+    _fields_ = [("shape_id", ctypes.c_int64), ("has_color", ctypes.c_int32),
+                ("color", ctypes.c_char * 64), ("flip_h", ctypes.c_int32),
+                ("flip_v", ctypes.c_int32), ("cache_key", ctypes.c_char * 128)]
 
 
 _vp = ctypes.c_void_p
@@ -102,6 +134,9 @@ _SIGS = {
     "omr_encode_jpeg": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_encode_jpeg_device": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_jpeg_quant_tables": (_i32, [_f32, _vp, _vp]),
+    "omr_tiff_max_bytes": (_sz, [_i32, _i32]),
+    "omr_encode_tiff": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_encode_tiff_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_encode_png": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_encode_png_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_render_shape_mask_png": (_i32, [_vp, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp, _sz,
@@ -113,6 +148,17 @@ _SIGS = {
     "omr_resolution_level": (_i32, [_i32, _i32]),
     "omr_check_plane_def": (_i32, [ctypes.POINTER(Region), _i32, _i32]),
     "omr_parse_lut": (_i32, [_vp, _sz, _vp]),
+    "omr_image_region_ctx_parse": (_i32, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                          _i32, ctypes.POINTER(ImageRegionCtxStruct), _vp, _sz]),
+    "omr_shape_mask_ctx_parse": (_i32, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                        _i32, ctypes.POINTER(ShapeMaskCtxStruct), _vp, _sz]),
+    "omr_lut_provider_create": (_i32, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "omr_lut_provider_destroy": (None, [_vp]),
+    "omr_lut_provider_count": (_i32, [_vp]),
+    "omr_lut_provider_add": (_i32, [_vp, ctypes.c_char_p, _vp]),
+    "omr_lut_provider_get": (_vp, [_vp, ctypes.c_char_p]),
+    "omr_create_rendering_def": (_i32, [_i32, _i32, _QD, _CB]),
+    "omr_update_settings": (_i32, [ctypes.POINTER(ImageRegionCtxStruct), _i32, _QD, _CB, _vp, _vp, _sz]),
 }
 
 MISSING = []

@@ -222,6 +222,15 @@ class Context:
         return self._encode(lib.omr_encode_png_device, d_argb, width, height,
                             cap=lib.omr_png_max_bytes(width, height, 3))
 
+    def encode_tiff(self, argb, width, height):
+        argb = np.ascontiguousarray(argb, dtype=np.uint32)
+        return self._encode(lib.omr_encode_tiff, argb, width, height,
+                            cap=lib.omr_tiff_max_bytes(width, height))
+
+    def encode_tiff_device(self, d_argb, width, height):
+        return self._encode(lib.omr_encode_tiff_device, d_argb, width, height,
+                            cap=lib.omr_tiff_max_bytes(width, height))
+
     def render_shape_mask_png(self, bits, width, height, rgba, flip_h=False, flip_v=False):
         bits = np.frombuffer(bytes(bits), dtype=np.uint8).copy()
         col = (ctypes.c_uint8 * 4)(*[int(v) for v in rgba])

@@ -19,6 +19,7 @@ import numpy as np
 from . import _lib
 from ._lib import lib
 from .context import make_qdef
+from .request import LutProvider  # noqa: F401  (C-backed LutProviderImpl, omr_request.cpp)
 
 # StatsFactory.initPixelsRange: the channel window defaults to the pixel-type range.
 TYPE_RANGE = {
@@ -88,29 +89,6 @@ class RenderingDef:
 
 def create_rendering_def(pixel_type, size_c):
     return RenderingDef(pixel_type, size_c)
-
-
-class LutProvider:
-    """LutProviderImpl (LutProviderImpl.java:29-75): every *.lut under a root, by basename."""
-
-    def __init__(self, root=None):
-        self.luts = {}
-        if root and os.path.isdir(root):
-            for dirpath, _, files in os.walk(root):
-                for fn in files:
-                    if fn.lower().endswith(".lut"):
-                        with open(os.path.join(dirpath, fn), "rb") as fh:
-                            data = fh.read()
-                        table = parse_lut(data)
-                        if table is not None:
-                            self.luts[fn] = table
-
-    def get(self, name):
-        return self.luts.get(name)
-
-    def get_lut_readers(self, bindings):
-        """Readers for ACTIVE channels only, None where a channel has no LUT (:63-73)."""
-        return [self.luts.get(b.lut_name) for b in bindings if b.active]
 
 
 def parse_lut(data):
