@@ -109,6 +109,115 @@ def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
             "host_fed": round(1e3 * float(np.median(t_host)), 4)}
 
 
+def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_cpu):
+    """render_image_region's default output (format=jpeg, ImageRegionRequestHandler.java:580-582)
+    on whole batches: render batch -> batched JPEG (device-resident in, device JPEG files out).
+    C2->JPEG on the C2 tiles, and BASELINE configs[0] (C1: 1-channel uint8 1024^2 greyscale,
+    uniform [0,255], q=0.9).  Per-kernel HIP-event timings: K2 render (2), J1 FDCT (5),
+    J3 Huffman (6), whole JPEG pipeline (4)."""
+    import numpy as np
+    from omr import _lib
+    from omr.context import make_bindings, make_qdef
+    from omr.synthetic import c2_channels
+    dev = data.device
+    q = 0.9
+    res = {}
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261015)
+    u8 = torch.randint(0, 256, (B, TILE, TILE), dtype=torch.uint8, device=dev, generator=g)
+    c1 = [{"input_start": 0.0, "input_end": 255.0, "global_min": 0.0, "global_max": 255.0}]
+    cases = {
+        "c2_u16_4ch_rgb_to_jpeg": (make_qdef("rgb"), c2_channels(CHANNELS), data, _lib.PIXELS_UINT16,
+                                   CHANNELS * TILE * TILE * 2, TILE * TILE * 2, True),
+        "c1_u8_grey_to_jpeg": (make_qdef("greyscale"), c1, u8, _lib.PIXELS_UINT8, TILE * TILE, TILE * TILE, False),
+    }
+    argb = torch.empty((B, TILE, TILE), dtype=torch.int32, device=dev)
+    cap = B * (TILE * TILE * 3)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    offs = torch.empty(B, dtype=torch.int64, device=dev)
+    lens = torch.empty(B, dtype=torch.int32, device=dev)
+    stat = torch.empty(B, dtype=torch.int32, device=dev)
+    for name, (qd, chans, src, pt, tstride, cstride, be) in cases.items():
+        binds = make_bindings(chans)
+
+        def step():
+            ctx.render_batch_strided_device(qd, chans, src, tstride, cstride, B, pt, TILE, TILE, argb,
+                                            big_endian=be, bindings=binds)
+            ctx.encode_jpeg_batch_device(argb, B, TILE, TILE, q, d_out, offs, lens, stat)
+        for _ in range(warmup):
+            step()
+        ctx.synchronize()
+        ctx.kernel_timings()
+        ctx.enable_kernel_timing(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ctx.synchronize()
+        el = time.perf_counter() - t0
+        ctx.enable_kernel_timing(False)
+        tm = {}
+        for ms, kind in ctx.kernel_timings():
+            tm.setdefault(kind, []).append(ms)
+        avg = {k: sum(v) / len(v) for k, v in tm.items()}
+        ln = lens.cpu().numpy().astype(np.int64)
+        assert (stat.cpu().numpy() == 0).all(), "JPEG batch did not fit its buffer"
+        px = TILE * TILE
+        nblk = (TILE // 16) ** 2 * 6
+        j1_bytes = B * (px * 4 + nblk * (128 + 4))               # ARGB in; coefs + aclen + dc out
+        j3_bytes = B * nblk * (128 + 2 + 4) + int(ln.sum())     # coefs + dc + offsets in; bitstream out
+        res[name] = {
+            "tiles_per_s": round(B * steps / el, 1),
+            "ms_per_step": round(1e3 * el / steps, 4),
+            "tiles_per_step": B,
+            "quality": q,
+            "mean_jpeg_bytes": int(ln.mean()),
+            "kernel_ms": {"render_K2": round(avg.get(2, float("nan")), 5),
+                          "jpeg_total": round(avg.get(4, float("nan")), 5),
+                          "J1_fdct": round(avg.get(5, float("nan")), 5),
+                          "J3_huffman": round(avg.get(6, float("nan")), 5)},
+            "J1_hbm_gbs": round(j1_bytes / (avg.get(5, float("nan")) * 1e-3) / 1e9, 1),
+            "J3_hbm_gbs": round(j3_bytes / (avg.get(6, float("nan")) * 1e-3) / 1e9, 1),
+        }
+        if with_cpu:
+            try:
+                res[name]["cpu_baseline"] = jpeg_cpu_baseline(torch, name, src, chans, pt, be, q,
+                                                              cpu_seconds, threads)
+            except Exception as e:
+                log(f"jpeg cpu baseline failed: {e}")
+    return res
+
+
+def jpeg_cpu_baseline(torch, name, src, chans, pt, be, q, seconds, threads):
+    """CPU restatement render + JPEG per request on a thread pool (ctypes releases the GIL)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    import oracle_lib
+    model = "greyscale" if len(chans) == 1 else "rgb"
+    host = src[:4].cpu().numpy()
+    if host.ndim == 4:
+        tiles = [[np.ascontiguousarray(host[t, c]) for c in range(host.shape[1])] for t in range(host.shape[0])]
+    else:
+        tiles = [[np.ascontiguousarray(host[t])] for t in range(host.shape[0])]
+
+    def one(i):
+        st, argb = oracle_lib.render(chans, tiles[i % len(tiles)], pt, TILE, TILE, model=model, big_endian=be)
+        return len(oracle_lib.encode_jpeg(argb, TILE, TILE, q))
+
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, range(threads)))
+        first = time.perf_counter() - t0
+        n = max(threads, int(threads * seconds / max(first, 1e-3)) // threads * threads)
+        t0 = time.perf_counter()
+        list(ex.map(one, range(n)))
+        secs = time.perf_counter() - t0
+    return {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "sample": f"{n} tiles ({name}: render + JPEG q={q}) in {secs:.2f} s on {threads} threads "
+                      f"(oracle/omr_oracle.c, -O3)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,6 +232,9 @@ def main():
                     help="batch descriptor: regular [tile][channel] layout or device pointer table")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-jpeg", action="store_true", help="skip the render->JPEG batch section")
+    ap.add_argument("--jpeg-batch", type=int, default=64, help="tiles per JPEG step")
+    ap.add_argument("--jpeg-steps", type=int, default=10)
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-tile latency probe (profiling runs: batch launches only)")
     args = ap.parse_args()
@@ -202,8 +314,11 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_latency:
             extra["p50_tile_latency_ms"] = latencies(torch, omr, ctx, qdef, chans, data)
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        if not args.no_jpeg:
+            extra["jpeg"] = jpeg_section(torch, ctx, data, min(args.jpeg_batch, B), args.jpeg_steps,
+                                         2, args.cpu_seconds / 2, threads, not args.no_cpu_baseline)
         if not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             try:
                 extra["cpu_baseline"] = cpu_baseline(torch, uniq, args.cpu_seconds, threads)
             except Exception as e:  # the baseline is reported, never the target

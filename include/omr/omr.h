@@ -237,6 +237,23 @@ omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, in
 omr_status omr_encode_jpeg_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
                                   int32_t height, float quality, uint8_t* out, size_t cap,
                                   size_t* out_len);
+/*
+ * Batched JPEG (same encoder, byte-identical per tile) of n_tiles device ARGB tiles
+ * (tile i at d_argb + i*tile_stride_px; 0 = width*height), e.g. the output of
+ * omr_render_batch_*_device.  Complete JFIF files are packed back to back in d_out
+ * (capacity out_cap bytes): file i at d_out + d_offsets[i], d_lengths[i] bytes (0 and
+ * d_status[i] = OMR_BUFFER_TOO_SMALL when it did not fit; d_status optional).
+ * Asynchronous on the context stream; width, height <= 4096.  This is the batch form of the
+ * per-request compressToStream calls (ImageRegionRequestHandler.java:580-582).
+ */
+omr_status omr_encode_jpeg_batch_device(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
+                                        int32_t n_tiles, int32_t width, int32_t height, float quality,
+                                        uint8_t* d_out, size_t out_cap, uint64_t* d_offsets,
+                                        uint32_t* d_lengths, int32_t* d_status);
+/* Same, host output: files packed in out (cap bytes), offsets/lengths host arrays; synchronous. */
+omr_status omr_encode_jpeg_batch(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
+                                 int32_t n_tiles, int32_t width, int32_t height, float quality,
+                                 uint8_t* out, size_t cap, uint64_t* offsets, uint32_t* lengths);
 /* Java ImageIO quality -> quantisation tables (natural order), JPEGQTable.getScaledInstance. */
 omr_status omr_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]);
 

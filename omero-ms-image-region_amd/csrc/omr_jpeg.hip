@@ -615,3 +615,660 @@ omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, in
 }
 
 }  // extern "C"
+
+// =====================================================================================
+// Batched JPEG: N same-size tiles per call, wave-parallel Huffman, one host sync at most.
+//
+// The reference encodes every tile on its own worker thread (compressToStream per request,
+// ImageRegionRequestHandler.java:580-582).  Here a whole batch of rendered tiles (e.g. the
+// output of omr_render_batch_*_device) is encoded by six launches whose grids span all tiles:
+//   B1  k_jpeg_fdct_batch   one wave per MCU: colour, downsample, FDCT, quantise (zig-zag lane
+//                           order), plus each block's AC Huffman length by ballot arithmetic
+//   B2  k_jpeg_block_scan   one workgroup per tile: DC lengths, exclusive scan -> block bit
+//                           offsets, tile bit length, zero the tile's word slot
+//   B3  k_jpeg_huff_batch   one wave per block: every lane emits its coefficient's symbol,
+//                           a wave scan places the bits, the block is assembled in LDS and
+//                           stored (boundary words by atomicOr)
+//   B4  k_jpeg_stuff_scan   one workgroup per tile: 0xFF count per 16-byte chunk -> chunk
+//                           output offsets, stuffed length
+//   B5  k_jpeg_tile_scan    one workgroup: tile output offsets (header + scan + EOI), status
+//   B6  k_jpeg_stuff_batch  stuffed bytes staged in LDS, copied out coalesced; JFIF header
+// Output: complete JFIF files packed back to back in the caller's device buffer.
+// =====================================================================================
+
+namespace omr {
+
+struct HuffLds {
+    uint16_t code[4][256];
+    uint8_t size[4][256];
+};
+
+__device__ __forceinline__ void load_huff_lds(HuffLds& h) {
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        h.code[i >> 8][i & 255] = c_huff[i >> 8].code[i & 255];
+        h.size[i >> 8][i & 255] = c_huff[i >> 8].size[i & 255];
+    }
+}
+
+// Inclusive wave64 prefix sum on DPP (row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 across rows): no LDS traffic, unlike __shfl_up (ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
+}
+
+__device__ __forceinline__ uint32_t wave_exclusive(uint32_t v, uint32_t& total) {
+    const uint32_t x = wave_incl_scan(v);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+    return x - v;
+}
+
+// Exact t / d for 0 <= t < 2^16, 1 <= d <= 2040 by one high multiply with m = ceil(2^32 / d):
+// n*m/2^32 exceeds n/d by < 2^-16 < 1/d, so the floor never crosses an integer.
+__device__ __forceinline__ int quant_recip(int t, int half, uint32_t m) {
+    if (t < 0) return -(int)__umulhi((uint32_t)(-t + half), m);
+    return (int)__umulhi((uint32_t)(t + half), m);
+}
+
+__constant__ uint8_t c_zigzag[64] = {
+    0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
+    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28,
+    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+struct B1Args {
+    const uint32_t* argb;
+    int64_t tile_stride;  // pixels between tiles
+    int16_t* coefs;       // [tile][nb][64] zig-zag order
+    uint16_t* aclen;      // [tile][nb] AC bits incl. ZRL/EOB
+    int16_t* dcs;         // [tile][nb] DC after dummy-block propagation
+    int32_t W, H, mcux, n_mcu, nb;
+    QTabs qt;
+};
+
+constexpr int kB1McuPerWave = 4;
+
+// Pixels (x, y) and (x+1, y) of one row (clamped to the image), as one 8-byte load when both
+// are inside the row.
+__device__ __forceinline__ void load_pair(const uint32_t* img, int W, int x, int y, uint32_t& a, uint32_t& b) {
+    const uint32_t* r = img + (int64_t)y * W;
+    if (x + 1 < W) {
+        const uint2 v = *reinterpret_cast<const uint2*>(r + x);   // x even, W*y even when W even
+        a = v.x; b = v.y;
+    } else {
+        a = r[min(x, W - 1)]; b = a;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
+    __shared__ int s[4][6 * 64 + 8];
+    __shared__ uint8_t s_acsize[2][256];
+    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int tile = blockIdx.y;
+    int* S = s[wv];
+    const int W = A.W, H = A.H;
+    // 8-byte pixel-pair loads need every row start 8-byte aligned
+    const bool even_w = (W & 1) == 0 && (A.tile_stride & 1) == 0 && ((uintptr_t)A.argb & 7) == 0;
+    const int cx = lane & 7, cy = lane >> 3;
+    const uint32_t* img = A.argb + (int64_t)tile * A.tile_stride;
+    const int ywib = (W + 7) / 8, yhib = (H + 7) / 8;
+    const int nat = c_zigzag[lane];                 // this lane owns zig-zag position `lane`
+    const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
+    const uint32_t my_ = (uint32_t)((0x100000000ull + (uint64_t)(qy << 3) - 1) / (uint64_t)(qy << 3));
+    const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
+    const int hy = qy << 2, hc = qc << 2;
+    const int m0 = (blockIdx.x * 4 + wv) * kB1McuPerWave;
+    for (int m = m0; m < min(m0 + kB1McuPerWave, A.n_mcu); ++m) {   // wave-uniform loop
+        const int mx = m % A.mcux, my = m / A.mcux;
+        {
+            const int x0 = mx * 16 + 2 * cx, y0 = my * 16 + 2 * cy;
+            const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
+            uint32_t p00, p01, p10, p11;
+            if (even_w) {
+                load_pair(img, W, min(x0, W - 1) & ~1, ya, p00, p01);
+                load_pair(img, W, min(x0, W - 1) & ~1, yb, p10, p11);
+                if (x0 > W - 1) { p00 = p01; p10 = p11; }           // both columns clamp to W-1
+            } else {
+                const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
+                p00 = img[(int64_t)ya * W + xa]; p01 = img[(int64_t)ya * W + xb];
+                p10 = img[(int64_t)yb * W + xa]; p11 = img[(int64_t)yb * W + xb];
+            }
+            int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
+            const int blk = (cy >> 2) * 2 + (cx >> 2);
+            const int o = ((2 * cy) & 7) * 8 + ((2 * cx) & 7);
+            ycc(p00, y, cb0, cr0); S[blk * 64 + o] = y - 128;
+            ycc(p01, y, cb1, cr1); S[blk * 64 + o + 1] = y - 128;
+            ycc(p10, y, cb2, cr2); S[blk * 64 + o + 8] = y - 128;
+            ycc(p11, y, cb3, cr3); S[blk * 64 + o + 9] = y - 128;
+            const int chv = (H + 1) / 2;
+            const int cyg = my * 8 + cy;
+            if (cyg >= chv) {
+                const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
+                const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
+                p00 = img[(int64_t)r0 * W + xa]; p01 = img[(int64_t)r0 * W + xb];
+                p10 = img[(int64_t)r1 * W + xa]; p11 = img[(int64_t)r1 * W + xb];
+                ycc(p00, y, cb0, cr0); ycc(p01, y, cb1, cr1); ycc(p10, y, cb2, cr2); ycc(p11, y, cb3, cr3);
+            }
+            const int bias = (cx & 1) ? 2 : 1;
+            S[4 * 64 + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
+            S[5 * 64 + cy * 8 + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane < 48) fdct8<0>(S + (lane >> 3) * 64 + (lane & 7) * 8, 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane < 48) fdct8<1>(S + (lane >> 3) * 64 + (lane & 7), 8);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int64_t b0 = (int64_t)tile * A.nb + (int64_t)m * 6;
+        int16_t* out = A.coefs + b0 * 64;
+        int dc[6];
+        uint32_t aclen[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            int q = k < 4 ? quant_recip(S[k * 64 + nat], hy, my_) : quant_recip(S[k * 64 + nat], hc, mc_);
+            if (k < 4) {
+                const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
+                if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
+            }
+            dc[k] = q;
+            if (lane != 0) out[k * 64 + lane] = (int16_t)q;
+            // AC Huffman length: run of zeros before this coefficient from the previous non-zero
+            const uint64_t nz = __ballot(lane != 0 && q != 0);
+            const int t = k < 4 ? 0 : 1;
+            uint32_t bits = 0;
+            if (lane != 0 && q != 0) {
+                const uint64_t below = nz & ((1ull << lane) - 1);
+                const int prev = below ? 63 - __clzll(below) : 0;
+                const int r = lane - prev - 1;
+                const int a = q < 0 ? -q : q;
+                const int nbits = 32 - __clz(a);
+                bits = (uint32_t)((r >> 4) * s_acsize[t][0xF0] + s_acsize[t][((r & 15) << 4) | nbits] + nbits);
+            }
+            if (lane == 0 && (nz >> 63) == 0) bits += s_acsize[t][0x00];   // EOB after the last non-zero
+            aclen[k] = wave_sum(bits);
+        }
+        if (lane == 0) {   // jccoefct.c dummy-block DC propagation
+            const bool c1 = mx * 2 + 1 >= ywib, row1 = my * 2 + 1 >= yhib;
+            if (c1) dc[1] = dc[0];
+            if (row1) { dc[2] = dc[1]; dc[3] = dc[1]; }
+            else if (c1) dc[3] = dc[2];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                out[k * 64] = (int16_t)dc[k];
+                A.dcs[b0 + k] = (int16_t)dc[k];
+                A.aclen[b0 + k] = (uint16_t)aclen[k];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+__device__ __forceinline__ int prev_block_in_tile(int b) {
+    const int m = b / 6, k = b - m * 6;
+    if (k == 1 || k == 2 || k == 3) return b - 1;
+    if (m == 0) return -1;
+    return k == 0 ? (m - 1) * 6 + 3 : (m - 1) * 6 + k;
+}
+
+__device__ __forceinline__ uint32_t dc_bits(const int16_t* dcs, int b, const HuffLds& h) {
+    const int pb = prev_block_in_tile(b);
+    int d = dcs[b] - (pb >= 0 ? dcs[pb] : 0);
+    if (d < 0) d = -d;
+    const int nbits = d ? 32 - __clz(d) : 0;
+    const int t = (b % 6) < 4 ? 0 : 2;
+    return h.size[t][nbits] + nbits;
+}
+
+constexpr int kTileThreads = 1024;
+
+struct B2Args {
+    const uint16_t* aclen;
+    const int16_t* dcs;
+    uint32_t* offs;        // [tile][nb] bit offset of each block inside its tile
+    uint32_t* tile_bits;   // [tile]
+    uint32_t* words;       // [tile][slot_words]
+    int32_t nb;
+    int64_t slot_words;
+};
+
+__global__ void __launch_bounds__(kTileThreads) k_jpeg_block_scan(B2Args A) {
+    __shared__ HuffLds h;
+    __shared__ uint32_t sw[16];
+    load_huff_lds(h);
+    __syncthreads();
+    const int tile = blockIdx.x;
+    const uint16_t* acl = A.aclen + (int64_t)tile * A.nb;
+    const int16_t* dcs = A.dcs + (int64_t)tile * A.nb;
+    uint32_t* offs = A.offs + (int64_t)tile * A.nb;
+    const int per = (A.nb + kTileThreads - 1) / kTileThreads;
+    const int i0 = min(A.nb, (int)threadIdx.x * per), i1 = min(A.nb, i0 + per);
+    uint32_t sum = 0;
+    for (int b = i0; b < i1; ++b) sum += acl[b] + dc_bits(dcs, b, h);
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(sum, sw, total);
+    for (int b = i0; b < i1; ++b) {
+        offs[b] = run;
+        run += acl[b] + dc_bits(dcs, b, h);
+    }
+    if (threadIdx.x == 0) A.tile_bits[tile] = total;
+    const uint32_t nw = (total + 31) / 32 + 1;
+    uint32_t* w = A.words + (int64_t)tile * A.slot_words;
+    for (uint32_t i = threadIdx.x; i < nw; i += kTileThreads) w[i] = 0;
+}
+
+struct B3Args {
+    const int16_t* coefs;
+    const int16_t* dcs;
+    const uint32_t* offs;
+    uint32_t* words;
+    int32_t nb;
+    int64_t slot_words;
+};
+
+constexpr int kBlkWords = 132;   // <= 64 lanes x 63 bits + 31 bits of start offset
+
+constexpr int kB3BlocksPerWave = 16;
+
+__global__ void __launch_bounds__(256) k_jpeg_huff_batch(B3Args A) {
+    __shared__ HuffLds h;
+    __shared__ uint32_t sbuf[4][kBlkWords];
+    load_huff_lds(h);
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    uint32_t* buf = sbuf[wv];
+    const int tile = blockIdx.y;
+    const int bbeg = (blockIdx.x * 4 + wv) * kB3BlocksPerWave;
+    const int bend = min(bbeg + kB3BlocksPerWave, A.nb);
+    const int16_t* tdcs = A.dcs + (int64_t)tile * A.nb;
+    uint32_t* twords = A.words + (int64_t)tile * A.slot_words;
+    for (int b = bbeg; b < bend; ++b) {                   // wave-uniform
+        for (int i = lane; i < kBlkWords; i += 64) buf[i] = 0;
+        const int64_t gb = (int64_t)tile * A.nb + b;
+        const int v = A.coefs[gb * 64 + lane];
+        const int k = b % 6;
+        const int td = k < 4 ? 0 : 2, ta = td + 1;
+        const uint64_t nz = __ballot(lane != 0 && v != 0);
+        const int last = nz ? 63 - __clzll(nz) : 0;
+        uint64_t code = 0;
+        uint32_t len = 0;
+        auto put = [&](uint32_t c, uint32_t n) { code = (code << n) | (c & ((1u << n) - 1)); len += n; };
+        if (lane == 0) {
+            const int pb = prev_block_in_tile(b);
+            int d = v - (pb >= 0 ? tdcs[pb] : 0);
+            int d2 = d;
+            if (d < 0) { d = -d; d2--; }
+            const int nbits = d ? 32 - __clz(d) : 0;
+            put(h.code[td][nbits], h.size[td][nbits]);
+            if (nbits) put((uint32_t)d2, nbits);
+        } else if (v != 0) {
+            const uint64_t below = nz & ((1ull << lane) - 1);
+            const int prev = below ? 63 - __clzll(below) : 0;
+            int r = lane - prev - 1;
+            while (r > 15) { put(h.code[ta][0xF0], h.size[ta][0xF0]); r -= 16; }
+            int a = v, a2 = v;
+            if (a < 0) { a = -a; a2--; }
+            const int nbits = 32 - __clz(a);
+            const int sym = (r << 4) + nbits;
+            put(h.code[ta][sym], h.size[ta][sym]);
+            put((uint32_t)a2, nbits);
+        }
+        if (lane == last && last < 63) put(h.code[ta][0], h.size[ta][0]);   // EOB
+        uint32_t blen;
+        const uint32_t pre = wave_exclusive(len, blen);
+        const uint32_t boff = A.offs[gb];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (len) {
+            const uint32_t p = (boff & 31) + pre;            // local bit position in buf
+            const uint32_t w0 = p >> 5, sh = p & 31;
+            const uint64_t hi = code << (64 - len);          // MSB-aligned, len >= 1
+            atomicOr(&buf[w0], (uint32_t)(hi >> 32) >> sh);
+            if (sh + len > 32) {
+                const uint64_t rest = hi << (32 - sh);
+                atomicOr(&buf[w0 + 1], (uint32_t)(rest >> 32));
+                if (sh + len > 64) atomicOr(&buf[w0 + 2], (uint32_t)rest);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t nwords = ((boff & 31) + blen + 31) >> 5;
+        uint32_t* dst = twords + (boff >> 5);
+        for (uint32_t i = lane; i < nwords; i += 64) {
+            const uint32_t wv2 = buf[i];
+            if (i == 0 || i == nwords - 1) atomicOr(&dst[i], wv2);
+            else dst[i] = wv2;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // buf is cleared for the next block
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+constexpr int kStuffBytes = 16;   // bytes per chunk in B4/B6
+
+__device__ __forceinline__ uint32_t seg_byte(const uint32_t* words, uint32_t i, uint32_t nbytes, uint32_t tb) {
+    uint32_t b = (words[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
+    if (i == nbytes - 1 && (tb & 7)) b |= 0xFFu >> (tb & 7);   // jchuff flush: pad with 1s
+    return b;
+}
+
+struct B4Args {
+    const uint32_t* words;
+    const uint32_t* tile_bits;
+    uint32_t* chunk_off;   // [tile][slot_chunks] stuffed byte offset of each chunk
+    uint32_t* stuffed;     // [tile] stuffed entropy-coded length
+    int64_t slot_words, slot_chunks;
+};
+
+__global__ void __launch_bounds__(kTileThreads) k_jpeg_stuff_scan(B4Args A) {
+    __shared__ uint32_t sw[16];
+    __shared__ uint32_t carry;
+    const int tile = blockIdx.x;
+    const uint32_t tb = A.tile_bits[tile], nbytes = (tb + 7) / 8;
+    const uint32_t nch = (nbytes + kStuffBytes - 1) / kStuffBytes;
+    const uint32_t* words = A.words + (int64_t)tile * A.slot_words;
+    uint32_t* co = A.chunk_off + (int64_t)tile * A.slot_chunks;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nch; base += kTileThreads) {
+        const uint32_t c = base + threadIdx.x;
+        uint32_t n = 0;
+        if (c < nch) {
+            const uint32_t e = min(nbytes, (c + 1) * kStuffBytes);
+            for (uint32_t i = c * kStuffBytes; i < e; ++i) n += seg_byte(words, i, nbytes, tb) == 0xFF;
+        }
+        uint32_t total;
+        const uint32_t ex = block_exclusive_scan(n, sw, total);
+        const uint32_t cr = carry;
+        if (c < nch) co[c] = c * kStuffBytes + cr + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = cr + total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) A.stuffed[tile] = nbytes + carry;
+}
+
+__device__ __forceinline__ uint64_t block_exclusive_scan64(uint64_t v, uint64_t* s_wave, uint64_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint64_t w = lane < nw ? s_wave[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;
+    }
+    __syncthreads();
+    const uint64_t off = wid ? s_wave[wid - 1] : 0;
+    total = s_wave[nw - 1];
+    __syncthreads();
+    return off + x - v;
+}
+
+struct B5Args {
+    const uint32_t* stuffed;
+    uint64_t* offsets;     // [tile] byte offset of the tile's file in out
+    uint32_t* lengths;     // [tile] file length (0 when it did not fit)
+    int32_t* status;       // [tile] OMR_OK / OMR_BUFFER_TOO_SMALL (optional)
+    uint8_t* out;
+    uint64_t cap;
+    int32_t n_tiles, hdr_len;
+};
+
+__global__ void __launch_bounds__(kTileThreads) k_jpeg_tile_scan(B5Args A) {
+    __shared__ uint64_t sw[16];
+    __shared__ uint64_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int base = 0; base < A.n_tiles; base += kTileThreads) {
+        const int t = base + threadIdx.x;
+        const uint64_t len = t < A.n_tiles ? (uint64_t)A.hdr_len + A.stuffed[t] + 2 : 0;
+        uint64_t total;
+        const uint64_t ex = block_exclusive_scan64(len, sw, total);
+        const uint64_t cr = carry;
+        if (t < A.n_tiles) {
+            const uint64_t off = cr + ex;
+            const bool fits = off + len <= A.cap;
+            A.offsets[t] = off;
+            A.lengths[t] = fits ? (uint32_t)len : 0;
+            if (A.status) A.status[t] = fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
+            if (fits) {                            // EOI
+                A.out[off + len - 2] = 0xFF;
+                A.out[off + len - 1] = 0xD9;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) carry = cr + total;
+        __syncthreads();
+    }
+}
+
+struct B6Args {
+    const uint32_t* words;
+    const uint32_t* tile_bits;
+    const uint32_t* chunk_off;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint8_t* hdr;
+    uint8_t* out;
+    int64_t slot_words, slot_chunks;
+    int32_t hdr_len;
+};
+
+constexpr int kB6Threads = 256;
+
+__global__ void __launch_bounds__(kB6Threads) k_jpeg_stuff_batch(B6Args A) {
+    __shared__ uint8_t sbytes[kB6Threads * kStuffBytes * 2];
+    __shared__ uint32_t s_end;
+    const int tile = blockIdx.y;
+    if (A.lengths[tile] == 0) return;          // did not fit: status says so
+    uint8_t* out = A.out + A.offsets[tile];
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < A.hdr_len; i += kB6Threads) out[i] = A.hdr[i];
+    out += A.hdr_len;
+    const uint32_t tb = A.tile_bits[tile], nbytes = (tb + 7) / 8;
+    const uint32_t nch = (nbytes + kStuffBytes - 1) / kStuffBytes;
+    const uint32_t* words = A.words + (int64_t)tile * A.slot_words;
+    const uint32_t* co = A.chunk_off + (int64_t)tile * A.slot_chunks;
+    // grid-stride over groups of kB6Threads chunks (the grid is sized for typical streams,
+    // not the worst-case slot)
+    for (uint32_t c0 = blockIdx.x * kB6Threads; c0 < nch; c0 += gridDim.x * kB6Threads) {
+        const uint32_t c = c0 + threadIdx.x;
+        const uint32_t cend = min(nch, c0 + kB6Threads);
+        const uint32_t base = co[c0];
+        if (c < nch) {
+            uint32_t o = co[c] - base;
+            const uint32_t e = min(nbytes, (c + 1) * kStuffBytes);
+            for (uint32_t i = c * kStuffBytes; i < e; ++i) {
+                const uint32_t b = seg_byte(words, i, nbytes, tb);
+                sbytes[o++] = (uint8_t)b;
+                if (b == 0xFF) sbytes[o++] = 0;
+            }
+            if (c == cend - 1) s_end = o;
+        }
+        __syncthreads();
+        const uint32_t n = s_end;
+        for (uint32_t i = threadIdx.x; i < n; i += kB6Threads) out[base + i] = sbytes[i];
+        __syncthreads();
+    }
+}
+
+// Batch workspace layout.
+struct JpegBatchLayout {
+    int64_t n_mcu, nb, slot_words, slot_chunks;
+    size_t coef, aclen, dcs, offs, tbits, words, chunk, stuffed, hdr, total;
+};
+
+static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
+    JpegBatchLayout L{};
+    L.n_mcu = (int64_t)((W + 15) / 16) * ((H + 15) / 16);
+    L.nb = L.n_mcu * 6;
+    L.slot_words = (L.nb * 1700 + 31) / 32 + 2;
+    L.slot_chunks = (L.slot_words * 4 + kStuffBytes - 1) / kStuffBytes + 1;
+    size_t o = align_up(base, 256);
+    auto take = [&](size_t bytes) { const size_t r = o; o = align_up(o + bytes, 256); return r; };
+    L.coef = take((size_t)n * L.nb * 128);
+    L.aclen = take((size_t)n * L.nb * 2);
+    L.dcs = take((size_t)n * L.nb * 2);
+    L.offs = take((size_t)n * L.nb * 4);
+    L.tbits = take((size_t)n * 4);
+    L.words = take((size_t)n * L.slot_words * 4);
+    L.chunk = take((size_t)n * L.slot_chunks * 4);
+    L.stuffed = take((size_t)n * 4);
+    L.hdr = take(1024);
+    L.total = o;
+    return L;
+}
+
+static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t tile_stride, int n, int W,
+                                       int H, float quality, uint8_t* d_out, uint64_t cap, uint64_t* d_offsets,
+                                       uint32_t* d_lengths, int32_t* d_status, const JpegBatchLayout& L) {
+    uint8_t ql[64], qc[64];
+    quant_tables(quality, ql, qc);
+    std::vector<uint8_t> hdr;
+    jpeg_header(hdr, W, H, ql, qc);
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    omr_status sst = stage_h2d(ctx, ws + L.hdr, hdr.data(), hdr.size());   // pinned ring: async-safe
+    if (sst) return sst;
+    B1Args a1;
+    a1.argb = d_argb;
+    a1.tile_stride = tile_stride;
+    a1.coefs = reinterpret_cast<int16_t*>(ws + L.coef);
+    a1.aclen = reinterpret_cast<uint16_t*>(ws + L.aclen);
+    a1.dcs = reinterpret_cast<int16_t*>(ws + L.dcs);
+    a1.W = W;
+    a1.H = H;
+    a1.mcux = (W + 15) / 16;
+    a1.n_mcu = (int32_t)L.n_mcu;
+    a1.nb = (int32_t)L.nb;
+    for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
+    B2Args a2{a1.aclen, a1.dcs, reinterpret_cast<uint32_t*>(ws + L.offs), reinterpret_cast<uint32_t*>(ws + L.tbits),
+              reinterpret_cast<uint32_t*>(ws + L.words), (int32_t)L.nb, L.slot_words};
+    B3Args a3{a1.coefs, a1.dcs, a2.offs, a2.words, (int32_t)L.nb, L.slot_words};
+    B4Args a4{a2.words, a2.tile_bits, reinterpret_cast<uint32_t*>(ws + L.chunk),
+              reinterpret_cast<uint32_t*>(ws + L.stuffed), L.slot_words, L.slot_chunks};
+    B5Args a5{a4.stuffed, d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
+    B6Args a6{a2.words, a2.tile_bits, a4.chunk_off, d_offsets, d_lengths, ws + L.hdr, d_out, L.slot_words,
+              L.slot_chunks, (int32_t)hdr.size()};
+    KernelTimer whole(ctx, 4);
+    {
+        KernelTimer t(ctx, 5);
+        hipLaunchKernelGGL(k_jpeg_fdct_batch, dim3((unsigned)((L.n_mcu + 4 * kB1McuPerWave - 1) / (4 * kB1McuPerWave)),
+                                                    (unsigned)n), dim3(256), 0,
+                           ctx->stream, a1);
+    }
+    hipLaunchKernelGGL(k_jpeg_block_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a2);
+    {
+        KernelTimer t(ctx, 6);
+        hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((unsigned)((L.nb + 4 * kB3BlocksPerWave - 1) / (4 * kB3BlocksPerWave)),
+                                                   (unsigned)n), dim3(256), 0,
+                           ctx->stream, a3);
+    }
+    hipLaunchKernelGGL(k_jpeg_stuff_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a4);
+    hipLaunchKernelGGL(k_jpeg_tile_scan, dim3(1), dim3(kTileThreads), 0, ctx->stream, a5);
+    // ~4 chunk groups per 1024^2 tile at typical rates; larger streams loop
+    const int64_t groups = std::max<int64_t>(1, std::min<int64_t>(64, (L.nb * 16 / kStuffBytes) / kB6Threads));
+    hipLaunchKernelGGL(k_jpeg_stuff_batch, dim3((unsigned)groups, (unsigned)n),
+                       dim3(kB6Threads), 0, ctx->stream, a6);
+    OMR_HIP(ctx, hipGetLastError());
+    return OMR_OK;
+}
+
+static omr_status check_jpeg_batch(Ctx* ctx, const void* d_argb, int n, int W, int H, int64_t stride) {
+    if (!d_argb) return fail(ctx, OMR_INVALID_ARGUMENT, "null ARGB batch");
+    if (n <= 0 || n > (1 << 20)) return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: n_tiles out of range");
+    if (W <= 0 || H <= 0 || W > 4096 || H > 4096)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: tile dimensions must be 1..4096");
+    if (stride < (int64_t)W * H) return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: tile stride < width*height");
+    return OMR_OK;
+}
+
+}  // namespace omr
+
+extern "C" {
+
+omr_status omr_encode_jpeg_batch_device(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
+                                        int32_t n_tiles, int32_t width, int32_t height, float quality,
+                                        uint8_t* d_out, size_t out_cap, uint64_t* d_offsets,
+                                        uint32_t* d_lengths, int32_t* d_status) {
+    using namespace omr;
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (tile_stride_px == 0) tile_stride_px = (int64_t)width * height;
+    omr_status st = check_jpeg_batch(ctx, d_argb, n_tiles, width, height, tile_stride_px);
+    if (st) return st;
+    if (!d_out || !d_offsets || !d_lengths) return fail(ctx, OMR_INVALID_ARGUMENT, "null batch output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    const JpegBatchLayout L = jpeg_batch_layout(width, height, n_tiles, 0);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    return encode_jpeg_batch_ws(ctx, d_argb, tile_stride_px, n_tiles, width, height, quality, d_out, out_cap,
+                                d_offsets, d_lengths, d_status, L);
+}
+
+}  // extern "C"
+
+extern "C" omr_status omr_encode_jpeg_batch(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
+                                            int32_t n_tiles, int32_t width, int32_t height, float quality,
+                                            uint8_t* out, size_t cap, uint64_t* offsets, uint32_t* lengths) {
+    using namespace omr;
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (tile_stride_px == 0) tile_stride_px = (int64_t)width * height;
+    omr_status st = check_jpeg_batch(ctx, d_argb, n_tiles, width, height, tile_stride_px);
+    if (st) return st;
+    if (!out || !offsets || !lengths) return fail(ctx, OMR_INVALID_ARGUMENT, "null batch output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    JpegBatchLayout L = jpeg_batch_layout(width, height, n_tiles, 0);
+    const size_t o_offs = align_up(L.total, 256);
+    const size_t o_lens = align_up(o_offs + (size_t)n_tiles * 8, 256);
+    const size_t o_out = align_up(o_lens + (size_t)n_tiles * 4, 256);
+    st = ensure_workspace(ctx, o_out + cap);
+    if (st) return st;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    uint64_t* d_offs = reinterpret_cast<uint64_t*>(ws + o_offs);
+    uint32_t* d_lens = reinterpret_cast<uint32_t*>(ws + o_lens);
+    st = encode_jpeg_batch_ws(ctx, d_argb, tile_stride_px, n_tiles, width, height, quality, ws + o_out, cap,
+                              d_offs, d_lens, nullptr, L);
+    if (st) return st;
+    OMR_HIP(ctx, hipMemcpyAsync(offsets, d_offs, (size_t)n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipMemcpyAsync(lengths, d_lens, (size_t)n_tiles * 4, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t used = 0;
+    bool short_buf = false;
+    for (int i = 0; i < n_tiles; ++i) {
+        if (lengths[i] == 0) short_buf = true;
+        else used = std::max<uint64_t>(used, offsets[i] + lengths[i]);
+    }
+    if (used) OMR_HIP(ctx, hipMemcpyAsync(out, ws + o_out, used, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (short_buf) return fail(ctx, OMR_BUFFER_TOO_SMALL, "JPEG batch output buffer too small (lengths 0)");
+    return OMR_OK;
+}

@@ -133,6 +133,8 @@ _SIGS = {
     "omr_png_max_bytes": (_sz, [_i32, _i32, _i32]),
     "omr_encode_jpeg": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_encode_jpeg_device": (_i32, [_vp, _vp, _i32, _i32, _f32, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_encode_jpeg_batch_device": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
+    "omr_encode_jpeg_batch": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp]),
     "omr_jpeg_quant_tables": (_i32, [_f32, _vp, _vp]),
     "omr_tiff_max_bytes": (_sz, [_i32, _i32]),
     "omr_encode_tiff": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),

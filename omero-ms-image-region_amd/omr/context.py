@@ -213,6 +213,25 @@ class Context:
         return self._encode(lib.omr_encode_jpeg_device, d_argb, width, height, float(quality),
                             cap=lib.omr_jpeg_max_bytes(width, height))
 
+    def encode_jpeg_batch_device(self, d_argb, n_tiles, width, height, quality, d_out, d_offsets,
+                                 d_lengths, d_status=None, tile_stride=0):
+        """Async batch encode on the device; files packed in d_out (uint8 tensor)."""
+        check(lib.omr_encode_jpeg_batch_device(self.h, _ptr(d_argb), tile_stride, n_tiles, width, height,
+                                               float(quality), _ptr(d_out), d_out.numel(), _ptr(d_offsets),
+                                               _ptr(d_lengths), _ptr(d_status)), self.h)
+
+    def encode_jpeg_batch(self, d_argb, n_tiles, width, height, quality, cap=None, tile_stride=0):
+        """Batch encode device ARGB tiles -> list of JPEG byte strings (one host sync)."""
+        if cap is None:
+            cap = n_tiles * (width * height + 4096)
+        out = np.empty(cap, dtype=np.uint8)
+        offs = np.zeros(n_tiles, dtype=np.uint64)
+        lens = np.zeros(n_tiles, dtype=np.uint32)
+        check(lib.omr_encode_jpeg_batch(self.h, _ptr(d_argb), tile_stride, n_tiles, width, height,
+                                        float(quality), out.ctypes.data, cap, offs.ctypes.data,
+                                        lens.ctypes.data), self.h)
+        return [out[int(o):int(o) + int(n)].tobytes() for o, n in zip(offs, lens)]
+
     def encode_png(self, argb, width, height):
         argb = np.ascontiguousarray(argb, dtype=np.uint32)
         return self._encode(lib.omr_encode_png, argb, width, height,
