@@ -218,6 +218,175 @@ def jpeg_cpu_baseline(torch, name, src, chans, pt, be, q, seconds, threads):
                       f"(oracle/omr_oracle.c, -O3)"}
 
 
+def _timed(torch, ctx, step, steps, warmup):
+    """Run warmup + timed steps; returns (elapsed_s, {kind: avg_ms}) from the context's HIP events."""
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    ctx.kernel_timings()
+    ctx.enable_kernel_timing(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    ctx.enable_kernel_timing(False)
+    tm = {}
+    for ms, kind in ctx.kernel_timings():
+        tm.setdefault(kind, []).append(ms)
+    return el, {k: sum(v) / len(v) for k, v in tm.items()}
+
+
+def _cpu_pool(fn, seconds, threads):
+    """fn(i) on a thread pool (ctypes releases the GIL): calibrate on one round, then time a
+    bounded sample.  Returns (n, secs)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(fn, range(threads)))
+        first = time.perf_counter() - t0
+        n = max(threads, int(threads * seconds / max(first, 1e-3)) // threads * threads)
+        t0 = time.perf_counter()
+        list(ex.map(fn, range(n)))
+        return n, time.perf_counter() - t0
+
+
+def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
+    """BASELINE configs[2] (C3): 3-channel uint16 512x512x64 Z-stack (big-endian, as ROMIO) ->
+    max / mean intensity projection of every active channel (K3, one launch for the 3 stacks)
+    -> composite of the projected full plane (K1+K2) (ImageRegionRequestHandler.java:506-575).
+    One step = one render_image_region request with p=intmax|0:63 (or intmean)."""
+    import numpy as np
+    from omr import _lib
+    from omr.context import make_qdef
+    from omr.synthetic import c2_channels
+    dev = torch.device("cuda", ctx.device)
+    S, Z, C = 512, 64, 3
+    g = torch.Generator(device=dev)
+    g.manual_seed(20261015 + 3)
+    # uniform uint16 values (every LUT entry, worst case for the window compares), stored big-endian
+    stacks = [torch.randint(0, 65536, (Z, S, S), dtype=torch.int32, device=dev, generator=g) for _ in range(C)]
+    stacks = [(s & 0xFF) << 8 | (s >> 8) for s in stacks]                                # -> BE bytes
+    stacks = [(s - 65536 * (s >= 32768).to(torch.int32)).to(torch.int16).contiguous() for s in stacks]
+    chans = c2_channels(C)
+    qd = make_qdef("rgb")
+    out = torch.empty((S, S), dtype=torch.int32, device=dev)
+    res = {}
+    for name, alg, end in (("max", _lib.PROJECTION_MAX, Z - 1), ("mean", _lib.PROJECTION_MEAN, Z - 1)):
+        def step():
+            ctx.render_projected_device(qd, chans, stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, out,
+                                        big_endian=True)
+        el, avg = _timed(torch, ctx, step, steps, warmup)
+        k3 = avg.get(3, float("nan"))
+        used_z = Z if alg == _lib.PROJECTION_MAX else Z - 1
+        alg_bytes = C * (used_z * S * S * 2 + S * S * 2)
+        r = {"requests_per_s": round(steps / el, 1), "ms_per_request": round(1e3 * el / steps, 4),
+             "kernel_ms": {"K3_project": round(k3, 5), "K2_render": round(avg.get(2, float("nan")), 5)},
+             "roofline": {"bound": "hbm", "kernel": f"k_project<u16,BE,{name}> (K3)",
+                          "achieved": round(alg_bytes / (k3 * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                          "unit": "GB/s", "frac": round(alg_bytes / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "algorithmic_bytes_per_launch": alg_bytes}}
+        if with_cpu:
+            try:
+                sys.path.insert(0, os.path.join(REPO, "tests"))
+                import oracle_lib
+                host = [s.cpu().numpy().view(np.uint16) for s in stacks]
+
+                def one(i):
+                    planes = []
+                    for c in range(C):
+                        st, p = oracle_lib.project(host[c], _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, be_in=True,
+                                                   be_out=True)
+                        planes.append(p.view(np.uint16))
+                    oracle_lib.render(chans, planes, _lib.PIXELS_UINT16, S, S, big_endian=True)
+                n, secs = _cpu_pool(one, cpu_seconds, threads)
+                r["cpu_baseline"] = {"value": round(n / secs, 3), "unit": "requests/s", "cores": threads,
+                                     "kind": "port",
+                                     "sample": f"{n} C3 {name} requests (3x project 512x512x64 u16 + composite) "
+                                               f"in {secs:.2f} s on {threads} threads (oracle/omr_oracle.c, -O3)"}
+            except Exception as e:
+                log(f"c3 cpu baseline failed: {e}")
+        res[name] = r
+    return res
+
+
+def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
+    """BASELINE configs[4] (C5): 3-channel float32 1024^2 tiles, log (reverse) / poly k=0.5 /
+    poly k=2 + .lut families, windows at p1/p99 (K2 eval mode: per-pixel double evaluation), plus
+    render_shape_mask of a 1024x1024 bit mask (colour FF000080, flip hv)."""
+    import numpy as np
+    from omr import _lib
+    from omr.context import make_bindings, make_qdef
+    from omr.renderer import f32
+    from omr.synthetic import C2_COLORS
+    dev = torch.device("cuda", ctx.device)
+    rng = np.random.default_rng(20261015 + 5)
+    uniq = 4
+    host = np.stack([np.stack([rng.lognormal(5, 1.5, (TILE, TILE)).astype(np.float32),
+                               rng.normal(0, 300, (TILE, TILE)).astype(np.float32),
+                               rng.lognormal(5, 1.5, (TILE, TILE)).astype(np.float32)]) for _ in range(uniq)])
+    lut = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
+    chans = []
+    for c in range(3):
+        lo, hi = np.percentile(host[0, c], 1), np.percentile(host[0, c], 99)
+        chans.append({"input_start": f32(lo), "input_end": f32(hi), "rgba": C2_COLORS[c]})
+    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
+    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
+    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=lut)
+    be_host = host.astype(">f4")
+    src = torch.from_numpy(np.ascontiguousarray(be_host).view(np.uint8)).to(dev)
+    data = torch.empty((B, 3 * TILE * TILE * 4), dtype=torch.uint8, device=dev)
+    for t in range(B):
+        data[t].copy_(src.view(uniq, -1)[t % uniq])
+    out = torch.empty((B, TILE, TILE), dtype=torch.int32, device=dev)
+    qd = make_qdef("rgb")
+    binds = make_bindings(chans)
+    plane = TILE * TILE * 4
+
+    def step():
+        ctx.render_batch_strided_device(qd, chans, data, 3 * plane, plane, B, _lib.PIXELS_FLOAT, TILE, TILE, out,
+                                        big_endian=True, bindings=binds)
+    el, avg = _timed(torch, ctx, step, steps, warmup)
+    k2 = avg.get(2, float("nan"))
+    per_tile = 3 * plane + TILE * TILE * 4
+    ach = per_tile * B / (k2 * 1e-3) / 1e9
+    r = {"tiles_per_s": round(B * steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4), "tiles_per_step": B,
+         "roofline": {"bound": "hbm", "kernel": "k_render<f32,BE,3ch,eval> (K2)", "achieved": round(ach, 1),
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                      "algorithmic_bytes_per_launch": per_tile * B, "avg_launch_ms": round(k2, 5)}}
+    if with_cpu:
+        try:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib
+            tiles = [[np.ascontiguousarray(be_host[t, c]) for c in range(3)] for t in range(uniq)]
+
+            def one(i):
+                oracle_lib.render(chans, tiles[i % uniq], _lib.PIXELS_FLOAT, TILE, TILE, big_endian=True)
+            n, secs = _cpu_pool(one, cpu_seconds, threads)
+            r["cpu_baseline"] = {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
+                                 "sample": f"{n} C5 tiles (3ch f32 1024^2, log/poly/lut/reverse) in {secs:.2f} s "
+                                           f"on {threads} threads (oracle/omr_oracle.c, -O3)"}
+        except Exception as e:
+            log(f"c5 cpu baseline failed: {e}")
+    # render_shape_mask: 1024x1024 mask of random ellipses, FF000080, flip hv (host API, p50)
+    yy, xx = np.mgrid[0:TILE, 0:TILE]
+    m = np.zeros((TILE, TILE), bool)
+    for _ in range(24):
+        cy, cx, ry, rx = rng.uniform(0, TILE), rng.uniform(0, TILE), rng.uniform(10, 120), rng.uniform(10, 120)
+        m |= ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1
+    bits = np.packbits(m.reshape(-1)).tobytes()
+    lat = []
+    for i in range(23):
+        t0 = time.perf_counter()
+        png = ctx.render_shape_mask_png(bits, TILE, TILE, (255, 0, 0, 128), flip_h=True, flip_v=True)
+        if i >= 3:
+            lat.append(time.perf_counter() - t0)
+    r["shape_mask_png"] = {"p50_ms": round(1e3 * float(np.median(lat)), 4), "png_bytes": len(png),
+                           "size": "1024x1024 1-bit, flip hv"}
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -235,6 +404,8 @@ def main():
     ap.add_argument("--no-jpeg", action="store_true", help="skip the render->JPEG batch section")
     ap.add_argument("--jpeg-batch", type=int, default=64, help="tiles per JPEG step")
     ap.add_argument("--jpeg-steps", type=int, default=10)
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the C3 (projection) and C5 (float32 families, shape mask) sections")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-tile latency probe (profiling runs: batch launches only)")
     args = ap.parse_args()
@@ -318,6 +489,19 @@ def main():
         if not args.no_jpeg:
             extra["jpeg"] = jpeg_section(torch, ctx, data, min(args.jpeg_batch, B), args.jpeg_steps,
                                          2, args.cpu_seconds / 2, threads, not args.no_cpu_baseline)
+        if not args.no_configs:
+            try:
+                extra["c3_projection"] = c3_section(torch, ctx, 20, 3, args.cpu_seconds / 4, threads,
+                                                    not args.no_cpu_baseline)
+            except Exception as e:
+                log(f"c3 section failed: {e}")
+                raise
+            try:
+                extra["c5_float"] = c5_section(torch, ctx, 32, 10, 2, args.cpu_seconds / 4, threads,
+                                               not args.no_cpu_baseline)
+            except Exception as e:
+                log(f"c5 section failed: {e}")
+                raise
         if not args.no_cpu_baseline:
             try:
                 extra["cpu_baseline"] = cpu_baseline(torch, uniq, args.cpu_seconds, threads)

@@ -191,6 +191,45 @@ def test_c5_float32_log_poly_reverse_lut(ctx):
             assert d.max() <= 1, f"channel {c}: max code-value diff {d.max()}"
 
 
+def test_c5_full_size_strided_batch(ctx):
+    """C5 at BASELINE size (3ch float32 1024^2, BE) through the strided batch API the bench
+    times: per-channel +-1 code value (greyscale solo renders) and composite +-2."""
+    import torch
+    h = w = 1024
+    rng = np.random.default_rng(20261015 + 5)
+    planes = [rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32),
+              rng.normal(0, 300, size=(h, w)).astype(np.float32),
+              rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32)]
+    lut = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
+    chans = []
+    for i, p in enumerate(planes):
+        chans.append({"input_start": f32(np.percentile(p, 1)), "input_end": f32(np.percentile(p, 99)),
+                      "rgba": C2_COLORS[i]})
+    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
+    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
+    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=lut)
+    src = [p.astype(">f4") for p in planes]
+    blob = np.concatenate([s.view(np.uint8).reshape(-1) for s in src])
+    d = torch.from_numpy(np.concatenate([blob, blob])).to("cuda")          # 2 identical tiles
+    plane = h * w * 4
+    for model, cs in [("rgb", chans)] + [("greyscale", [dict(ch, active=(i == c)) for i, ch in enumerate(chans)])
+                                           for c in range(3)]:
+        out = torch.empty((2, h, w), dtype=torch.int32, device="cuda")
+        ctx.render_batch_strided_device(O.make_qdef(model), cs, d, 3 * plane, plane, 2, _lib.PIXELS_FLOAT, w, h,
+                                        out, big_endian=True)
+        ctx.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        st, exp = O.render(cs, src, _lib.PIXELS_FLOAT, w, h, big_endian=True, model=model)
+        assert st == 0
+        np.testing.assert_array_equal(got[0], got[1])
+        if model == "rgb":
+            assert_argb_close(got[0], exp, tol=2)
+        else:
+            diff = np.abs((got[0] & 0xFF).astype(int) - (exp & 0xFF).astype(int))
+            assert diff.max() <= 1, f"{model}: max code-value diff {diff.max()}"
+            assert (diff > 0).mean() < 1e-3                  # ulp-level boundary flips only
+
+
 def test_float_linear_and_int32_double_exact(ctx):
     h, w = 32, 48
     rng = np.random.default_rng(3)
