@@ -26,7 +26,9 @@ enum ChanMode : int32_t {
     kModeTable8 = 0,   // 8-bit types: quantization+codomain+colour folded into contrib[raw byte]
     kModeLinear16 = 1, // 16-bit linear: exact double evaluation of the LUT entry, contrib[v]
     kModeLut16 = 2,    // 16-bit other families / noise reduction: byte LUT gather, contrib[v]
-    kModeEval = 3      // 32-bit int / float / double: per-pixel q(x) in double, contrib[v]
+    kModeEval = 3,     // 32-bit int / float / double: per-pixel q(x) in double, contrib[v]
+    kModeThresh = 4    // float / int32 / uint32 with q monotone in x: K1 finds the 255 code
+                       // thresholds of q in key space, K2 binary-searches them in LDS
 };
 
 // One active channel as the kernels see it (device memory, read uniformly).

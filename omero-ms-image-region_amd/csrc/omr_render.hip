@@ -81,7 +81,8 @@ struct K2Chan {
     uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
 };
 
-enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3, kK2Fast16 = 4 };
+enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3, kK2Fast16 = 4,
+                    kK2Thresh = 5 /* float / 32-bit, every channel kModeThresh: no double math */ };
 
 struct K2Args {
     const RenderPlan* plan;     // full plan in HBM (eval mode reads the family parameters)
@@ -91,6 +92,10 @@ struct K2Args {
     int32_t strided;
     const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
+    const uint32_t* thresh;     // [n_active][256] kModeThresh code thresholds (K1)
+    const uint16_t* buckets;    // [n_active][kBuckets] kModeThresh key buckets (K1)
+    int32_t use_thresh;         // some channel is kModeThresh: stage thresh + buckets in LDS too
+    uint32_t n_work;            // work blocks of 256*CPT chunks (grid-stride in eval mode)
     uint32_t* out;              // [n_tiles][H][W]
     int32_t* status;            // optional per-tile status
     int32_t* flag;              // sticky error word
@@ -214,22 +219,157 @@ __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds
     return v;
 }
 
+// ---- kModeThresh: q(x) through its code thresholds in order-preserving key space.
+// key(x) is a uint32 whose unsigned order is the numeric order of x (NaN aside), so for a
+// q that is monotone non-decreasing in x (checked on the host: window, NR, family and both
+// rounding stages are all monotone once f is monotone on [ws, we)):
+//   q(x) = min(#{c in 1..255 : T[c] <= key(x)}, q(max key)),  T[c] = min{key : q(key) >= c}.
+// T is found by K1 with the very eval_q K2's kModeEval path evaluates, so the two modes give
+// identical codes; K2 then costs 8 LDS reads per pixel instead of a double log/pow.
+template <int PT> struct KeyDomain;
+template <> struct KeyDomain<OMR_PIXELS_FLOAT> {             // non-NaN keys: -inf .. +inf
+    static constexpr uint32_t lo = 0x007FFFFFu, hi = 0xFF800000u;
+};
+template <> struct KeyDomain<OMR_PIXELS_INT32> { static constexpr uint32_t lo = 0u, hi = 0xFFFFFFFFu; };
+template <> struct KeyDomain<OMR_PIXELS_UINT32> { static constexpr uint32_t lo = 0u, hi = 0xFFFFFFFFu; };
+
+__device__ __forceinline__ uint32_t float_key(uint32_t bits) {
+    return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+}
+
+template <int PT> __device__ __forceinline__ uint32_t raw_key(uint32_t raw) {
+    if constexpr (PT == OMR_PIXELS_FLOAT) return float_key(raw);
+    else if constexpr (PT == OMR_PIXELS_INT32) return raw ^ 0x80000000u;
+    else return raw;
+}
+
+template <int PT> __device__ __forceinline__ double key_value(uint32_t k) {
+    if constexpr (PT == OMR_PIXELS_FLOAT)
+        return (double)__uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+    else if constexpr (PT == OMR_PIXELS_INT32) return (double)(int32_t)(k ^ 0x80000000u);
+    else return (double)k;
+}
+
+// grid: (64, n_active) x 256 threads; wave w of block b finds T[c], c = 4b + w, by a 64-ary
+// search of the key domain (every lane evaluates q at one of 64 evenly spaced keys, a ballot
+// narrows the interval 64-fold: <= 6 rounds instead of 33 bisection steps).
+// thr[a][0] = q(max key) | q(NaN) << 8; thr[a][c] = T[c] (0xFFFFFFFF when no key reaches c).
+template <int PT>
+__global__ void __launch_bounds__(256) k_build_thresh(const RenderPlan* __restrict__ plan,
+                                                      uint32_t* __restrict__ thr) {
+    const int a = blockIdx.y;
+    const ChanParam& p = plan->ch[a];
+    if (p.mode != kModeThresh) return;
+    const int cds = plan->cd_start, cde = plan->cd_end;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    constexpr uint32_t klo = KeyDomain<PT>::lo, khi = KeyDomain<PT>::hi;
+    if (c == 0) {
+        if (lane == 0) {
+            const uint32_t cmax = eval_q(key_value<PT>(khi), p, cds, cde);
+            const uint32_t qnan = PT == OMR_PIXELS_FLOAT ? eval_q(__builtin_nan(""), p, cds, cde) : 0u;
+            thr[a * 256] = cmax | (qnan << 8);
+        }
+        return;
+    }
+    uint64_t lo = klo, hi = (uint64_t)khi + 1;      // answer in [lo, hi]; hi = "none"
+    while (lo < hi) {                               // wave-uniform
+        const uint64_t n = hi - lo, step = (n + 63) / 64;
+        const uint64_t m = lo + lane * step;
+        const bool pred = m < hi && eval_q(key_value<PT>((uint32_t)m), p, cds, cde) >= c;
+        const uint64_t mask = __ballot(pred);
+        if (mask == 0) {
+            lo = lo + ((n - 1) / step) * step + 1;      // past the last probed key
+        } else {
+            const uint64_t j = (uint64_t)(__ffsll((unsigned long long)mask) - 1);
+            if (j == 0) hi = lo;
+            else { hi = lo + j * step; lo = lo + (j - 1) * step + 1; }
+        }
+    }
+    if (lane == 0) thr[a * 256 + c] = lo > khi ? 0xFFFFFFFFu : (uint32_t)lo;
+}
+
+// Buckets over the key range where a kModeThresh channel's code varies, [T[1], T[cmax]):
+// bucket b covers 2^shift keys; its entry is (#T <= its first key) | (#T inside it) << 8, so K2
+// searches only the few thresholds of its bucket (usually 0-2) instead of all 255.
+constexpr int kBucketsLog2 = 11, kBuckets = 1 << kBucketsLog2;
+
+__device__ __forceinline__ uint32_t bucket_shift(uint32_t span) {
+    const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
+    return bits > (uint32_t)kBucketsLog2 ? bits - kBucketsLog2 : 0u;
+}
+
+// #{c in 1..255 : T[c] <= key} over the sorted thresholds.
+__device__ __forceinline__ uint32_t thresh_count(const uint32_t* __restrict__ T, uint32_t key) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t st = 128; st >= 1; st >>= 1) pos += (T[pos + st] <= key) ? st : 0u;
+    return pos;
+}
+
+// grid: (kBuckets/256, n_active) x 256 threads.
+__global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restrict__ plan,
+                                                       const uint32_t* __restrict__ thr,
+                                                       uint16_t* __restrict__ bkt) {
+    const int a = blockIdx.y;
+    if (plan->ch[a].mode != kModeThresh) return;
+    const uint32_t* T = thr + a * 256;
+    const uint32_t cmax = T[0] & 0xFFu;
+    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
+    uint16_t e = 0;
+    if (k1 > k0) {
+        const uint32_t sh = bucket_shift(k1 - k0);
+        const uint64_t ks = (uint64_t)k0 + ((uint64_t)b << sh);
+        if (ks < k1) {
+            const uint64_t ke = std::min<uint64_t>(ks + (1ull << sh) - 1, (uint64_t)k1 - 1);
+            const uint32_t lo = thresh_count(T, (uint32_t)ks), hi = thresh_count(T, (uint32_t)ke);
+            e = (uint16_t)(lo | ((hi - lo) << 8));
+        }
+    }
+    bkt[a * kBuckets + b] = e;
+}
+
 constexpr int kCPT = 2;   // chunks per thread of the fixed-channel-count kernels
 
-// One full (non-persistent) grid: block b owns chunks [b*256*CPT, (b+1)*256*CPT), thread t the
-// chunks b*256*CPT + k*256 + t.  Every channel load of every chunk is issued before any compute
+// LDS of one K2 block: contrib [na][256] u32, then (kModeThresh) thresholds [na][256] u32 and
+// buckets [na][kBuckets] u16.
+__host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh) {
+    return (size_t)na * (1024 + (thresh ? 1024 + 2 * kBuckets : 0));
+}
+
+template <int MODE, int BPP>
+__device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_contrib, int na) {
+    // one 16-byte load per lane for up to 4 channels of contrib; the threshold tables follow
+    for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
+        *reinterpret_cast<uint4*>(s_contrib + i) = *reinterpret_cast<const uint4*>(A.contrib + i);
+    if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
+        if (A.use_thresh) {
+            uint32_t* s_thr = s_contrib + na * 256;
+            for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
+                *reinterpret_cast<uint4*>(s_thr + i) = *reinterpret_cast<const uint4*>(A.thresh + i);
+            uint32_t* s_b = s_thr + na * 256;
+            const uint32_t* g_b = reinterpret_cast<const uint32_t*>(A.buckets);
+            for (int i = threadIdx.x * 4; i < na * kBuckets / 2; i += kBlock * 4)
+                *reinterpret_cast<uint4*>(s_b + i) = *reinterpret_cast<const uint4*>(g_b + i);
+        }
+    }
+}
+
+// The chunks of work block wb: [wb*256*CPT, (wb+1)*256*CPT), thread t the chunks
+// wb*256*CPT + k*256 + t.  Every channel load of every chunk is issued before any compute
 // (CPT*NA 16-B loads in flight per lane); plain loads (measured faster than non-temporal here,
 // tools/probe_stream.hip).  NA == 0: runtime channel count, one chunk per thread, clamp per add.
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
-__global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
+// STAGE: load the LDS tables here, after the pixel loads are in flight (one-pass grids).
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, bool STAGE>
+__device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* s_contrib) {
     constexpr int CPT = NA > 0 ? kCPT : 1;
     constexpr int NL = NA > 0 ? NA : 1;
     const int na = NA > 0 ? NA : A.n_active;
     const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
     const int W = A.width, H = A.height;
     const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
-    const uint32_t g0 = blockIdx.x * (kBlock * CPT);
+    const uint32_t g0 = wb * (kBlock * CPT);
     uint32_t btile = 0;
     if (A.tile_uniform) btile = fdiv(g0, A.cpt);          // whole block inside one tile (scalar)
     auto plane_base = [&](uint32_t t, int a) -> const uint8_t* {
@@ -269,11 +409,13 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
             for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(ck[k][a], pb[k][a] + off);
         }
     }
-    // Contribution tables -> LDS, issued after the pixel loads so their latencies overlap
-    // (one 16-byte load per lane for up to 4 channels; a single wait).
-    for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
-        *reinterpret_cast<uint4*>(s_contrib + i) = *reinterpret_cast<const uint4*>(A.contrib + i);
-    __syncthreads();
+    if constexpr (STAGE) {
+        // tables -> LDS, issued after the pixel loads so their latencies overlap
+        k2_stage_tables<MODE, BPP>(A, s_contrib, na);
+        __syncthreads();
+    }
+    uint32_t* const s_thr = s_contrib + na * 256;
+    const uint16_t* const s_bkt = reinterpret_cast<const uint16_t*>(s_thr + na * 256);
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
         const uint32_t g = gk[k];
@@ -294,6 +436,36 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
                 load_chunk<BPP, VEC>(c, plane_base(tile, a) + in_off);
             }
             const uint32_t* tab = s_contrib + a * 256;
+            if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
+                if (MODE == kK2Thresh || p.mode == kModeThresh) {          // uniform: bucket, then the few thresholds in it
+                    const uint32_t* T = s_thr + a * 256;
+                    const uint16_t* Bk = s_bkt + a * kBuckets;
+                    const uint32_t meta = T[0];
+                    const uint32_t cmax = meta & 0xFFu, cnan = (meta >> 8) & 0xFFu;
+                    const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
+                    const uint32_t sh = bucket_shift(k1 > k0 ? k1 - k0 : 0u);
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) {
+                        uint32_t raw = c.dw[j];
+                        if constexpr (BE) raw = bswap32(raw);
+                        const uint32_t key = raw_key<PT>(raw);
+                        const bool inr = key >= k0 && key < k1;
+                        const uint32_t e = Bk[min((key - k0) >> sh, (uint32_t)kBuckets - 1)];
+                        uint32_t base = inr ? (e & 0xFFu) : (key >= k1 ? cmax : 0u);
+                        uint32_t len = inr ? (e >> 8) : 0u;
+                        while (len > 0) {
+                            const uint32_t half = len >> 1;
+                            const bool le = T[base + half + 1] <= key;
+                            base = le ? base + half + 1 : base;
+                            len = le ? len - half - 1 : half;
+                        }
+                        if constexpr (PT == OMR_PIXELS_FLOAT) base = ((raw & 0x7FFFFFFFu) > 0x7F800000u) ? cnan : base;
+                        acc[j] += tab[base];
+                        if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
+                    }
+                    continue;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < VEC; ++j) {
                 uint32_t e;
@@ -314,9 +486,11 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
                         v = A.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
                     }
                     e = tab[v];
-                } else {
+                } else if constexpr (MODE == kK2Eval) {
                     const double x = pixel_double<BPP, VEC, BE, PT>(c, j);
                     e = tab[eval_q(x, A.plan->ch[a], A.cd_start, A.cd_end)];
+                } else {
+                    e = 0;   // kK2Thresh: every channel took the threshold path above
                 }
                 acc[j] += e;
                 if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
@@ -351,6 +525,23 @@ __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
     }
 }
 
+// Integer / 8-bit modes: one full (non-persistent) grid, one work block per workgroup, tables
+// staged behind the pixel loads.  Eval mode (float / 32-bit; threshold + bucket tables up to
+// 6 KiB per channel): a grid of a few workgroups per CU that stage the tables once and stride
+// over the work blocks.
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
+__global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
+    if constexpr (MODE == kK2Eval || MODE == kK2Thresh) {
+        k2_stage_tables<MODE, BPP>(A, s_contrib, NA > 0 ? NA : A.n_active);
+        __syncthreads();
+        for (uint32_t wb = blockIdx.x; wb < A.n_work; wb += gridDim.x)
+            k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, false>(A, wb, s_contrib);
+    } else {
+        k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, true>(A, blockIdx.x, s_contrib);
+    }
+}
+
 // ------------------------------------------------------------------------------- host side
 struct PreparedPlan {
     RenderPlan plan;
@@ -374,6 +565,30 @@ static int32_t ceil_to_i32(double v) {
     if (c <= -2147483647.0) return -2147483647;
     if (c >= 2147483647.0) return 2147483647;
     return (int32_t)c;
+}
+
+// kModeThresh precondition: q is monotone non-decreasing in x.  Below ws it is cdStart, at or
+// above we cdEnd, and inside [ws, we) it is round(a1*round(a0*(f(x) - f(ws))) + cdStart) with
+// a0, a1 >= 0 — monotone once f is increasing and finite on [ws, we]: always for linear; for
+// log / poly / exp when ws > 0 and k > 0 (x^k, ln x, e^(x^k) increase on x > 0).  Noise
+// reduction only widens the two constant ends.  Codes must stay inside one byte without wrap.
+static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixel_type) {
+    if (pixel_type != OMR_PIXELS_FLOAT && pixel_type != OMR_PIXELS_INT32 && pixel_type != OMR_PIXELS_UINT32)
+        return false;
+    if (q.cd_start < 0 || q.cd_end > 255 || q.cd_start > q.cd_end) return false;
+    if (!std::isfinite(p.ws) || !std::isfinite(p.we) || !(p.ws < p.we)) return false;
+    if (p.nr && !std::isfinite(p.dec)) return false;
+    // a0 NaN (e.g. x^0.5 with ws < 0 gives f(ws) = NaN): a0*(f(x) - ys) is NaN for every x, so
+    // the window maps to round(a1*0 + cdStart) = cdStart — a step function, monotone.
+    if (p.a0 != p.a0) return true;
+    if (!std::isfinite(p.ys) || !std::isfinite(p.a0) || !(p.a0 > 0) || !std::isfinite(p.a1) || p.a1 < 0) return false;
+    if (p.nr && !std::isfinite(p.dec)) return false;
+    if (p.family == OMR_FAMILY_LINEAR) return true;
+    const double ye = host_family_map(p.family, p.we, p.k);
+    if (!std::isfinite(ye) || !(ye > p.ys)) return false;
+    if (!(p.ws > 0)) return false;
+    if (p.family != OMR_FAMILY_LOGARITHMIC && !(p.k > 0 && std::isfinite(p.k))) return false;
+    return true;
 }
 
 static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch,
@@ -445,13 +660,16 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
                 }
             }
         } else {
-            p.mode = kModeEval;
+            p.mode = thresh_ok(p, *q, pixel_type) ? kModeThresh : kModeEval;
             p.gmin = INT32_MIN;
             p.gmax = INT32_MAX;
         }
         ++na;
     }
     P.n_active = na;
+    if (na > 8)   // threshold + bucket tables are 6 KiB of LDS per channel: keep K2 within 48 KiB
+        for (int i = 0; i < na; ++i)
+            if (P.ch[i].mode == kModeThresh) P.ch[i].mode = kModeEval;
     pp.plan_bytes = offsetof(RenderPlan, ch) + sizeof(ChanParam) * (size_t)(na > 0 ? na : 1);
     pp.lut_bytes = lut_off;
     return OMR_OK;
@@ -459,14 +677,16 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
 
 // Workspace layout for one render launch: [plan][contrib][luts][extra...]
 struct RenderLayout {
-    size_t plan_off = 0, contrib_off = 0, lut_off = 0, extra_off = 0, total = 0;
+    size_t plan_off = 0, contrib_off = 0, thresh_off = 0, bucket_off = 0, lut_off = 0, extra_off = 0, total = 0;
 };
 
 static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
     RenderLayout L;
     L.plan_off = 0;
     L.contrib_off = align_up(sizeof(RenderPlan), 256);
-    L.lut_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
+    L.thresh_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
+    L.bucket_off = L.thresh_off + align_up((size_t)kMaxActive * 256 * 4, 256);
+    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * kBuckets * 2, 256);
     L.extra_off = L.lut_off + align_up(pp.lut_bytes, 256);
     L.total = L.extra_off + extra;
     return L;
@@ -474,7 +694,7 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
 
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_t s) {
-    const size_t lds = (size_t)(na > 0 ? na : 1) * 256 * 4;
+    const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
     switch (na) {
     case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
     case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
@@ -500,6 +720,11 @@ static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, 
         return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, s)
                                      : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, s);
     } else if constexpr (BPP == 4) {
+        if (mode16 == kK2Thresh) {
+            if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Thresh>(a, na, grid, s);
+            if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Thresh>(a, na, grid, s);
+            return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Thresh>(a, na, grid, s);
+        }
         if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, s);
         if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, s);
         return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, s);
@@ -569,6 +794,22 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
             OMR_HIP(ctx, hipGetLastError());
         }
     }
+    bool use_thresh = false;
+    for (int i = 0; i < na; ++i) use_thresh |= pp.plan.ch[i].mode == kModeThresh;
+    uint32_t* d_thresh = reinterpret_cast<uint32_t*>(ws + L.thresh_off);
+    uint16_t* d_buckets = reinterpret_cast<uint16_t*>(ws + L.bucket_off);
+    if (use_thresh) {
+        const dim3 g(64, na);
+        switch (pixel_type) {
+        case OMR_PIXELS_FLOAT: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_FLOAT>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
+        case OMR_PIXELS_INT32: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_INT32>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
+        default: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_UINT32>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
+        }
+        OMR_HIP(ctx, hipGetLastError());
+        hipLaunchKernelGGL(k_build_buckets, dim3(kBuckets / 256, na), dim3(256), 0, ctx->stream, d_plan, d_thresh,
+                           d_buckets);
+        OMR_HIP(ctx, hipGetLastError());
+    }
     (void)d_luts;
     const int bpp = bytes_per_pixel(pixel_type);
     const int vec = aligned ? (bpp <= 2 ? 8 : 16 / bpp) : 1;
@@ -589,6 +830,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     }
     a.ws_base = ws;
     a.contrib = d_contrib;
+    a.thresh = d_thresh;
+    a.buckets = d_buckets;
+    a.use_thresh = use_thresh ? 1 : 0;
     a.out = d_out;
     a.status = d_status;
     a.flag = ctx->d_flag;
@@ -630,9 +874,14 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         if (c.mode != kModeLinear16) all_linear = false;
         if (!(c.mode == kModeLinear16 && fast_linear_ok(c, pp.plan))) all_fast = false;
     }
-    const int mode16 = all_fast ? kK2Fast16 : all_linear ? kK2Linear16 : kK2Mixed16;
+    bool all_thresh = na > 0;
+    for (int i = 0; i < na; ++i) all_thresh &= pp.plan.ch[i].mode == kModeThresh;
+    const int mode16 = bpp == 4 ? (all_thresh ? kK2Thresh : kK2Eval)
+                                : all_fast ? kK2Fast16 : all_linear ? kK2Linear16 : kK2Mixed16;
     const uint64_t per_block = (uint64_t)kBlock * cpt_thread;
-    const int grid = (int)((total + per_block - 1) / per_block);
+    a.n_work = (uint32_t)((total + per_block - 1) / per_block);
+    const bool eval_mode = bpp >= 4;     // kK2Eval: grid-stride over the work blocks
+    const int grid = eval_mode ? (int)std::min<uint64_t>(a.n_work, (uint64_t)ctx->cu_count * 8) : (int)a.n_work;
     hipError_t e;
     const bool be = big_endian != 0;
     KernelTimer timer(ctx, 2);

@@ -348,3 +348,90 @@ def test_invalid_arguments(ctx):
         host_render(ctx, chans, [p], 99, 4, 4)
     # zero-size region without a flip renders nothing and succeeds (renderAsPackedInt -> int[0])
     assert host_render(ctx, chans, [p], _lib.PIXELS_UINT16, 0, 0).size == 0
+
+
+def _edge_values(ch, pt, qd, n=65536):
+    """Pixel values that pin every code boundary of q for one channel: the oracle's codes over
+    a dense sweep of the window, every value where the code changes with its type neighbours,
+    the window ends and the type's specials (NaN, +-inf, -0, extremes)."""
+    ws, we = ch["input_start"], ch["input_end"]
+    span = we - ws
+    if pt == _lib.PIXELS_FLOAT:
+        sweep = np.linspace(ws - 0.05 * span, we + 0.05 * span, 40000).astype(np.float32)
+        dt = np.float32
+    else:
+        info = np.iinfo(np.int32 if pt == _lib.PIXELS_INT32 else np.uint32)
+        sweep = np.unique(np.clip(np.linspace(ws - 0.05 * span, we + 0.05 * span, 40000),
+                                  info.min, info.max).astype(np.int64)).astype(np.int32 if pt == _lib.PIXELS_INT32 else np.uint32)
+        dt = sweep.dtype
+    codes = np.array([O.quantize(float(x), ch) for x in sweep[:: max(1, len(sweep) // 4000)]])
+    sub = sweep[:: max(1, len(sweep) // 4000)]
+    edges = sub[1:][np.diff(codes) != 0]
+    vals = [sweep, edges]
+    if pt == _lib.PIXELS_FLOAT:
+        for e in (edges, np.float32([ws, we])):
+            vals += [np.nextafter(e, np.float32(np.inf)), np.nextafter(e, np.float32(-np.inf))]
+        vals.append(np.float32([np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 3.4e38, -3.4e38, 1e-45]))
+    else:
+        info = np.iinfo(dt)
+        vals += [(edges.astype(np.int64) + d).clip(info.min, info.max).astype(dt) for d in (-1, 1)]
+        vals.append(np.array([info.min, info.max, 0, 1, info.max - 1], dtype=dt))
+    v = np.concatenate([np.asarray(a, dtype=dt) for a in vals])
+    return np.resize(v, n).astype(dt)
+
+
+@pytest.mark.parametrize("case", [
+    dict(pt=_lib.PIXELS_FLOAT, ws=-100.5, we=1000.25),
+    dict(pt=_lib.PIXELS_FLOAT, ws=-100.5, we=1000.25, noise_reduction=True),
+    dict(pt=_lib.PIXELS_FLOAT, ws=3.0, we=700.0, cd=(10, 200, 100)),
+    dict(pt=_lib.PIXELS_FLOAT, ws=1.5, we=5000.0, family=_lib.FAMILY_LOGARITHMIC, tol=1),
+    dict(pt=_lib.PIXELS_FLOAT, ws=0.1, we=900.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5, tol=1),
+    dict(pt=_lib.PIXELS_FLOAT, ws=2.0, we=300.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, tol=1),
+    dict(pt=_lib.PIXELS_FLOAT, ws=0.5, we=50.0, family=_lib.FAMILY_EXPONENTIAL, coefficient=0.3, tol=1),
+    dict(pt=_lib.PIXELS_FLOAT, ws=-5.0, we=50.0, family=_lib.FAMILY_LOGARITHMIC, tol=1),   # Eval fallback
+    dict(pt=_lib.PIXELS_FLOAT, ws=-700.0, we=650.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5),  # a0 NaN
+    dict(pt=_lib.PIXELS_FLOAT, ws=-70.0, we=65.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, tol=1),  # Eval
+    dict(pt=_lib.PIXELS_INT32, ws=-1e9, we=2e9),
+    dict(pt=_lib.PIXELS_INT32, ws=-7.0, we=250.0, reverse=True),
+    dict(pt=_lib.PIXELS_UINT32, ws=1000.0, we=4e9),
+    dict(pt=_lib.PIXELS_UINT32, ws=10.0, we=70000.0, family=_lib.FAMILY_LOGARITHMIC, tol=1),
+])
+def test_threshold_mode_code_boundaries(ctx, case):
+    """kModeThresh (monotone q through 255 LDS thresholds) against the CPU restatement at every
+    code boundary, the window ends and NaN / inf / -0 / type extremes.  Linear: bit-exact;
+    transcendental families: +-1 (north_star float bar), with boundary flips only."""
+    case = dict(case)
+    pt, tol, cd = case.pop("pt"), case.pop("tol", 0), case.pop("cd", (0, 255, 255))
+    ch = {"input_start": f32(case.pop("ws")), "input_end": f32(case.pop("we")), "rgba": (255, 255, 255, 255)}
+    ch.update(case)
+    qd = O.make_qdef("greyscale", cd[0], cd[1], cd[2])
+    h, w = 64, 1024
+    x = _edge_values(dict(ch), pt, qd, h * w).reshape(h, w)
+    for be in (False, True):
+        src = [x.astype(x.dtype.newbyteorder(">")) if be else x]
+        st, exp = O.render([ch], src, pt, w, h, big_endian=be, qdef=qd)
+        assert st == 0
+        got = ctx.render_packed_int(qd, [ch], src, pt, w, h, big_endian=be)
+        d = np.abs((got & 0xFF).astype(int) - (exp & 0xFF).astype(int))
+        assert d.max() <= tol, f"max code diff {d.max()} at {x.reshape(-1)[np.argmax(d)]!r}"
+        if tol:
+            assert (d > 0).mean() < 0.01
+
+
+def test_mixed_threshold_and_eval_channels(ctx):
+    """One channel through thresholds (log, ws > 0), one through per-pixel double evaluation
+    (x^2 over a window that crosses 0: not monotone) in the same launch; float and int32."""
+    h, w = 64, 128
+    rng = np.random.default_rng(31)
+    for pt, dt in ((_lib.PIXELS_FLOAT, np.float32), (_lib.PIXELS_INT32, np.int32)):
+        planes = [(rng.lognormal(4, 1.2, (h, w))).astype(dt), rng.normal(0, 50, (h, w)).astype(dt)]
+        chans = [{"input_start": f32(5.0), "input_end": f32(900.0), "rgba": (255, 0, 0, 255),
+                  "family": _lib.FAMILY_LOGARITHMIC},
+                 {"input_start": f32(-60.0), "input_end": f32(70.0), "rgba": (0, 255, 255, 255),
+                  "family": _lib.FAMILY_POLYNOMIAL, "coefficient": 2.0, "reverse": True}]
+        for be in (False, True):
+            src = [p.astype(p.dtype.newbyteorder(">")) if be else p for p in planes]
+            st, exp = O.render(chans, src, pt, w, h, big_endian=be)
+            got = host_render(ctx, chans, src, pt, w, h, big_endian=be)
+            assert_argb_close(got, exp, tol=1)
+            assert np.mean(got == exp) > 0.99
