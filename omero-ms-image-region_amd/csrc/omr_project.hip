@@ -166,6 +166,138 @@ __global__ void __launch_bounds__(kBlock) k_project(K3Args A) {
     }
 }
 
+// K3v: 16-byte vector loads (one per lane per plane) when the stack is 16-B aligned and a plane
+// is a whole number of 16-B chunks.  SPLIT: the 4 waves of a block take consecutive quarters of
+// the z range for the same 64 chunks and combine through LDS in z order — legal where the
+// combine is exact: max (order-free, NaN skipped, +0 start) and integer sums (int64, exact).
+// Float / double mean and sum keep one lane per chunk walking every z in the reference order.
+#define OMR_GLOBAL __attribute__((address_space(1)))
+typedef uint32_t p32x4 __attribute__((ext_vector_type(4)));
+template <typename T> struct VecPx {
+    using U = typename Raw<T>::U;
+    static constexpr int V = 16 / (int)sizeof(T);
+    static __device__ __forceinline__ void split(const p32x4& q, U (&u)[V]) {
+        __builtin_memcpy(&u[0], &q, 16);
+    }
+};
+
+template <typename T, bool BE>
+__device__ __forceinline__ T px_of(typename Raw<T>::U u) {
+    if constexpr (BE) u = bswap_any<typename Raw<T>::U>(u);
+    T t;
+    __builtin_memcpy(&t, &u, sizeof(T));
+    return t;
+}
+
+template <typename T, bool BEI, bool BEO, int ALG, bool SPLIT>
+__global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter) {
+    using U = typename Raw<T>::U;
+    using AT = typename Acc<T>::type;
+    constexpr int V = VecPx<T>::V;
+    constexpr bool MAX = ALG == OMR_PROJECTION_MAX;
+    using Part = typename std::conditional<MAX, T, AT>::type;
+    __shared__ Part s_part[SPLIT ? 3 * 64 * V : 1];
+    const int s = blockIdx.y;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t c = SPLIT ? blockIdx.x * 64 + lane : blockIdx.x * kBlock + threadIdx.x;
+    const bool live = c < A.chunks;
+    const uint32_t cc = live ? c : A.chunks - 1;
+    const OMR_GLOBAL p32x4* base = (const OMR_GLOBAL p32x4*)(const void*)(A.stacks[s]) + cc;
+    const uint64_t pchunks = (uint64_t)A.chunks * (uint64_t)A.stepping;   // uint4s between used planes
+    const uint32_t i0 = SPLIT ? (uint32_t)((uint64_t)n_iter * wave / 4) : 0u;
+    const uint32_t i1 = SPLIT ? (uint32_t)((uint64_t)n_iter * (wave + 1) / 4) : n_iter;
+    Part acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = (Part)0;
+    const OMR_GLOBAL p32x4* p = base + ((uint64_t)A.start + 0) * A.chunks + (uint64_t)i0 * pchunks;
+    uint32_t i = i0;
+    auto fold = [&](const p32x4 q) {
+        U u[V];
+        VecPx<T>::split(q, u);
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            const T v = px_of<T, BEI>(u[j]);
+            if constexpr (MAX) { if (v > acc[j]) acc[j] = v; }   // stackValue > projectedValue (:187)
+            else acc[j] += (Part)v;
+        }
+    };
+    for (; i + 8 <= i1; i += 8, p += 8 * pchunks) {          // 8 independent 16-B loads in flight
+        p32x4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = p[u * pchunks];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) fold(q[u]);
+    }
+    for (; i < i1; ++i, p += pchunks) fold(*p);
+    if constexpr (SPLIT) {
+        if (wave > 0) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) s_part[((wave - 1) * 64 + lane) * V + j] = acc[j];
+        }
+        __syncthreads();
+        if (wave > 0) return;
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const Part v = s_part[(w * 64 + lane) * V + j];
+                if constexpr (MAX) { if (v > acc[j]) acc[j] = v; }
+                else acc[j] += v;
+            }
+    }
+    if (!live) return;
+    U o[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+        T t;
+        if constexpr (MAX) {
+            t = acc[j];
+        } else {
+            double v = (double)acc[j];
+            if (ALG == OMR_PROJECTION_MEAN) v = v / (double)n_iter;
+            if (v > type_max<T>()) v = type_max<T>();
+            t = narrow<T>(v);
+        }
+        U u;
+        __builtin_memcpy(&u, &t, sizeof(T));
+        if constexpr (BEO) u = bswap_any<U>(u);
+        o[j] = u;
+    }
+    p32x4 q;
+    __builtin_memcpy(&q, o, 16);
+    ((OMR_GLOBAL p32x4*)(void*)(A.outs[s]))[c] = q;
+}
+
+template <typename T, bool BEI, bool BEO>
+static hipError_t launch_project_v(const K3Args& a, int alg, uint32_t n_iter, bool split, uint32_t chunks16,
+                                   int n, hipStream_t s) {
+    const dim3 gs((chunks16 + 63) / 64, n), g1((chunks16 + kBlock - 1) / kBlock, n);
+    switch (alg) {
+    case OMR_PROJECTION_MAX:
+        hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MAX, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        break;
+    case OMR_PROJECTION_MEAN:
+        if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, false>), g1, dim3(kBlock), 0, s, a, n_iter);
+        break;
+    default:
+        if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, false>), g1, dim3(kBlock), 0, s, a, n_iter);
+        break;
+    }
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_project_vt(const K3Args& a, int alg, bool bei, bool beo, uint32_t n_iter, uint32_t chunks16,
+                                    int n, hipStream_t s) {
+    const bool split = alg == OMR_PROJECTION_MAX || !std::is_floating_point<T>::value;
+    if (bei) return beo ? launch_project_v<T, true, true>(a, alg, n_iter, split, chunks16, n, s)
+                        : launch_project_v<T, true, false>(a, alg, n_iter, split, chunks16, n, s);
+    return beo ? launch_project_v<T, false, true>(a, alg, n_iter, split, chunks16, n, s)
+               : launch_project_v<T, false, false>(a, alg, n_iter, split, chunks16, n, s);
+}
+
 template <typename T, bool BEI, bool BEO>
 static hipError_t launch_project_alg(const K3Args& a, int alg, dim3 grid, hipStream_t s) {
     switch (alg) {
@@ -225,6 +357,31 @@ omr_status enqueue_projection(Ctx* ctx, const void* const* d_stacks, void* const
     const bool bi = be_in != 0, bo = be_out != 0;
     hipError_t e;
     KernelTimer timer(ctx, 3);
+    // Vector path: every stack and output 16-B aligned, planes a whole number of 16-B chunks.
+    bool vec = (a.plane * bpp) % 16 == 0;
+    for (int i = 0; i < n && vec; ++i)
+        vec = reinterpret_cast<uintptr_t>(a.stacks[i]) % 16 == 0 && reinterpret_cast<uintptr_t>(a.outs[i]) % 16 == 0;
+    if (vec) {
+        const uint32_t c16 = (uint32_t)(a.plane * bpp / 16);
+        K3Args b = a;
+        b.chunks = c16;
+        // iterations: max over z in [start, end], mean/sum over z in [start, end) (ProjectionService.java:184, :271)
+        uint32_t n_iter = 0;
+        if (algorithm == OMR_PROJECTION_MAX) n_iter = end >= start ? (uint32_t)((end - start) / stepping + 1) : 0u;
+        else n_iter = end > start ? (uint32_t)((end - start + stepping - 1) / stepping) : 0u;
+        switch (pixel_type) {
+        case OMR_PIXELS_INT8: e = launch_project_vt<int8_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_UINT8: e = launch_project_vt<uint8_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_INT16: e = launch_project_vt<int16_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_UINT16: e = launch_project_vt<uint16_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_INT32: e = launch_project_vt<int32_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_UINT32: e = launch_project_vt<uint32_t>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        case OMR_PIXELS_FLOAT: e = launch_project_vt<float>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        default: e = launch_project_vt<double>(b, algorithm, bi, bo, n_iter, c16, n, ctx->stream); break;
+        }
+        OMR_HIP(ctx, e);
+        return OMR_OK;
+    }
     switch (pixel_type) {
     case OMR_PIXELS_INT8: e = launch_project_t<int8_t>(a, algorithm, bi, bo, grid, ctx->stream); break;
     case OMR_PIXELS_UINT8: e = launch_project_t<uint8_t>(a, algorithm, bi, bo, grid, ctx->stream); break;

@@ -45,6 +45,22 @@ def test_projection_bit_exact_all_types(ctx, pt, dtype, alg):
         np.testing.assert_array_equal(got, exp, err_msg=f"{start},{end},{step},{bi},{bo}")
 
 
+@pytest.mark.parametrize("pt,dtype", TYPES)
+@pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM])
+def test_projection_vector_path_all_types(ctx, pt, dtype, alg):
+    """16-B vector K3 (plane = whole 16-B chunks): z split over 4 waves for max and integer
+    sums, uneven quarters, unroll tails, start > end, stepping."""
+    z, h, w = 37, 16, 24
+    stack = rand_stack(dtype, z, h, w, 300 + pt)
+    for (start, end, step, bi, bo) in [(0, 36, 1, False, False), (2, 30, 3, True, True), (5, 5, 1, True, False),
+                                       (9, 4, 1, False, True), (0, 36, 7, True, True), (1, 34, 1, False, False)]:
+        src = stack.astype(stack.dtype.newbyteorder(">")) if bi else stack
+        st, exp = O.project(src, pt, w, h, z, alg, start, end, step, be_in=bi, be_out=bo)
+        assert st == 0
+        got = ctx.project_stack(src, pt, w, h, z, alg, start, end, step, big_endian_in=bi, big_endian_out=bo)
+        np.testing.assert_array_equal(got, exp, err_msg=f"{start},{end},{step},{bi},{bo}")
+
+
 def test_projection_device_api_and_validation(ctx):
     import torch
     z, h, w = 64, 128, 256
