@@ -617,22 +617,24 @@ omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, in
 }  // extern "C"
 
 // =====================================================================================
-// Batched JPEG: N same-size tiles per call, wave-parallel Huffman, one host sync at most.
+// Batched JPEG: N same-size tiles per call, lane-per-block Huffman, one host sync at most.
 //
 // The reference encodes every tile on its own worker thread (compressToStream per request,
 // ImageRegionRequestHandler.java:580-582).  Here a whole batch of rendered tiles (e.g. the
-// output of omr_render_batch_*_device) is encoded by six launches whose grids span all tiles:
+// output of omr_render_batch_*_device) is encoded by eight launches whose grids span all tiles:
 //   B1  k_jpeg_fdct_batch   one wave per MCU: colour, downsample, FDCT, quantise (zig-zag lane
 //                           order), plus each block's AC Huffman length by ballot arithmetic
-//   B2  k_jpeg_block_scan   one workgroup per tile: DC lengths, exclusive scan -> block bit
-//                           offsets, tile bit length, zero the tile's word slot
-//   B3  k_jpeg_huff_batch   one wave per block: every lane emits its coefficient's symbol,
-//                           a wave scan places the bits, the block is assembled in LDS and
-//                           stored (boundary words by atomicOr)
-//   B4  k_jpeg_stuff_scan   one workgroup per tile: 0xFF count per 16-byte chunk -> chunk
-//                           output offsets, stuffed length
+//   B2a k_jpeg_block_bits   one lane per block: total bit length (DC needs the previous block's
+//                           DC), sums per group of 256 blocks
+//   B2b k_jpeg_group_scan   one workgroup per tile: group bit offsets, tile bit length, zero
+//                           the tile's bit-stream words
+//   B3  k_jpeg_huff_thread  one lane per block: in-group scan -> bit offset, Huffman-code the 64
+//                           register-resident coefficients, whole words stored, shared words ORed
+//   B4a k_jpeg_stuff_count  0xFF count per 16-byte chunk of the stream, sums per 256 chunks
+//   B4b k_jpeg_group_scan   one workgroup per tile: chunk-group offsets, stuffed length
 //   B5  k_jpeg_tile_scan    one workgroup: tile output offsets (header + scan + EOI), status
-//   B6  k_jpeg_stuff_batch  stuffed bytes staged in LDS, copied out coalesced; JFIF header
+//   B6  k_jpeg_stuff_batch  per chunk group: in-group scan, stuffed bytes staged in LDS and
+//                           copied out coalesced; JFIF header
 // Output: complete JFIF files packed back to back in the caller's device buffer.
 // =====================================================================================
 
@@ -709,8 +711,12 @@ __device__ __forceinline__ void load_pair(const uint32_t* img, int W, int x, int
     }
 }
 
+// Block stride of the per-wave LDS MCU buffer: 73 words makes both FDCT passes (48 lanes on
+// rows of stride 8, then on columns) hit 48 distinct banks; 64 gave 6-way conflicts.
+constexpr int kBS = 73;
+
 __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
-    __shared__ int s[4][6 * 64 + 8];
+    __shared__ int s[4][6 * kBS + 8];
     __shared__ uint8_t s_acsize[2][256];
     for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
     __syncthreads();
@@ -729,28 +735,38 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
     const int hy = qy << 2, hc = qc << 2;
     const int m0 = (blockIdx.x * 4 + wv) * kB1McuPerWave;
-    for (int m = m0; m < min(m0 + kB1McuPerWave, A.n_mcu); ++m) {   // wave-uniform loop
+    const int m1 = min(m0 + kB1McuPerWave, A.n_mcu);
+    // The next MCU's four pixels are loaded while this one is transformed (one pass of HBM
+    // latency per wave instead of one per MCU).
+    uint32_t n00 = 0, n01 = 0, n10 = 0, n11 = 0;
+    auto fetch = [&](int m) {
+        const int mx = m % A.mcux, my = m / A.mcux;
+        const int x0 = mx * 16 + 2 * cx, y0 = my * 16 + 2 * cy;
+        const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
+        if (even_w) {
+            load_pair(img, W, min(x0, W - 1) & ~1, ya, n00, n01);
+            load_pair(img, W, min(x0, W - 1) & ~1, yb, n10, n11);
+            if (x0 > W - 1) { n00 = n01; n10 = n11; }           // both columns clamp to W-1
+        } else {
+            const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
+            n00 = img[(int64_t)ya * W + xa]; n01 = img[(int64_t)ya * W + xb];
+            n10 = img[(int64_t)yb * W + xa]; n11 = img[(int64_t)yb * W + xb];
+        }
+    };
+    if (m0 < m1) fetch(m0);
+    for (int m = m0; m < m1; ++m) {   // wave-uniform loop
         const int mx = m % A.mcux, my = m / A.mcux;
         {
-            const int x0 = mx * 16 + 2 * cx, y0 = my * 16 + 2 * cy;
-            const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
-            uint32_t p00, p01, p10, p11;
-            if (even_w) {
-                load_pair(img, W, min(x0, W - 1) & ~1, ya, p00, p01);
-                load_pair(img, W, min(x0, W - 1) & ~1, yb, p10, p11);
-                if (x0 > W - 1) { p00 = p01; p10 = p11; }           // both columns clamp to W-1
-            } else {
-                const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
-                p00 = img[(int64_t)ya * W + xa]; p01 = img[(int64_t)ya * W + xb];
-                p10 = img[(int64_t)yb * W + xa]; p11 = img[(int64_t)yb * W + xb];
-            }
+            const int x0 = mx * 16 + 2 * cx;
+            uint32_t p00 = n00, p01 = n01, p10 = n10, p11 = n11;
+            if (m + 1 < m1) fetch(m + 1);
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
             const int o = ((2 * cy) & 7) * 8 + ((2 * cx) & 7);
-            ycc(p00, y, cb0, cr0); S[blk * 64 + o] = y - 128;
-            ycc(p01, y, cb1, cr1); S[blk * 64 + o + 1] = y - 128;
-            ycc(p10, y, cb2, cr2); S[blk * 64 + o + 8] = y - 128;
-            ycc(p11, y, cb3, cr3); S[blk * 64 + o + 9] = y - 128;
+            ycc(p00, y, cb0, cr0); S[blk * kBS + o] = y - 128;
+            ycc(p01, y, cb1, cr1); S[blk * kBS + o + 1] = y - 128;
+            ycc(p10, y, cb2, cr2); S[blk * kBS + o + 8] = y - 128;
+            ycc(p11, y, cb3, cr3); S[blk * kBS + o + 9] = y - 128;
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             if (cyg >= chv) {
@@ -761,17 +777,17 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
                 ycc(p00, y, cb0, cr0); ycc(p01, y, cb1, cr1); ycc(p10, y, cb2, cr2); ycc(p11, y, cb3, cr3);
             }
             const int bias = (cx & 1) ? 2 : 1;
-            S[4 * 64 + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
-            S[5 * 64 + cy * 8 + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
+            S[4 * kBS + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
+            S[5 * kBS + cy * 8 + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < 48) fdct8<0>(S + (lane >> 3) * 64 + (lane & 7) * 8, 1);
+        if (lane < 48) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * 8, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < 48) fdct8<1>(S + (lane >> 3) * 64 + (lane & 7), 8);
+        if (lane < 48) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), 8);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -781,7 +797,7 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
         uint32_t aclen[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            int q = k < 4 ? quant_recip(S[k * 64 + nat], hy, my_) : quant_recip(S[k * 64 + nat], hc, mc_);
+            int q = k < 4 ? quant_recip(S[k * kBS + nat], hy, my_) : quant_recip(S[k * kBS + nat], hc, mc_);
             if (k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
@@ -838,133 +854,171 @@ __device__ __forceinline__ uint32_t dc_bits(const int16_t* dcs, int b, const Huf
 }
 
 constexpr int kTileThreads = 1024;
+constexpr int kGrp = 256;   // blocks per B3 workgroup = chunks per B4a/B6 group
 
-struct B2Args {
+__device__ __forceinline__ uint32_t block_reduce_sum(uint32_t v, uint32_t* s_wave) {
+    uint32_t total;
+    block_exclusive_scan(v, s_wave, total);
+    return total;
+}
+
+// B2a: one lane per 8x8 block: its bit length (AC part from B1, DC part needs the previous
+// block's DC in scan order); per-256-block group sums.
+struct B2aArgs {
     const uint16_t* aclen;
     const int16_t* dcs;
-    uint32_t* offs;        // [tile][nb] bit offset of each block inside its tile
-    uint32_t* tile_bits;   // [tile]
-    uint32_t* words;       // [tile][slot_words]
-    int32_t nb;
-    int64_t slot_words;
+    uint16_t* bits;        // [tile][nb]
+    uint32_t* gsum;        // [tile][ngb]
+    int32_t nb, ngb;
 };
 
-__global__ void __launch_bounds__(kTileThreads) k_jpeg_block_scan(B2Args A) {
-    __shared__ HuffLds h;
+__global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
+    __shared__ uint8_t s_dc[2][16];
     __shared__ uint32_t sw[16];
-    load_huff_lds(h);
+    if (threadIdx.x < 32) s_dc[threadIdx.x >> 4][threadIdx.x & 15] = c_huff[2 * (threadIdx.x >> 4)].size[threadIdx.x & 15];
     __syncthreads();
-    const int tile = blockIdx.x;
-    const uint16_t* acl = A.aclen + (int64_t)tile * A.nb;
-    const int16_t* dcs = A.dcs + (int64_t)tile * A.nb;
-    uint32_t* offs = A.offs + (int64_t)tile * A.nb;
-    const int per = (A.nb + kTileThreads - 1) / kTileThreads;
-    const int i0 = min(A.nb, (int)threadIdx.x * per), i1 = min(A.nb, i0 + per);
-    uint32_t sum = 0;
-    for (int b = i0; b < i1; ++b) sum += acl[b] + dc_bits(dcs, b, h);
-    uint32_t total;
-    uint32_t run = block_exclusive_scan(sum, sw, total);
-    for (int b = i0; b < i1; ++b) {
-        offs[b] = run;
-        run += acl[b] + dc_bits(dcs, b, h);
+    const int tile = blockIdx.y, b = blockIdx.x * kGrp + threadIdx.x;
+    uint32_t bits = 0;
+    if (b < A.nb) {
+        const int16_t* dcs = A.dcs + (int64_t)tile * A.nb;
+        const int pb = prev_block_in_tile(b);
+        int d = dcs[b] - (pb >= 0 ? dcs[pb] : 0);
+        if (d < 0) d = -d;
+        const int nbits = d ? 32 - __clz(d) : 0;
+        bits = A.aclen[(int64_t)tile * A.nb + b] + s_dc[(b % 6) < 4 ? 0 : 1][nbits] + nbits;
+        A.bits[(int64_t)tile * A.nb + b] = (uint16_t)bits;
     }
-    if (threadIdx.x == 0) A.tile_bits[tile] = total;
-    const uint32_t nw = (total + 31) / 32 + 1;
-    uint32_t* w = A.words + (int64_t)tile * A.slot_words;
-    for (uint32_t i = threadIdx.x; i < nw; i += kTileThreads) w[i] = 0;
+    const uint32_t total = block_reduce_sum(bits, sw);
+    if (threadIdx.x == 0) A.gsum[(int64_t)tile * A.ngb + blockIdx.x] = total;
+}
+
+// B2b / B4b: one workgroup per tile: exclusive scan of its group sums (in place), the tile
+// total, and (B2b) zeroing of the words the tile's bit stream will occupy.
+struct GroupScanArgs {
+    uint32_t* gsum;              // [tile][stride] -> exclusive offsets
+    const uint32_t* n_groups;    // [tile] (nullptr: fixed_groups)
+    uint32_t* total;             // [tile]
+    uint32_t* zero_words;        // B2b: [tile][slot_words] zero-filled up to the total (or nullptr)
+    const uint32_t* base_add;    // B4b: total += base_add-derived byte count (or nullptr)
+    int64_t stride, slot_words;
+    int32_t fixed_groups;
+};
+
+__global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs A) {
+    __shared__ uint32_t sw[16];
+    __shared__ uint32_t carry;
+    const int tile = blockIdx.x;
+    uint32_t* g = A.gsum + (int64_t)tile * A.stride;
+    const uint32_t ng = A.n_groups ? A.n_groups[tile] : (uint32_t)A.fixed_groups;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < ng; base += kTileThreads) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < ng ? g[i] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_exclusive_scan(v, sw, tot);
+        const uint32_t c = carry;
+        if (i < ng) g[i] = c + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) carry = c + tot;
+        __syncthreads();
+    }
+    uint32_t total = carry;
+    if (A.base_add) total += (A.base_add[tile] + 7) / 8;   // B4b: stuffed bytes = bytes + 0xFF count
+    if (threadIdx.x == 0) A.total[tile] = total;
+    if (A.zero_words) {                                    // B2b: the tile's bit stream words
+        const uint32_t nw = (total + 31) / 32 + 1;
+        uint4* w4 = reinterpret_cast<uint4*>(A.zero_words + (int64_t)tile * A.slot_words);
+        for (uint32_t i = threadIdx.x; i < (nw + 3) / 4; i += kTileThreads) w4[i] = make_uint4(0, 0, 0, 0);
+    }
 }
 
 struct B3Args {
     const int16_t* coefs;
     const int16_t* dcs;
-    const uint32_t* offs;
+    const uint16_t* bits;    // [tile][nb]
+    const uint32_t* goff;    // [tile][ngb] exclusive bit offset of each 256-block group
     uint32_t* words;
-    int32_t nb;
+    int32_t nb, ngb;
     int64_t slot_words;
 };
 
-constexpr int kBlkWords = 132;   // <= 64 lanes x 63 bits + 31 bits of start offset
-
-constexpr int kB3BlocksPerWave = 16;
-
-__global__ void __launch_bounds__(256) k_jpeg_huff_batch(B3Args A) {
+// B3: one lane per 8x8 block; the workgroup's 256 consecutive blocks find their bit offsets
+// by a block scan on top of the group offset.  The block's 64 zig-zag coefficients arrive as
+// eight 16-byte loads into registers (the loop over them is unrolled, so every coefficient is
+// a static register), the codes come from the LDS Huffman tables and accumulate in a 64-bit
+// register; whole 32-bit words are stored directly, the two words a block may share with its
+// neighbours are ORed in.
+__global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     __shared__ HuffLds h;
-    __shared__ uint32_t sbuf[4][kBlkWords];
+    __shared__ uint32_t sw[16];
     load_huff_lds(h);
-    __syncthreads();
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    uint32_t* buf = sbuf[wv];
     const int tile = blockIdx.y;
-    const int bbeg = (blockIdx.x * 4 + wv) * kB3BlocksPerWave;
-    const int bend = min(bbeg + kB3BlocksPerWave, A.nb);
-    const int16_t* tdcs = A.dcs + (int64_t)tile * A.nb;
-    uint32_t* twords = A.words + (int64_t)tile * A.slot_words;
-    for (int b = bbeg; b < bend; ++b) {                   // wave-uniform
-        for (int i = lane; i < kBlkWords; i += 64) buf[i] = 0;
-        const int64_t gb = (int64_t)tile * A.nb + b;
-        const int v = A.coefs[gb * 64 + lane];
-        const int k = b % 6;
-        const int td = k < 4 ? 0 : 2, ta = td + 1;
-        const uint64_t nz = __ballot(lane != 0 && v != 0);
-        const int last = nz ? 63 - __clzll(nz) : 0;
-        uint64_t code = 0;
-        uint32_t len = 0;
-        auto put = [&](uint32_t c, uint32_t n) { code = (code << n) | (c & ((1u << n) - 1)); len += n; };
-        if (lane == 0) {
-            const int pb = prev_block_in_tile(b);
-            int d = v - (pb >= 0 ? tdcs[pb] : 0);
-            int d2 = d;
-            if (d < 0) { d = -d; d2--; }
-            const int nbits = d ? 32 - __clz(d) : 0;
-            put(h.code[td][nbits], h.size[td][nbits]);
-            if (nbits) put((uint32_t)d2, nbits);
-        } else if (v != 0) {
-            const uint64_t below = nz & ((1ull << lane) - 1);
-            const int prev = below ? 63 - __clzll(below) : 0;
-            int r = lane - prev - 1;
+    const int b = blockIdx.x * kGrp + threadIdx.x;
+    const int64_t gb = (int64_t)tile * A.nb + b;
+    const uint32_t mybits = b < A.nb ? A.bits[gb] : 0u;
+    uint32_t gtot;
+    const uint32_t boff = A.goff[(int64_t)tile * A.ngb + blockIdx.x] + block_exclusive_scan(mybits, sw, gtot);
+    if (b >= A.nb) return;
+    const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
+    uint4 q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = src[i];
+    const int pb = prev_block_in_tile(b);
+    const int pred = pb >= 0 ? A.dcs[(int64_t)tile * A.nb + pb] : 0;
+    uint32_t* words = A.words + (int64_t)tile * A.slot_words;
+    uint64_t acc = 0;
+    int nacc = (int)(boff & 31);
+    uint32_t wpos = boff >> 5;
+    bool first = true;
+    auto put = [&](uint32_t v, int n) {          // n <= 16
+        acc = (acc << n) | (v & ((1u << n) - 1));
+        nacc += n;
+        if (nacc >= 32) {
+            const uint32_t w = (uint32_t)(acc >> (nacc - 32));
+            if (first) atomicOr(&words[wpos], w);   // shares bits with the previous block
+            else words[wpos] = w;
+            first = false;
+            ++wpos;
+            nacc -= 32;
+        }
+    };
+    auto coef = [&](int k) -> int {
+        const uint32_t* d = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
+        const uint32_t w = d[(k >> 1) & 3];
+        return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
+    };
+    const int kk = b % 6;
+    const int td = kk < 4 ? 0 : 2, ta = td + 1;
+    {
+        int d = coef(0) - pred, d2 = d;
+        if (d < 0) { d = -d; d2--; }
+        const int nbits = d ? 32 - __clz(d) : 0;
+        put(h.code[td][nbits], h.size[td][nbits]);
+        if (nbits) put((uint32_t)d2, nbits);
+    }
+    int r = 0;
+#pragma unroll
+    for (int k = 1; k < 64; ++k) {
+        const int c = coef(k);
+        if (c == 0) {
+            ++r;
+        } else {
             while (r > 15) { put(h.code[ta][0xF0], h.size[ta][0xF0]); r -= 16; }
-            int a = v, a2 = v;
+            int a = c, a2 = c;
             if (a < 0) { a = -a; a2--; }
             const int nbits = 32 - __clz(a);
             const int sym = (r << 4) + nbits;
             put(h.code[ta][sym], h.size[ta][sym]);
             put((uint32_t)a2, nbits);
+            r = 0;
         }
-        if (lane == last && last < 63) put(h.code[ta][0], h.size[ta][0]);   // EOB
-        uint32_t blen;
-        const uint32_t pre = wave_exclusive(len, blen);
-        const uint32_t boff = A.offs[gb];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (len) {
-            const uint32_t p = (boff & 31) + pre;            // local bit position in buf
-            const uint32_t w0 = p >> 5, sh = p & 31;
-            const uint64_t hi = code << (64 - len);          // MSB-aligned, len >= 1
-            atomicOr(&buf[w0], (uint32_t)(hi >> 32) >> sh);
-            if (sh + len > 32) {
-                const uint64_t rest = hi << (32 - sh);
-                atomicOr(&buf[w0 + 1], (uint32_t)(rest >> 32));
-                if (sh + len > 64) atomicOr(&buf[w0 + 2], (uint32_t)rest);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const uint32_t nwords = ((boff & 31) + blen + 31) >> 5;
-        uint32_t* dst = twords + (boff >> 5);
-        for (uint32_t i = lane; i < nwords; i += 64) {
-            const uint32_t wv2 = buf[i];
-            if (i == 0 || i == nwords - 1) atomicOr(&dst[i], wv2);
-            else dst[i] = wv2;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // buf is cleared for the next block
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
+    if (r > 0) put(h.code[ta][0], h.size[ta][0]);   // EOB
+    if (nacc > 0) atomicOr(&words[wpos], (uint32_t)(acc << (32 - nacc)));   // shared with the next block
 }
 
-constexpr int kStuffBytes = 16;   // bytes per chunk in B4/B6
+constexpr int kStuffBytes = 16;   // bytes per chunk in B4a/B6
 
 __device__ __forceinline__ uint32_t seg_byte(const uint32_t* words, uint32_t i, uint32_t nbytes, uint32_t tb) {
     uint32_t b = (words[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
@@ -972,40 +1026,52 @@ __device__ __forceinline__ uint32_t seg_byte(const uint32_t* words, uint32_t i, 
     return b;
 }
 
-struct B4Args {
+// The 16 bytes of chunk c (big-endian bytes of 4 words), pad bits of the final byte set.
+__device__ __forceinline__ void chunk_bytes(const uint32_t* words, uint32_t c, uint32_t nbytes, uint32_t tb,
+                                            uint32_t (&w)[4]) {
+    const uint4 q = reinterpret_cast<const uint4*>(words)[c];
+    w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+    const uint32_t last = nbytes - 1;
+    if ((tb & 7) && last >= c * kStuffBytes && last < (c + 1) * kStuffBytes) {
+        const uint32_t i = last - c * kStuffBytes;
+        w[i >> 2] |= (0xFFu >> (tb & 7)) << (24 - 8 * (i & 3));
+    }
+}
+
+// B4a: 0xFF count of every 16-byte chunk of the entropy-coded segment (u8) and per-256-chunk
+// group sums; a grid-stride loop over the tile's groups (the grid is sized for typical streams).
+struct B4aArgs {
     const uint32_t* words;
     const uint32_t* tile_bits;
-    uint32_t* chunk_off;   // [tile][slot_chunks] stuffed byte offset of each chunk
-    uint32_t* stuffed;     // [tile] stuffed entropy-coded length
-    int64_t slot_words, slot_chunks;
+    uint8_t* cnt;          // [tile][slot_chunks]
+    uint32_t* csum;        // [tile][slot_groups]
+    uint32_t* n_groups;    // [tile]
+    int64_t slot_words, slot_chunks, slot_groups;
 };
 
-__global__ void __launch_bounds__(kTileThreads) k_jpeg_stuff_scan(B4Args A) {
+__global__ void __launch_bounds__(kGrp) k_jpeg_stuff_count(B4aArgs A) {
     __shared__ uint32_t sw[16];
-    __shared__ uint32_t carry;
-    const int tile = blockIdx.x;
+    const int tile = blockIdx.y;
     const uint32_t tb = A.tile_bits[tile], nbytes = (tb + 7) / 8;
     const uint32_t nch = (nbytes + kStuffBytes - 1) / kStuffBytes;
+    const uint32_t ng = (nch + kGrp - 1) / kGrp;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.n_groups[tile] = ng;
     const uint32_t* words = A.words + (int64_t)tile * A.slot_words;
-    uint32_t* co = A.chunk_off + (int64_t)tile * A.slot_chunks;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < nch; base += kTileThreads) {
-        const uint32_t c = base + threadIdx.x;
+    for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
+        const uint32_t c = g * kGrp + threadIdx.x;
         uint32_t n = 0;
         if (c < nch) {
-            const uint32_t e = min(nbytes, (c + 1) * kStuffBytes);
-            for (uint32_t i = c * kStuffBytes; i < e; ++i) n += seg_byte(words, i, nbytes, tb) == 0xFF;
+            uint32_t w[4];
+            chunk_bytes(words, c, nbytes, tb, w);
+            const uint32_t e = min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes);
+#pragma unroll
+            for (int i = 0; i < kStuffBytes; ++i)
+                n += (i < (int)e && ((w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF) == 0xFF) ? 1u : 0u;
+            A.cnt[(int64_t)tile * A.slot_chunks + c] = (uint8_t)n;
         }
-        uint32_t total;
-        const uint32_t ex = block_exclusive_scan(n, sw, total);
-        const uint32_t cr = carry;
-        if (c < nch) co[c] = c * kStuffBytes + cr + ex;
-        __syncthreads();
-        if (threadIdx.x == 0) carry = cr + total;
-        __syncthreads();
+        const uint32_t total = block_reduce_sum(n, sw);
+        if (threadIdx.x == 0) A.csum[(int64_t)tile * A.slot_groups + g] = total;
     }
-    if (threadIdx.x == 0) A.stuffed[tile] = nbytes + carry;
 }
 
 __device__ __forceinline__ uint64_t block_exclusive_scan64(uint64_t v, uint64_t* s_wave, uint64_t& total) {
@@ -1075,74 +1141,81 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_tile_scan(B5Args A) {
 struct B6Args {
     const uint32_t* words;
     const uint32_t* tile_bits;
-    const uint32_t* chunk_off;
+    const uint8_t* cnt;
+    const uint32_t* coff;    // [tile][slot_groups] exclusive 0xFF count before each group
     const uint64_t* offsets;
     const uint32_t* lengths;
     const uint8_t* hdr;
     uint8_t* out;
-    int64_t slot_words, slot_chunks;
+    int64_t slot_words, slot_chunks, slot_groups;
     int32_t hdr_len;
 };
 
-constexpr int kB6Threads = 256;
-
-__global__ void __launch_bounds__(kB6Threads) k_jpeg_stuff_batch(B6Args A) {
-    __shared__ uint8_t sbytes[kB6Threads * kStuffBytes * 2];
-    __shared__ uint32_t s_end;
+// B6: per group of 256 chunks: in-group scan of the 0xFF counts, stuffed bytes staged in LDS,
+// copied out coalesced.  Block 0 of each tile also writes the JFIF header.
+__global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
+    __shared__ uint8_t sbytes[kGrp * kStuffBytes * 2];
+    __shared__ uint32_t sw[16];
     const int tile = blockIdx.y;
     if (A.lengths[tile] == 0) return;          // did not fit: status says so
     uint8_t* out = A.out + A.offsets[tile];
     if (blockIdx.x == 0)
-        for (int i = threadIdx.x; i < A.hdr_len; i += kB6Threads) out[i] = A.hdr[i];
+        for (int i = threadIdx.x; i < A.hdr_len; i += kGrp) out[i] = A.hdr[i];
     out += A.hdr_len;
     const uint32_t tb = A.tile_bits[tile], nbytes = (tb + 7) / 8;
     const uint32_t nch = (nbytes + kStuffBytes - 1) / kStuffBytes;
+    const uint32_t ng = (nch + kGrp - 1) / kGrp;
     const uint32_t* words = A.words + (int64_t)tile * A.slot_words;
-    const uint32_t* co = A.chunk_off + (int64_t)tile * A.slot_chunks;
-    // grid-stride over groups of kB6Threads chunks (the grid is sized for typical streams,
-    // not the worst-case slot)
-    for (uint32_t c0 = blockIdx.x * kB6Threads; c0 < nch; c0 += gridDim.x * kB6Threads) {
-        const uint32_t c = c0 + threadIdx.x;
-        const uint32_t cend = min(nch, c0 + kB6Threads);
-        const uint32_t base = co[c0];
+    for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
+        const uint32_t c = g * kGrp + threadIdx.x;
+        const uint32_t n = c < nch ? A.cnt[(int64_t)tile * A.slot_chunks + c] : 0u;
+        uint32_t gtot;
+        const uint32_t ex = block_exclusive_scan(n, sw, gtot);
+        uint32_t o = threadIdx.x * kStuffBytes + ex;
         if (c < nch) {
-            uint32_t o = co[c] - base;
-            const uint32_t e = min(nbytes, (c + 1) * kStuffBytes);
-            for (uint32_t i = c * kStuffBytes; i < e; ++i) {
-                const uint32_t b = seg_byte(words, i, nbytes, tb);
-                sbytes[o++] = (uint8_t)b;
-                if (b == 0xFF) sbytes[o++] = 0;
+            uint32_t w[4];
+            chunk_bytes(words, c, nbytes, tb, w);
+            const uint32_t e = min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes);
+            for (uint32_t i = 0; i < e; ++i) {
+                const uint32_t bv = (w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
+                sbytes[o++] = (uint8_t)bv;
+                if (bv == 0xFF) sbytes[o++] = 0;
             }
-            if (c == cend - 1) s_end = o;
         }
         __syncthreads();
-        const uint32_t n = s_end;
-        for (uint32_t i = threadIdx.x; i < n; i += kB6Threads) out[base + i] = sbytes[i];
+        const uint32_t gbytes = min(nbytes - g * kGrp * kStuffBytes, (uint32_t)(kGrp * kStuffBytes)) + gtot;
+        const uint64_t base = (uint64_t)g * kGrp * kStuffBytes + A.coff[(int64_t)tile * A.slot_groups + g];
+        for (uint32_t i = threadIdx.x; i < gbytes; i += kGrp) out[base + i] = sbytes[i];
         __syncthreads();
     }
 }
 
 // Batch workspace layout.
 struct JpegBatchLayout {
-    int64_t n_mcu, nb, slot_words, slot_chunks;
-    size_t coef, aclen, dcs, offs, tbits, words, chunk, stuffed, hdr, total;
+    int64_t n_mcu, nb, ngb, slot_words, slot_chunks, slot_groups;
+    size_t coef, aclen, dcs, bits, gsum, tbits, words, cnt, csum, ngroups, stuffed, hdr, total;
 };
 
 static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
     JpegBatchLayout L{};
     L.n_mcu = (int64_t)((W + 15) / 16) * ((H + 15) / 16);
     L.nb = L.n_mcu * 6;
-    L.slot_words = (L.nb * 1700 + 31) / 32 + 2;
-    L.slot_chunks = (L.slot_words * 4 + kStuffBytes - 1) / kStuffBytes + 1;
+    L.ngb = (L.nb + kGrp - 1) / kGrp;
+    L.slot_words = ((L.nb * 1700 + 31) / 32 + 2 + 3) / 4 * 4;      // 16-B aligned tile slots
+    L.slot_chunks = L.slot_words * 4 / kStuffBytes;
+    L.slot_groups = (L.slot_chunks + kGrp - 1) / kGrp;
     size_t o = align_up(base, 256);
     auto take = [&](size_t bytes) { const size_t r = o; o = align_up(o + bytes, 256); return r; };
     L.coef = take((size_t)n * L.nb * 128);
     L.aclen = take((size_t)n * L.nb * 2);
     L.dcs = take((size_t)n * L.nb * 2);
-    L.offs = take((size_t)n * L.nb * 4);
+    L.bits = take((size_t)n * L.nb * 2);
+    L.gsum = take((size_t)n * L.ngb * 4);
     L.tbits = take((size_t)n * 4);
     L.words = take((size_t)n * L.slot_words * 4);
-    L.chunk = take((size_t)n * L.slot_chunks * 4);
+    L.cnt = take((size_t)n * L.slot_chunks);
+    L.csum = take((size_t)n * L.slot_groups * 4);
+    L.ngroups = take((size_t)n * 4);
     L.stuffed = take((size_t)n * 4);
     L.hdr = take(1024);
     L.total = o;
@@ -1159,6 +1232,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     omr_status sst = stage_h2d(ctx, ws + L.hdr, hdr.data(), hdr.size());   // pinned ring: async-safe
     if (sst) return sst;
+    auto u32 = [&](size_t off) { return reinterpret_cast<uint32_t*>(ws + off); };
     B1Args a1;
     a1.argb = d_argb;
     a1.tile_stride = tile_stride;
@@ -1171,14 +1245,19 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     a1.n_mcu = (int32_t)L.n_mcu;
     a1.nb = (int32_t)L.nb;
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
-    B2Args a2{a1.aclen, a1.dcs, reinterpret_cast<uint32_t*>(ws + L.offs), reinterpret_cast<uint32_t*>(ws + L.tbits),
-              reinterpret_cast<uint32_t*>(ws + L.words), (int32_t)L.nb, L.slot_words};
-    B3Args a3{a1.coefs, a1.dcs, a2.offs, a2.words, (int32_t)L.nb, L.slot_words};
-    B4Args a4{a2.words, a2.tile_bits, reinterpret_cast<uint32_t*>(ws + L.chunk),
-              reinterpret_cast<uint32_t*>(ws + L.stuffed), L.slot_words, L.slot_chunks};
-    B5Args a5{a4.stuffed, d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
-    B6Args a6{a2.words, a2.tile_bits, a4.chunk_off, d_offsets, d_lengths, ws + L.hdr, d_out, L.slot_words,
-              L.slot_chunks, (int32_t)hdr.size()};
+    uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
+    B2aArgs a2{a1.aclen, a1.dcs, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
+    GroupScanArgs a2b{u32(L.gsum), nullptr, u32(L.tbits), u32(L.words), nullptr, L.ngb, L.slot_words, (int32_t)L.ngb};
+    B3Args a3{a1.coefs, a1.dcs, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
+    B4aArgs a4{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), u32(L.ngroups), L.slot_words, L.slot_chunks,
+               L.slot_groups};
+    GroupScanArgs a4b{u32(L.csum), u32(L.ngroups), u32(L.stuffed), nullptr, u32(L.tbits), L.slot_groups, 0, 0};
+    B5Args a5{u32(L.stuffed), d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
+    B6Args a6{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), d_offsets, d_lengths, ws + L.hdr, d_out,
+              L.slot_words, L.slot_chunks, L.slot_groups, (int32_t)hdr.size()};
+    // chunk groups of a typical stream (<= ~2 B per pixel); longer streams loop in B4a/B6
+    const int64_t est_groups = std::max<int64_t>(1, std::min<int64_t>(L.slot_groups,
+                                   ((int64_t)W * H * 2 / kStuffBytes + kGrp - 1) / kGrp));
     KernelTimer whole(ctx, 4);
     {
         KernelTimer t(ctx, 5);
@@ -1186,19 +1265,16 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
                                                     (unsigned)n), dim3(256), 0,
                            ctx->stream, a1);
     }
-    hipLaunchKernelGGL(k_jpeg_block_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a2);
+    hipLaunchKernelGGL(k_jpeg_block_bits, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a2);
+    hipLaunchKernelGGL(k_jpeg_group_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a2b);
     {
         KernelTimer t(ctx, 6);
-        hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((unsigned)((L.nb + 4 * kB3BlocksPerWave - 1) / (4 * kB3BlocksPerWave)),
-                                                   (unsigned)n), dim3(256), 0,
-                           ctx->stream, a3);
+        hipLaunchKernelGGL(k_jpeg_huff_thread, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a3);
     }
-    hipLaunchKernelGGL(k_jpeg_stuff_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a4);
+    hipLaunchKernelGGL(k_jpeg_stuff_count, dim3((unsigned)est_groups, (unsigned)n), dim3(kGrp), 0, ctx->stream, a4);
+    hipLaunchKernelGGL(k_jpeg_group_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a4b);
     hipLaunchKernelGGL(k_jpeg_tile_scan, dim3(1), dim3(kTileThreads), 0, ctx->stream, a5);
-    // ~4 chunk groups per 1024^2 tile at typical rates; larger streams loop
-    const int64_t groups = std::max<int64_t>(1, std::min<int64_t>(64, (L.nb * 16 / kStuffBytes) / kB6Threads));
-    hipLaunchKernelGGL(k_jpeg_stuff_batch, dim3((unsigned)groups, (unsigned)n),
-                       dim3(kB6Threads), 0, ctx->stream, a6);
+    hipLaunchKernelGGL(k_jpeg_stuff_batch, dim3((unsigned)est_groups, (unsigned)n), dim3(kGrp), 0, ctx->stream, a6);
     OMR_HIP(ctx, hipGetLastError());
     return OMR_OK;
 }
