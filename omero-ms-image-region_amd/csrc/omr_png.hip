@@ -164,23 +164,34 @@ __global__ void k_png_adler(PngArgs A) {
     t[0] = adler >> 24; t[1] = adler >> 16; t[2] = adler >> 8; t[3] = adler;
 }
 
-constexpr int kCrcSeg = 2048;
+constexpr int kCrcSeg = 128;
 
-// CRC-32 of chunk type + data = bytes [4, 8 + zlen) of the chunk buffer, in segments.
+// CRC-32 of chunk type + data = bytes [4, 8 + zlen) of the chunk buffer: one 128-byte segment
+// per lane (a short serial table walk), each segment's CRC shifted to the end of the data by
+// x^(8n) mod P, XOR-combined within the workgroup and once per workgroup in memory.
 __global__ void __launch_bounds__(256) k_png_crc(PngArgs A) {
     __shared__ uint32_t t[256];
+    __shared__ uint32_t s_x[4];
     t[threadIdx.x] = c_crc.t[threadIdx.x];
     __syncthreads();
     const int64_t n = 4 + A.zlen;
     const uint8_t* d = A.chunk + 4;
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t b0 = s * kCrcSeg;
-    if (b0 >= n) return;
-    const int64_t b1 = min(n, b0 + kCrcSeg);
-    uint32_t r = 0xFFFFFFFFu;
-    for (int64_t i = b0; i < b1; ++i) r = t[(r ^ d[i]) & 0xFF] ^ (r >> 8);
-    const uint32_t crc = ~r;
-    atomicXor(A.crc_out, multmodp(x2nmodp((uint64_t)(n - b1), 3), crc));
+    uint32_t v = 0;
+    if (b0 < n) {
+        const int64_t b1 = min(n, b0 + kCrcSeg);
+        uint32_t r = 0xFFFFFFFFu;
+        for (int64_t i = b0; i < b1; ++i) r = t[(r ^ d[i]) & 0xFF] ^ (r >> 8);
+        v = multmodp(x2nmodp((uint64_t)(n - b1), 3), ~r);
+    }
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) s_x[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t x = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
+        if (x) atomicXor(A.crc_out, x);
+    }
 }
 
 __global__ void k_png_finish(PngArgs A) {
