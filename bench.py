@@ -387,6 +387,81 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
     return r
 
 
+def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
+    """The step before the path: C2 tiles read from a ROMIO repository
+    file (big-endian XYZCT planes, as pixelsService.getPixelBuffer opens, ImageRegionRequestHandler
+    .java:302-309) by omr_render_pixel_buffer_tiles: pread into pinned staging, H2D on a copy
+    stream, K1+K2, ARGB back to the host (pinned or pageable) or kept in HBM and JPEG-encoded
+    there (only the JPEG files cross PCIe).  The file is a 4096x4096 4-channel uint16 image
+    (128 MiB, page-cache resident after writing); requests walk its 16 tiles repeatedly."""
+    import tempfile
+    import numpy as np
+    from omr import PixelBuffer, _lib, write_romio
+    from omr.context import make_bindings, make_qdef
+    from omr.synthetic import c2_channels
+    host = uniq.cpu().numpy().view(np.uint16).byteswap()      # native values of the BE tiles
+    grid = 4
+    img = np.empty((1, CHANNELS, 1, grid * TILE, grid * TILE), dtype=np.uint16)
+    for ty in range(grid):
+        for tx in range(grid):
+            img[0, :, 0, ty * TILE:(ty + 1) * TILE, tx * TILE:(tx + 1) * TILE] = host[(ty * grid + tx) % host.shape[0]]
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    fd, path = tempfile.mkstemp(prefix="omr_romio_", dir=d)
+    os.close(fd)
+    res = {"file": f"4096x4096x4ch uint16 ROMIO ({img.nbytes >> 20} MiB, {'tmpfs' if d else 'tmp'})",
+           "tiles_per_call": n_req, "pcie_bytes_per_tile_in": CHANNELS * TILE * TILE * 2}
+    try:
+        write_romio(path, img, _lib.PIXELS_UINT16)
+        qd = make_qdef("rgb")
+        chans = c2_channels(CHANNELS)
+        binds = make_bindings(chans)
+        reqs = [(0, 0, (i % grid) * TILE, ((i // grid) % grid) * TILE) for i in range(n_req)]
+        pb = PixelBuffer(path, grid * TILE, grid * TILE, 1, CHANNELS, 1, _lib.PIXELS_UINT16)
+        dev_out = torch.empty((n_req, TILE, TILE), dtype=torch.int32, device=uniq.device)
+        pageable = np.empty((n_req, TILE, TILE), dtype=np.uint32)
+        nbytes = n_req * TILE * TILE * 4
+        pin = _lib.lib.omr_pinned_alloc(ctx.h, nbytes)
+        import ctypes
+        pinned = np.ctypeslib.as_array((ctypes.c_uint32 * (n_req * TILE * TILE)).from_address(pin)).reshape(
+            n_req, TILE, TILE)
+        jpeg_cap = n_req * (TILE * TILE * 3)
+        d_jpg = torch.empty(jpeg_cap, dtype=torch.uint8, device=uniq.device)
+        offs = torch.empty(n_req, dtype=torch.int64, device=uniq.device)
+        lens = torch.empty(n_req, dtype=torch.int32, device=uniq.device)
+        stat = torch.empty(n_req, dtype=torch.int32, device=uniq.device)
+
+        def to_jpeg():
+            ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE, out=dev_out, bindings=binds)
+            ctx.encode_jpeg_batch_device(dev_out, n_req, TILE, TILE, 0.9, d_jpg, offs, lens, stat)
+            ln = lens.cpu()
+            end = int((offs.cpu() + ln.to(torch.int64)).max())
+            return d_jpg[:end].cpu()
+        modes = {
+            "device_out": lambda: ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE, out=dev_out,
+                                                                bindings=binds),
+            "host_pinned_out": lambda: ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE, out=pinned,
+                                                                     bindings=binds),
+            "host_pageable_out": lambda: ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
+                                                                       out=pageable, bindings=binds),
+            "to_jpeg_host": to_jpeg,
+        }
+        for name, fn in modes.items():
+            fn()
+            ctx.synchronize()
+            reps = 3
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            ctx.synchronize()
+            el = time.perf_counter() - t0
+            res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
+        _lib.lib.omr_pinned_free(ctx.h, pin)
+        pb.close()
+    finally:
+        os.unlink(path)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -490,6 +565,12 @@ def main():
             extra["jpeg"] = jpeg_section(torch, ctx, data, min(args.jpeg_batch, B), args.jpeg_steps,
                                          2, args.cpu_seconds / 2, threads, not args.no_cpu_baseline)
         if not args.no_configs:
+            try:
+                extra["host_fed"] = host_fed_section(torch, ctx, uniq, 64, args.cpu_seconds / 4, threads,
+                                                     not args.no_cpu_baseline)
+            except Exception as e:
+                log(f"host-fed section failed: {e}")
+                raise
             try:
                 extra["c3_projection"] = c3_section(torch, ctx, 20, 3, args.cpu_seconds / 4, threads,
                                                     not args.no_cpu_baseline)

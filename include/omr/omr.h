@@ -127,6 +127,42 @@ int32_t     omr_ctx_kernel_timings(omr_ctx* ctx, float* ms_out, int32_t* kind_ou
 void*       omr_pinned_alloc(omr_ctx* ctx, size_t bytes);
 void        omr_pinned_free(omr_ctx* ctx, void* p);
 
+/* ---- pixel buffer: ROMIO repository file -> pinned staging -> HBM ---------- */
+/*
+ * Replaces pixelsService.getPixelBuffer(pixels, false) (ImageRegionRequestHandler.java:302-309)
+ * for repository-backed images (upstream ome.io.nio.RomioPixelBuffer):
+ * one file of big-endian planes in XYZCT order, plane (z, c, t) at
+ * ((t*sizeC + c)*sizeZ + z) * sizeX*sizeY*bytesPerPixel.  Read-only; safe to share between
+ * contexts and threads (pread).  open: OMR_NOT_FOUND when the file does not exist,
+ * OMR_INVALID_ARGUMENT when it is shorter than the dimensions say.
+ */
+typedef struct omr_pixel_buffer omr_pixel_buffer;
+omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_y, int32_t size_z,
+                                 int32_t size_c, int32_t size_t_, int32_t pixel_type,
+                                 omr_pixel_buffer** out);
+void       omr_pixel_buffer_close(omr_pixel_buffer* pb);
+/* RomioPixelBuffer.getPlaneOffset(z, c, t) in bytes; -1 when out of range. */
+int64_t    omr_pixel_buffer_plane_offset(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t);
+/* PixelBuffer.getTile(z, c, t, x, y, w, h): w*h pixels, rows packed, file (big-endian) byte order.
+ * OMR_INVALID_ARGUMENT outside the image (DimensionsOutOfBoundsException). */
+omr_status omr_pixel_buffer_get_tile(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t,
+                                     int32_t x, int32_t y, int32_t w, int32_t h, void* dst, size_t cap);
+typedef struct omr_tile_request { int32_t z, t, x, y; } omr_tile_request;
+/*
+ * n render_image_region tile requests (ImageRegionRequestHandler.java:430-600: getPixelBuffer ->
+ * renderAsPackedInt -> flip) of one image at one rendering setting, all width x height: reader
+ * threads pread each group of tiles straight into pinned memory while the previous group is
+ * copied to HBM (own copy stream), rendered (K1+K2) and copied back.  argb_out: n*height*width
+ * uint32 in host memory (out_on_device 0; pinned memory from omr_pinned_alloc skips a bounce
+ * copy) or in device memory (1: e.g. for omr_encode_jpeg_batch_device).  Synchronous.
+ */
+omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb,
+                                         const omr_quantum_def* qdef,
+                                         const omr_channel_binding* channels, int32_t size_c,
+                                         const omr_tile_request* reqs, int32_t n, int32_t width,
+                                         int32_t height, int32_t flip_h, int32_t flip_v,
+                                         uint32_t* argb_out, int32_t out_on_device);
+
 /* ---- render (quantize + codomain + composite + flip) ------------------ */
 /*
  * Replaces renderer.renderAsPackedInt(planeDef, null)  (ImageRegionRequestHandler.java:559)

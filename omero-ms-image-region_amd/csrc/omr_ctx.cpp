@@ -154,6 +154,7 @@ void omr_ctx_destroy(omr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->pixbuf_state && c->pixbuf_state_free) c->pixbuf_state_free(c->pixbuf_state);
     for (auto& t : c->timed) { c->event_pool.push_back(t.start); c->event_pool.push_back(t.stop); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     for (int i = 0; i < 2; ++i) {

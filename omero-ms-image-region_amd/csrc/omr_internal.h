@@ -78,6 +78,9 @@ struct Ctx {
     struct Timed { hipEvent_t start, stop; int kind; };
     std::vector<Timed> timed;
     std::vector<hipEvent_t> event_pool;
+    // pixel-buffer pipeline (omr_pixbuf.cpp): reader threads + double-buffered staging
+    void* pixbuf_state = nullptr;
+    void (*pixbuf_state_free)(void*) = nullptr;
 };
 
 // Bracket one hot-kernel launch with events when timing is enabled.

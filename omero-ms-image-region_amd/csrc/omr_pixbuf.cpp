@@ -1,0 +1,360 @@
+// omr_pixbuf.cpp — the step before the path: ROMIO pixel buffer -> pinned staging -> device.
+//
+// Replaces pixelsService.getPixelBuffer(pixels, false) (ImageRegionRequestHandler.java:302-309)
+// for repository-backed images, i.e. upstream ome.io.nio.RomioPixelBuffer: one file of
+// big-endian planes in XYZCT order, plane (z, c, t) at ((t*sizeC + c)*sizeZ + z) * planeBytes,
+// rows of sizeX pixels.  getTile(z, c, t, x, y, w, h) reads h row segments of that plane.
+//
+// omr_render_pixel_buffer_tiles is the host-fed render_image_region path for many tiles of one
+// image at one setting (a viewer panning over a pyramid level): worker threads pread each group
+// of tiles straight into a pinned slot, the slot goes to HBM on a copy stream, K1+K2 render it
+// on the context's stream and the ARGB comes back (or stays in HBM for a JPEG batch), with two
+// slots in flight so file reads, PCIe copies and kernels overlap.
+#include "omr_internal.h"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+struct omr_pixel_buffer {
+    int fd = -1;
+    int32_t sx = 0, sy = 0, sz = 0, sc = 0, st = 0, pt = 0, bpp = 0;
+    int64_t row_bytes = 0, plane_bytes = 0, total = 0;
+};
+
+namespace omr {
+
+// Fixed pool of reader threads (one per context, created on first use).
+class ReadPool {
+public:
+    explicit ReadPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~ReadPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // Runs job(i) for i in [0, n) on the pool and the calling thread; returns when all are done.
+    void run(int n, const std::function<void(int)>& job) {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            n_ = n;
+            next_.store(0);
+            done_ = 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return done_ == n_; });
+        job_ = nullptr;
+    }
+    int size() const { return (int)th_.size(); }
+
+private:
+    void work() {
+        for (;;) {
+            const int i = next_.fetch_add(1);
+            if (i >= n_) return;
+            (*job_)(i);
+            std::lock_guard<std::mutex> g(m_);
+            if (++done_ == n_) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* job_ = nullptr;
+    std::atomic<int> next_{0};
+    int n_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Double-buffered staging of one context.
+struct PixPipe {
+    ReadPool pool;
+    void* pin_in[2] = {nullptr, nullptr};
+    void* pin_out[2] = {nullptr, nullptr};
+    void* d_in[2] = {nullptr, nullptr};
+    void* d_out[2] = {nullptr, nullptr};
+    size_t in_cap = 0, out_cap = 0;
+    hipEvent_t h2d[2] = {nullptr, nullptr}, rend[2] = {nullptr, nullptr}, d2h[2] = {nullptr, nullptr};
+    hipStream_t copy = nullptr;
+    explicit PixPipe(int threads) : pool(threads) {}
+    ~PixPipe() {
+        if (copy) (void)hipStreamSynchronize(copy);
+        for (int i = 0; i < 2; ++i) {
+            if (pin_in[i]) (void)hipHostFree(pin_in[i]);
+            if (pin_out[i]) (void)hipHostFree(pin_out[i]);
+            if (d_in[i]) (void)hipFree(d_in[i]);
+            if (d_out[i]) (void)hipFree(d_out[i]);
+            for (hipEvent_t e : {h2d[i], rend[i], d2h[i]})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (copy) (void)hipStreamDestroy(copy);
+    }
+};
+
+static void free_pipe(void* p) { delete static_cast<PixPipe*>(p); }
+
+static omr_status get_pipe(Ctx* c, PixPipe*& out) {
+    if (!c->pixbuf_state) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        auto* p = new PixPipe((int)std::max(1u, std::min(hw ? hw : 4u, 16u) - 1));
+        c->pixbuf_state = p;
+        c->pixbuf_state_free = free_pipe;
+        OMR_HIP(c, hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking));
+        for (int i = 0; i < 2; ++i)
+            for (hipEvent_t* e : {&p->h2d[i], &p->rend[i], &p->d2h[i]})
+                OMR_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    out = static_cast<PixPipe*>(c->pixbuf_state);
+    return OMR_OK;
+}
+
+static omr_status grow(Ctx* c, PixPipe* p, size_t in_bytes, size_t out_bytes, bool host_out) {
+    if (in_bytes > p->in_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (p->pin_in[i]) OMR_HIP(c, hipHostFree(p->pin_in[i]));
+            if (p->d_in[i]) OMR_HIP(c, hipFree(p->d_in[i]));
+            p->pin_in[i] = p->d_in[i] = nullptr;
+        }
+        for (int i = 0; i < 2; ++i) {
+            OMR_HIP(c, hipHostMalloc(&p->pin_in[i], in_bytes, hipHostMallocDefault));
+            OMR_HIP(c, hipMalloc(&p->d_in[i], in_bytes));
+        }
+        p->in_cap = in_bytes;
+    }
+    if (out_bytes > p->out_cap) {
+        for (int i = 0; i < 2; ++i) {
+            if (p->pin_out[i]) OMR_HIP(c, hipHostFree(p->pin_out[i]));
+            if (p->d_out[i]) OMR_HIP(c, hipFree(p->d_out[i]));
+            p->pin_out[i] = p->d_out[i] = nullptr;
+        }
+        for (int i = 0; i < 2; ++i) {
+            OMR_HIP(c, hipMalloc(&p->d_out[i], out_bytes));
+            if (host_out) OMR_HIP(c, hipHostMalloc(&p->pin_out[i], out_bytes, hipHostMallocDefault));
+        }
+        p->out_cap = out_bytes;
+    }
+    if (host_out && !p->pin_out[0]) {
+        for (int i = 0; i < 2; ++i) OMR_HIP(c, hipHostMalloc(&p->pin_out[i], p->out_cap, hipHostMallocDefault));
+    }
+    return OMR_OK;
+}
+
+// pread until done (short reads, EINTR).
+static bool read_full(int fd, void* dst, size_t n, int64_t off) {
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    while (n) {
+        const ssize_t r = ::pread(fd, d, n, (off_t)off);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            return false;
+        }
+        if (r == 0) return false;
+        d += r;
+        n -= (size_t)r;
+        off += r;
+    }
+    return true;
+}
+
+static bool tile_in_bounds(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t, int32_t x, int32_t y,
+                           int32_t w, int32_t h) {
+    return z >= 0 && z < pb->sz && c >= 0 && c < pb->sc && t >= 0 && t < pb->st && x >= 0 && y >= 0 && w >= 0 &&
+           h >= 0 && (int64_t)x + w <= pb->sx && (int64_t)y + h <= pb->sy;
+}
+
+static int64_t plane_offset(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t) {
+    return (((int64_t)t * pb->sc + c) * pb->sz + z) * pb->plane_bytes;
+}
+
+// Rows y..y+h of the plane, columns x..x+w, packed into dst.
+static bool read_tile(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t, int32_t x, int32_t y, int32_t w,
+                      int32_t h, uint8_t* dst) {
+    const int64_t base = plane_offset(pb, z, c, t) + (int64_t)y * pb->row_bytes + (int64_t)x * pb->bpp;
+    const size_t seg = (size_t)w * pb->bpp;
+    if (w == pb->sx) return read_full(pb->fd, dst, seg * (size_t)h, base);   // one contiguous band
+    for (int32_t r = 0; r < h; ++r)
+        if (!read_full(pb->fd, dst + seg * r, seg, base + (int64_t)r * pb->row_bytes)) return false;
+    return true;
+}
+
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_y, int32_t size_z, int32_t size_c,
+                                 int32_t size_t_, int32_t pixel_type, omr_pixel_buffer** out) {
+    if (!out) return OMR_INVALID_ARGUMENT;
+    *out = nullptr;
+    const int bpp = bytes_per_pixel(pixel_type);
+    if (!path || !bpp || size_x <= 0 || size_y <= 0 || size_z <= 0 || size_c <= 0 || size_t_ <= 0)
+        return OMR_INVALID_ARGUMENT;
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return OMR_NOT_FOUND;
+    auto* pb = new omr_pixel_buffer;
+    pb->fd = fd;
+    pb->sx = size_x; pb->sy = size_y; pb->sz = size_z; pb->sc = size_c; pb->st = size_t_;
+    pb->pt = pixel_type;
+    pb->bpp = bpp;
+    pb->row_bytes = (int64_t)size_x * bpp;
+    pb->plane_bytes = pb->row_bytes * size_y;
+    pb->total = pb->plane_bytes * size_z * size_c * size_t_;
+    struct stat sb;
+    if (::fstat(fd, &sb) != 0 || (int64_t)sb.st_size < pb->total) {   // RomioPixelBuffer size check
+        ::close(fd);
+        delete pb;
+        return OMR_INVALID_ARGUMENT;
+    }
+    *out = pb;
+    return OMR_OK;
+}
+
+void omr_pixel_buffer_close(omr_pixel_buffer* pb) {
+    if (!pb) return;
+    if (pb->fd >= 0) ::close(pb->fd);
+    delete pb;
+}
+
+int64_t omr_pixel_buffer_plane_offset(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t) {
+    if (!pb || !tile_in_bounds(pb, z, c, t, 0, 0, 0, 0)) return -1;
+    return plane_offset(pb, z, c, t);
+}
+
+omr_status omr_pixel_buffer_get_tile(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t, int32_t x,
+                                     int32_t y, int32_t w, int32_t h, void* dst, size_t cap) {
+    if (!pb || !dst) return OMR_INVALID_ARGUMENT;
+    if (!tile_in_bounds(pb, z, c, t, x, y, w, h)) return OMR_INVALID_ARGUMENT;   // DimensionsOutOfBounds
+    if (cap < (size_t)w * h * pb->bpp) return OMR_BUFFER_TOO_SMALL;
+    return read_tile(pb, z, c, t, x, y, w, h, static_cast<uint8_t*>(dst)) ? OMR_OK : OMR_INTERNAL;
+}
+
+omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, const omr_quantum_def* qdef,
+                                         const omr_channel_binding* channels, int32_t size_c,
+                                         const omr_tile_request* reqs, int32_t n, int32_t width, int32_t height,
+                                         int32_t flip_h, int32_t flip_v, uint32_t* argb_out, int32_t out_on_device) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (!pb || !qdef || !channels || !reqs || !argb_out || n < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "null argument");
+    if (size_c != pb->sc) return fail(ctx, OMR_INVALID_ARGUMENT, "channel bindings do not match the pixel buffer's sizeC");
+    if (width <= 0 || height <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "bad tile size");
+    if (n == 0) return OMR_OK;
+    std::vector<int32_t> act;
+    for (int c = 0; c < size_c; ++c)
+        if (channels[c].active) {
+            if (qdef->model == OMR_MODEL_GREYSCALE && !act.empty()) break;   // first active only
+            act.push_back(c);
+        }
+    for (int i = 0; i < n; ++i)
+        for (int32_t c : act)
+            if (!tile_in_bounds(pb, reqs[i].z, c, reqs[i].t, reqs[i].x, reqs[i].y, width, height))
+                return fail(ctx, OMR_INVALID_ARGUMENT, "tile request " + std::to_string(i) + " outside the image");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    PixPipe* P = nullptr;
+    omr_status st = get_pipe(ctx, P);
+    if (st) return st;
+    const size_t plane = (size_t)width * height * pb->bpp;
+    const size_t plane_al = align_up(plane, 256);
+    const size_t tile_out = (size_t)width * height * 4;
+    // group: ~64 MiB of planes per slot
+    const int na = std::max<int>(1, (int)act.size());
+    const int G = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, ((size_t)64 << 20) / (plane_al * na)));
+    const size_t tab_bytes = align_up(sizeof(void*) * (size_t)G * size_c, 256);
+    bool host_out = !out_on_device;
+    bool out_pinned = false;
+    if (host_out) {
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, argb_out) == hipSuccess && attr.type == hipMemoryTypeHost) out_pinned = true;
+        (void)hipGetLastError();
+    }
+    st = grow(ctx, P, tab_bytes + plane_al * (size_t)G * na, tile_out * G, host_out && !out_pinned);
+    if (st) return st;
+    const int ngroups = (n + G - 1) / G;
+    std::atomic<bool> io_error{false};
+    auto finish_host = [&](int g) -> omr_status {   // bounce slot -> caller (pageable output)
+        const int s = g & 1, t0 = g * G, cnt = std::min(G, n - t0);
+        OMR_HIP(ctx, hipEventSynchronize(P->d2h[s]));
+        const uint8_t* src = static_cast<const uint8_t*>(P->pin_out[s]);
+        uint8_t* dst = reinterpret_cast<uint8_t*>(argb_out) + (size_t)t0 * tile_out;
+        const size_t total = tile_out * (size_t)cnt, piece = 1 << 20;
+        const int pieces = (int)((total + piece - 1) / piece);
+        P->pool.run(pieces, [&](int i) {
+            const size_t o = (size_t)i * piece;
+            std::memcpy(dst + o, src + o, std::min(piece, total - o));
+        });
+        return OMR_OK;
+    };
+    for (int g = 0; g < ngroups; ++g) {
+        const int s = g & 1, t0 = g * G, cnt = std::min(G, n - t0);
+        if (g >= 2) OMR_HIP(ctx, hipEventSynchronize(P->h2d[s]));   // pinned slot s is free again
+        uint8_t* hin = static_cast<uint8_t*>(P->pin_in[s]);
+        uint8_t* din = static_cast<uint8_t*>(P->d_in[s]);
+        const void** tab = reinterpret_cast<const void**>(hin);
+        for (int i = 0; i < cnt; ++i)
+            for (int c = 0; c < size_c; ++c) tab[(size_t)i * size_c + c] = nullptr;
+        for (int i = 0; i < cnt; ++i)
+            for (int a = 0; a < (int)act.size(); ++a)
+                tab[(size_t)i * size_c + act[a]] = din + tab_bytes + plane_al * ((size_t)i * na + a);
+        P->pool.run(cnt * (int)act.size(), [&](int j) {   // file -> pinned, one tile-channel plane per job
+            const int i = j / (int)act.size(), a = j % (int)act.size();
+            const omr_tile_request& r = reqs[t0 + i];
+            uint8_t* dst = hin + tab_bytes + plane_al * ((size_t)i * na + a);
+            if (!read_tile(pb, r.z, act[a], r.t, r.x, r.y, width, height, dst)) io_error = true;
+        });
+        if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
+        if (g >= 2) OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free
+        OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes + plane_al * (size_t)cnt * na, hipMemcpyHostToDevice, P->copy));
+        OMR_HIP(ctx, hipEventRecord(P->h2d[s], P->copy));
+        OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d[s], 0));
+        uint32_t* dout = out_on_device ? argb_out + (size_t)t0 * width * height : static_cast<uint32_t*>(P->d_out[s]);
+        st = omr_render_batch_device(ctx, qdef, channels, size_c, reinterpret_cast<const void* const*>(din), cnt, 0,
+                                     pb->pt, 1, width, height, flip_h, flip_v, dout, nullptr);
+        if (st) return st;
+        OMR_HIP(ctx, hipEventRecord(P->rend[s], ctx->stream));
+        if (host_out) {
+            void* dst = out_pinned ? static_cast<void*>(reinterpret_cast<uint8_t*>(argb_out) + (size_t)t0 * tile_out)
+                                   : P->pin_out[s];
+            OMR_HIP(ctx, hipMemcpyAsync(dst, dout, tile_out * (size_t)cnt, hipMemcpyDeviceToHost, ctx->stream));
+            OMR_HIP(ctx, hipEventRecord(P->d2h[s], ctx->stream));
+            if (!out_pinned && g >= 1) {
+                st = finish_host(g - 1);
+                if (st) return st;
+            }
+        }
+    }
+    if (host_out && !out_pinned) {
+        st = finish_host(ngroups - 1);
+        if (st) return st;
+    }
+    return omr_ctx_synchronize(ctx);
+}
+
+}  // extern "C"

@@ -5,12 +5,14 @@ Layers:
   context   Context: one per worker thread / GPU (device, stream, workspace)
   renderer  Renderer facade mirroring the omeis Renderer calls the reference makes
             (ImageRegionRequestHandler.java:436-440, :689-741, :559)
+  pixbuf    PixelBuffer: ROMIO repository pixel files (getPixelBuffer, :302-309)
   request   ImageRegionCtx / ShapeMaskCtx parsing and the handler glue
             (ImageRegionCtx.java, ImageRegionRequestHandler.java, ShapeMaskRequestHandler.java)
 """
 from . import _lib
 from ._lib import OmrError
 from .context import Context
+from .pixbuf import PixelBuffer, write_romio
 from .renderer import (ChannelSettings, Renderer, ReverseIntensityContext, create_rendering_def,
                        flip, split_html_color)
 from .request import (ImageRegionCtx, ImageRegionRequestHandler, InMemoryPixelBuffer, LutProvider,
@@ -19,4 +21,4 @@ from .request import (ImageRegionCtx, ImageRegionRequestHandler, InMemoryPixelBu
 __all__ = ["_lib", "OmrError", "Context", "Renderer", "ChannelSettings", "ReverseIntensityContext",
            "create_rendering_def", "flip", "split_html_color", "ImageRegionCtx",
            "ImageRegionRequestHandler", "InMemoryPixelBuffer", "LutProvider", "RequestError",
-           "ShapeMaskCtx", "ShapeMaskRequestHandler"]
+           "ShapeMaskCtx", "ShapeMaskRequestHandler", "PixelBuffer", "write_romio"]

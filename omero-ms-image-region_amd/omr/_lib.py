@@ -60,6 +60,10 @@ class ChannelBinding(ctypes.Structure):
                 ("lut", ctypes.POINTER(ctypes.c_uint8))]
 
 
+class TileRequest(ctypes.Structure):
+    _fields_ = [("z", ctypes.c_int32), ("t", ctypes.c_int32), ("x", ctypes.c_int32), ("y", ctypes.c_int32)]
+
+
 class Region(ctypes.Structure):
     _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
@@ -113,6 +117,12 @@ _SIGS = {
     "omr_ctx_kernel_timings": (_i32, [_vp, _vp, _vp, _i32]),
     "omr_pinned_alloc": (_vp, [_vp, _sz]),
     "omr_pinned_free": (None, [_vp, _vp]),
+    "omr_pixel_buffer_open": (_i32, [ctypes.c_char_p, _i32, _i32, _i32, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
+    "omr_pixel_buffer_close": (None, [_vp]),
+    "omr_pixel_buffer_plane_offset": (_i64, [_vp, _i32, _i32, _i32]),
+    "omr_pixel_buffer_get_tile": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _sz]),
+    "omr_render_pixel_buffer_tiles": (_i32, [_vp, _vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
+                                             _i32]),
     "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
                                      _i32, _vp]),
     "omr_render_packed_int_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32,

@@ -161,6 +161,23 @@ class Context:
                                                   _ptr(status)), self.h)
         return out
 
+    def render_pixel_buffer_tiles(self, qdef, channels, pixbuf, requests, width, height, out=None,
+                                  flip_h=False, flip_v=False, bindings=None):
+        """Pipelined host-fed tiles: requests = [(z, t, x, y)]; out: host numpy [n][h][w] uint32
+        (allocated when None) or a device tensor (rendered in place)."""
+        if bindings is None:
+            bindings = make_bindings(channels)
+        arr, keep = bindings
+        n = len(requests)
+        reqs = (_lib.TileRequest * max(n, 1))(*[_lib.TileRequest(*r) for r in requests])
+        on_device = out is not None and hasattr(out, "data_ptr")
+        if out is None:
+            out = np.empty((n, height, width), dtype=np.uint32)
+        check(lib.omr_render_pixel_buffer_tiles(self.h, pixbuf.h, ctypes.byref(qdef), arr, len(channels), reqs, n,
+                                                width, height, int(flip_h), int(flip_v), _ptr(out),
+                                                int(on_device)), self.h)
+        return out
+
     def flip_argb_device(self, src, dst, width, height, flip_h, flip_v):
         check(lib.omr_flip_argb_device(self.h, _ptr(src), _ptr(dst), width, height, int(flip_h),
                                        int(flip_v)), self.h)

@@ -288,13 +288,28 @@ class ImageRegionRequestHandler:
             start = irc.projectionStart if irc.projectionStart is not None else 0
             end = irc.projectionEnd if irc.projectionEnd is not None else pb.size_z - 1
             w, h = pb.size_x, pb.size_y
-            stacks = [pb.stack_ptr(c, irc.t) if bindings[c].active else None for c in range(pb.size_c)]
+            keep = []
+            if hasattr(pb, "stack_to_device"):            # ROMIO file: stage the stacks in HBM
+                keep = [pb.stack_to_device(c, irc.t, dev) if bindings[c].active else None
+                        for c in range(pb.size_c)]
+                stacks = [k.data_ptr() if k is not None else None for k in keep]
+            else:
+                stacks = [pb.stack_ptr(c, irc.t) if bindings[c].active else None for c in range(pb.size_c)]
             out = out_argb if out_argb is not None else torch.empty((h, w), dtype=torch.int32, device=dev)
             _lib.check(lib.omr_render_projected_device(
                 self.ctx.h, ctypes.byref(qdef), bindings, pb.size_c,
                 (ctypes.c_void_p * pb.size_c)(*stacks), pb.pixel_type, int(pb.big_endian), w, h,
                 pb.size_z, irc.projection, start, end, 1, int(irc.flipHorizontal),
                 int(irc.flipVertical), out.data_ptr()), self.ctx.h)
+            pb.close()
+        elif hasattr(pb, "stack_to_device"):
+            # ROMIO file: getTile reads straight into pinned staging, then K1+K2 (omr_pixbuf.cpp)
+            w, h = rd.width, rd.height
+            out = out_argb if out_argb is not None else torch.empty((h, w), dtype=torch.int32, device=dev)
+            req = _lib.TileRequest(irc.z, irc.t, rd.x, rd.y)
+            _lib.check(lib.omr_render_pixel_buffer_tiles(
+                self.ctx.h, pb.h, ctypes.byref(qdef), bindings, pb.size_c, ctypes.byref(req), 1, w, h,
+                int(irc.flipHorizontal), int(irc.flipVertical), out.data_ptr(), 1), self.ctx.h)
             pb.close()
         else:
             w, h = rd.width, rd.height

@@ -161,3 +161,63 @@ def test_shape_mask_handler(ctx):
     with pytest.raises(RequestError) as e:
         ShapeMaskRequestHandler(ctx, smc).render_shape_mask(None, w, h)
     assert e.value.http_status == 404
+
+
+@pytest.mark.parametrize("kw", [
+    dict(tile="0,1,0", format="png", flip="hv"),
+    dict(region="100,50,333,77", format="png", m="g"),
+    dict(p="intmax", format="png"),
+    dict(tile="0,0,1", q="0.9"),                                     # default format: jpeg
+])
+def test_romio_pixel_buffer_matches_resident(ctx, image, tmp_path, kw):
+    """The same request through a ROMIO repository file (getPixelBuffer, :302-309: pread into
+    pinned staging) and through the HBM-resident buffer: identical encoded bytes."""
+    from omr import PixelBuffer, write_romio
+    levels_np, _ = image
+    path = tmp_path / "pixels"
+    write_romio(path, levels_np[0], _lib.PIXELS_UINT16)
+    irc = ImageRegionCtx(params(**kw))
+    resident = ImageRegionRequestHandler(ctx, irc).render_image_region(buffer(image))
+    pb = PixelBuffer(path, SIZE, SIZE, Z, C, 1, _lib.PIXELS_UINT16)
+    pb.getTileSize = lambda: (TILE, TILE)                            # the resident buffer's tiling
+    from_file = ImageRegionRequestHandler(ctx, ImageRegionCtx(params(**kw))).render_image_region(pb)
+    assert from_file == resident
+
+
+def test_pipelined_pixel_buffer_tiles(ctx, tmp_path):
+    """omr_render_pixel_buffer_tiles over more tiles than one staging group (3 groups of <= 8
+    1024^2 4-channel tiles), host pageable / host pinned / device outputs, vs the CPU restatement."""
+    import torch
+    from omr import PixelBuffer, write_romio
+    from omr.synthetic import c2_channels
+    X, Y, Zf, Cf, T = 2048, 1024, 2, 4, 2
+    rng = np.random.default_rng(5)
+    px = rng.integers(0, 65536, (T, Cf, Zf, Y, X), dtype=np.uint16)
+    path = tmp_path / "big"
+    write_romio(path, px, _lib.PIXELS_UINT16)
+    chans = c2_channels(4)
+    chans[2]["active"] = False
+    q = O.make_qdef("rgb")
+    reqs = [(i % Zf, (i // 2) % T, (i % 2) * 1024, 0) for i in range(19)]
+    W = H = 1024
+    with PixelBuffer(path, X, Y, Zf, Cf, T, _lib.PIXELS_UINT16) as pb:
+        host = ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, flip_h=True)
+        dev = torch.empty((len(reqs), H, W), dtype=torch.int32, device="cuda")
+        ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, out=dev, flip_h=True)
+        nbytes = len(reqs) * H * W * 4
+        p = _lib.lib.omr_pinned_alloc(ctx.h, nbytes)
+        assert p
+        try:
+            pinned = np.ctypeslib.as_array((ctypes.c_uint32 * (len(reqs) * H * W)).from_address(p)).reshape(-1, H, W)
+            ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, out=pinned, flip_h=True)
+            pinned_copy = pinned.copy()
+        finally:
+            _lib.lib.omr_pinned_free(ctx.h, p)
+    dev_np = dev.cpu().numpy().view(np.uint32)
+    for i, (z, t, x, y) in enumerate(reqs):
+        planes = [np.ascontiguousarray(px[t, c, z, y:y + H, x:x + W]).astype(">u2") for c in range(Cf)]
+        st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, W, H, big_endian=True, flip_h=True)
+        assert st == 0
+        np.testing.assert_array_equal(host[i], exp, err_msg=f"host tile {i}")
+        np.testing.assert_array_equal(dev_np[i], exp, err_msg=f"device tile {i}")
+        np.testing.assert_array_equal(pinned_copy[i], exp, err_msg=f"pinned tile {i}")
