@@ -444,8 +444,12 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
             "host_pageable_out": lambda: ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
                                                                        out=pageable, bindings=binds),
             "to_jpeg_host": to_jpeg,
+            "device_out_staged": None,
         }
         for name, fn in modes.items():
+            if fn is None:          # reader threads -> pinned staging instead of DMA from the mapping
+                _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 0)
+                fn = modes["device_out"]
             fn()
             ctx.synchronize()
             reps = 3
@@ -455,6 +459,7 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
             ctx.synchronize()
             el = time.perf_counter() - t0
             res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
+        _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
         _lib.lib.omr_pinned_free(ctx.h, pin)
         pb.close()
     finally:

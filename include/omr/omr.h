@@ -156,6 +156,10 @@ typedef struct omr_tile_request { int32_t z, t, x, y; } omr_tile_request;
  * uint32 in host memory (out_on_device 0; pinned memory from omr_pinned_alloc skips a bounce
  * copy) or in device memory (1: e.g. for omr_encode_jpeg_batch_device).  Synchronous.
  */
+/* Tile rows DMA'd straight from the registered file mapping (1, default) or copied by reader
+ * threads into pinned staging first (0).  The DMA path falls back to staging on its own when the
+ * driver refuses to register the mapping. */
+omr_status omr_ctx_set_pixel_buffer_dma(omr_ctx* ctx, int32_t enable);
 omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb,
                                          const omr_quantum_def* qdef,
                                          const omr_channel_binding* channels, int32_t size_c,

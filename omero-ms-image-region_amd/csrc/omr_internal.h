@@ -80,6 +80,7 @@ struct Ctx {
     std::vector<hipEvent_t> event_pool;
     // pixel-buffer pipeline (omr_pixbuf.cpp): reader threads + double-buffered staging
     void* pixbuf_state = nullptr;
+    bool pixbuf_direct = true;   // DMA tile rows from a registered file mapping when possible
     void (*pixbuf_state_free)(void*) = nullptr;
 };
 

@@ -6,13 +6,16 @@
 // rows of sizeX pixels.  getTile(z, c, t, x, y, w, h) reads h row segments of that plane.
 //
 // omr_render_pixel_buffer_tiles is the host-fed render_image_region path for many tiles of one
-// image at one setting (a viewer panning over a pyramid level): worker threads pread each group
-// of tiles straight into a pinned slot, the slot goes to HBM on a copy stream, K1+K2 render it
-// on the context's stream and the ARGB comes back (or stays in HBM for a JPEG batch), with two
-// slots in flight so file reads, PCIe copies and kernels overlap.
+// image at one setting (a viewer panning over a pyramid level).  The file is mapped read-only;
+// when HIP accepts the mapping (hipHostRegister), the copy engine reads every tile's rows from
+// the page cache into HBM with 2-D copies on a copy stream — no CPU byte copy.  Otherwise worker
+// threads copy each group of tiles into a pinned slot that is then sent in one copy.  K1+K2
+// render on the context's stream and the ARGB comes back (or stays in HBM for a JPEG batch);
+// two slots are in flight so reads, PCIe copies and kernels overlap.
 #include "omr_internal.h"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -27,6 +30,12 @@ struct omr_pixel_buffer {
     int fd = -1;
     int32_t sx = 0, sy = 0, sz = 0, sc = 0, st = 0, pt = 0, bpp = 0;
     int64_t row_bytes = 0, plane_bytes = 0, total = 0;
+    // Read-only shared mapping of the file: getTile copies rows out of the page cache, and once
+    // registered with HIP (hipHostRegister, first pipelined render) the copy engines read tile
+    // rows straight from it — no CPU copy at all.
+    const uint8_t* map = nullptr;
+    std::mutex reg_m;
+    int reg_state = 0;   // 0 untried, 1 registered, -1 not registrable (pread/memcpy path)
 };
 
 namespace omr {
@@ -200,10 +209,28 @@ static bool read_tile(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t 
                       int32_t h, uint8_t* dst) {
     const int64_t base = plane_offset(pb, z, c, t) + (int64_t)y * pb->row_bytes + (int64_t)x * pb->bpp;
     const size_t seg = (size_t)w * pb->bpp;
+    if (pb->map) {
+        for (int32_t r = 0; r < h; ++r) std::memcpy(dst + seg * r, pb->map + base + (int64_t)r * pb->row_bytes, seg);
+        return true;
+    }
     if (w == pb->sx) return read_full(pb->fd, dst, seg * (size_t)h, base);   // one contiguous band
     for (int32_t r = 0; r < h; ++r)
         if (!read_full(pb->fd, dst + seg * r, seg, base + (int64_t)r * pb->row_bytes)) return false;
     return true;
+}
+
+// Register the file mapping with HIP once (portable, read-only): from then on tile rows are
+// DMA'd from the page cache.  Returns false when the driver refuses (the pread path stays).
+static bool ensure_registered(omr_pixel_buffer* pb) {
+    if (!pb->map) return false;
+    std::lock_guard<std::mutex> g(pb->reg_m);
+    if (pb->reg_state == 0) {
+        const hipError_t e = hipHostRegister(const_cast<uint8_t*>(pb->map), (size_t)pb->total,
+                                             hipHostRegisterPortable | hipHostRegisterReadOnly);
+        pb->reg_state = e == hipSuccess ? 1 : -1;
+        if (e != hipSuccess) (void)hipGetLastError();
+    }
+    return pb->reg_state == 1;
 }
 
 }  // namespace omr
@@ -235,12 +262,18 @@ omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_
         delete pb;
         return OMR_INVALID_ARGUMENT;
     }
+    void* m = ::mmap(nullptr, (size_t)pb->total, PROT_READ, MAP_SHARED, fd, 0);
+    if (m != MAP_FAILED) pb->map = static_cast<const uint8_t*>(m);
     *out = pb;
     return OMR_OK;
 }
 
 void omr_pixel_buffer_close(omr_pixel_buffer* pb) {
     if (!pb) return;
+    if (pb->map) {
+        if (pb->reg_state == 1) (void)hipHostUnregister(const_cast<uint8_t*>(pb->map));
+        ::munmap(const_cast<uint8_t*>(pb->map), (size_t)pb->total);
+    }
     if (pb->fd >= 0) ::close(pb->fd);
     delete pb;
 }
@@ -256,6 +289,12 @@ omr_status omr_pixel_buffer_get_tile(const omr_pixel_buffer* pb, int32_t z, int3
     if (!tile_in_bounds(pb, z, c, t, x, y, w, h)) return OMR_INVALID_ARGUMENT;   // DimensionsOutOfBounds
     if (cap < (size_t)w * h * pb->bpp) return OMR_BUFFER_TOO_SMALL;
     return read_tile(pb, z, c, t, x, y, w, h, static_cast<uint8_t*>(dst)) ? OMR_OK : OMR_INTERNAL;
+}
+
+omr_status omr_ctx_set_pixel_buffer_dma(omr_ctx* ctx, int32_t enable) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    ctx->pixbuf_direct = enable != 0;
+    return OMR_OK;
 }
 
 omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, const omr_quantum_def* qdef,
@@ -298,6 +337,7 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
     st = grow(ctx, P, tab_bytes + plane_al * (size_t)G * na, tile_out * G, host_out && !out_pinned);
     if (st) return st;
     const int ngroups = (n + G - 1) / G;
+    const bool direct = ctx->pixbuf_direct && ensure_registered(const_cast<omr_pixel_buffer*>(pb));
     std::atomic<bool> io_error{false};
     auto finish_host = [&](int g) -> omr_status {   // bounce slot -> caller (pageable output)
         const int s = g & 1, t0 = g * G, cnt = std::min(G, n - t0);
@@ -323,15 +363,34 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
         for (int i = 0; i < cnt; ++i)
             for (int a = 0; a < (int)act.size(); ++a)
                 tab[(size_t)i * size_c + act[a]] = din + tab_bytes + plane_al * ((size_t)i * na + a);
-        P->pool.run(cnt * (int)act.size(), [&](int j) {   // file -> pinned, one tile-channel plane per job
-            const int i = j / (int)act.size(), a = j % (int)act.size();
-            const omr_tile_request& r = reqs[t0 + i];
-            uint8_t* dst = hin + tab_bytes + plane_al * ((size_t)i * na + a);
-            if (!read_tile(pb, r.z, act[a], r.t, r.x, r.y, width, height, dst)) io_error = true;
-        });
-        if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
+        if (!direct) {
+            P->pool.run(cnt * (int)act.size(), [&](int j) {   // file -> pinned, one tile-channel plane per job
+                const int i = j / (int)act.size(), a = j % (int)act.size();
+                const omr_tile_request& r = reqs[t0 + i];
+                uint8_t* dst = hin + tab_bytes + plane_al * ((size_t)i * na + a);
+                if (!read_tile(pb, r.z, act[a], r.t, r.x, r.y, width, height, dst)) io_error = true;
+            });
+            if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
+        }
         if (g >= 2) OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free
-        OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes + plane_al * (size_t)cnt * na, hipMemcpyHostToDevice, P->copy));
+        if (direct) {
+            // registered mapping: the copy engine reads each tile's rows from the page cache
+            OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes, hipMemcpyHostToDevice, P->copy));
+            for (int i = 0; i < cnt; ++i) {
+                const omr_tile_request& r = reqs[t0 + i];
+                for (int a = 0; a < (int)act.size(); ++a) {
+                    const uint8_t* src = pb->map + plane_offset(pb, r.z, act[a], r.t) + (int64_t)r.y * pb->row_bytes +
+                                         (int64_t)r.x * pb->bpp;
+                    OMR_HIP(ctx, hipMemcpy2DAsync(din + tab_bytes + plane_al * ((size_t)i * na + a),
+                                                  (size_t)width * pb->bpp, src, (size_t)pb->row_bytes,
+                                                  (size_t)width * pb->bpp, (size_t)height, hipMemcpyHostToDevice,
+                                                  P->copy));
+                }
+            }
+        } else {
+            OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes + plane_al * (size_t)cnt * na, hipMemcpyHostToDevice,
+                                        P->copy));
+        }
         OMR_HIP(ctx, hipEventRecord(P->h2d[s], P->copy));
         OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d[s], 0));
         uint32_t* dout = out_on_device ? argb_out + (size_t)t0 * width * height : static_cast<uint32_t*>(P->d_out[s]);

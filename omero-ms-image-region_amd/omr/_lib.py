@@ -121,6 +121,7 @@ _SIGS = {
     "omr_pixel_buffer_close": (None, [_vp]),
     "omr_pixel_buffer_plane_offset": (_i64, [_vp, _i32, _i32, _i32]),
     "omr_pixel_buffer_get_tile": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _sz]),
+    "omr_ctx_set_pixel_buffer_dma": (_i32, [_vp, _i32]),
     "omr_render_pixel_buffer_tiles": (_i32, [_vp, _vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                              _i32]),
     "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,

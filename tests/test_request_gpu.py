@@ -184,7 +184,8 @@ def test_romio_pixel_buffer_matches_resident(ctx, image, tmp_path, kw):
     assert from_file == resident
 
 
-def test_pipelined_pixel_buffer_tiles(ctx, tmp_path):
+@pytest.mark.parametrize("dma", [True, False])
+def test_pipelined_pixel_buffer_tiles(ctx, tmp_path, dma):
     """omr_render_pixel_buffer_tiles over more tiles than one staging group (3 groups of <= 8
     1024^2 4-channel tiles), host pageable / host pinned / device outputs, vs the CPU restatement."""
     import torch
@@ -200,6 +201,7 @@ def test_pipelined_pixel_buffer_tiles(ctx, tmp_path):
     q = O.make_qdef("rgb")
     reqs = [(i % Zf, (i // 2) % T, (i % 2) * 1024, 0) for i in range(19)]
     W = H = 1024
+    _lib.check(_lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, int(dma)))
     with PixelBuffer(path, X, Y, Zf, Cf, T, _lib.PIXELS_UINT16) as pb:
         host = ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, flip_h=True)
         dev = torch.empty((len(reqs), H, W), dtype=torch.int32, device="cuda")
@@ -213,6 +215,7 @@ def test_pipelined_pixel_buffer_tiles(ctx, tmp_path):
             pinned_copy = pinned.copy()
         finally:
             _lib.lib.omr_pinned_free(ctx.h, p)
+    _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
     dev_np = dev.cpu().numpy().view(np.uint32)
     for i, (z, t, x, y) in enumerate(reqs):
         planes = [np.ascontiguousarray(px[t, c, z, y:y + H, x:x + W]).astype(">u2") for c in range(Cf)]
