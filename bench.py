@@ -387,6 +387,46 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
     return r
 
 
+def png_section(torch, ctx, data):
+    """format=png (ImageRegionRequestHandler.java:583-600): one rendered C2 1024^2 tile -> device
+    PNG (adaptive filters + dynamic-Huffman deflate, K5), p50 latency and size; PIL's zlib PNG
+    writer on the host is timed beside it as a CPU reference point (ImageIO's writer cannot run
+    here)."""
+    import io
+    import numpy as np
+    from omr import _lib
+    from omr.context import make_qdef
+    from omr.synthetic import c2_channels
+    out = torch.empty((TILE, TILE), dtype=torch.int32, device=data.device)
+    ctx.render_packed_int_device(make_qdef("rgb"), c2_channels(CHANNELS), [data[0, c] for c in range(CHANNELS)],
+                                 _lib.PIXELS_UINT16, TILE, TILE, out, big_endian=True)
+    ctx.synchronize()
+    lat = []
+    for i in range(13):
+        t0 = time.perf_counter()
+        png = ctx.encode_png_device(out, TILE, TILE)
+        if i >= 3:
+            lat.append(time.perf_counter() - t0)
+    res = {"p50_ms": round(1e3 * float(np.median(lat)), 4), "png_bytes": len(png),
+           "raw_bytes": (3 * TILE + 1) * TILE, "ratio": round(len(png) / ((3 * TILE + 1) * TILE), 4)}
+    try:
+        from PIL import Image
+        a = out.cpu().numpy().view(np.uint32)
+        rgb = np.stack([(a >> 16) & 0xFF, (a >> 8) & 0xFF, a & 0xFF], -1).astype(np.uint8)
+        im = Image.fromarray(rgb)
+        t = []
+        for i in range(4):
+            b = io.BytesIO()
+            t0 = time.perf_counter()
+            im.save(b, format="PNG")
+            t.append(time.perf_counter() - t0)
+        res["cpu_pil_zlib"] = {"p50_ms": round(1e3 * float(np.median(t)), 3), "png_bytes": len(b.getvalue()),
+                               "cores": 1}
+    except Exception as e:   # PIL is a reference point only
+        log(f"PIL PNG reference failed: {e}")
+    return res
+
+
 def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
     """The step before the path: C2 tiles read from a ROMIO repository
     file (big-endian XYZCT planes, as pixelsService.getPixelBuffer opens, ImageRegionRequestHandler
@@ -570,6 +610,11 @@ def main():
             extra["jpeg"] = jpeg_section(torch, ctx, data, min(args.jpeg_batch, B), args.jpeg_steps,
                                          2, args.cpu_seconds / 2, threads, not args.no_cpu_baseline)
         if not args.no_configs:
+            try:
+                extra["png"] = png_section(torch, ctx, data)
+            except Exception as e:
+                log(f"png section failed: {e}")
+                raise
             try:
                 extra["host_fed"] = host_fed_section(torch, ctx, uniq, 64, args.cpu_seconds / 4, threads,
                                                      not args.no_cpu_baseline)
