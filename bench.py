@@ -427,6 +427,56 @@ def png_section(torch, ctx, data):
     return res
 
 
+def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8):
+    """render_image_region JPEG tiles (q 0.9) served to concurrent clients from the ROMIO file:
+    one request at a time on one context (the reference's shape: a Renderer per request) vs the
+    batcher (omr_batcher_*: the dispatcher coalesces what the 8 client threads submit, 8 tiles
+    per client at a time like a viewer filling a screen, into GPU batches).  Requests walk the 16 distinct tiles, so identical tiles in flight together are
+    rendered once."""
+    import threading
+    import numpy as np
+    from omr import Batcher
+    reqs = [(0, 0, (i % grid) * TILE, ((i // grid) % grid) * TILE) for i in range(n_req)]
+    dev = torch.empty((TILE, TILE), dtype=torch.int32, device="cuda")
+    lat = []
+    t0 = time.perf_counter()
+    for r in reqs[:64]:
+        a = time.perf_counter()
+        ctx.render_pixel_buffer_tiles(qd, chans, pb, [r], TILE, TILE, out=dev, bindings=binds)
+        ctx.encode_jpeg_device(dev, TILE, TILE, 0.9)
+        lat.append(time.perf_counter() - a)
+    el = time.perf_counter() - t0
+    res = {"requests": n_req, "clients": clients,
+           "one_at_a_time": {"tiles_per_s": round(64 / el, 1), "p50_ms": round(1e3 * float(np.median(lat)), 3)}}
+    for mb, wait_us in ((64, 1000),):
+        lats = []
+        with Batcher(ctx.device, max_batch=mb, max_wait_us=wait_us) as b:
+            def client(k):          # a viewer asks for a screenful (8 tiles) at a time
+                mine = list(range(k, n_req, clients))
+                for s0 in range(0, len(mine), 8):
+                    a = time.perf_counter()
+                    ts = [b.submit(pb, qd, chans, *reqs[i], TILE, TILE, quality=0.9, bindings=binds)
+                          for i in mine[s0:s0 + 8]]
+                    for t in ts:
+                        b.wait(t)
+                        lats.append(time.perf_counter() - a)
+            for warm in (True, False):
+                lats.clear()
+                ths = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
+                t0 = time.perf_counter()
+                for t in ths:
+                    t.start()
+                for t in ths:
+                    t.join()
+                el = time.perf_counter() - t0
+            st = b.stats()
+        res[f"batcher_max{mb}_wait{wait_us}us"] = {"tiles_per_s": round(n_req / el, 1),
+                                                   "p50_ms": round(1e3 * float(np.median(lats)), 3),
+                                                   "rendered": st["rendered"], "dedup": st["dedup"],
+                                                   "rounds": st["batches"]}
+    return res
+
+
 def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
     """The step before the path: C2 tiles read from a ROMIO repository
     file (big-endian XYZCT planes, as pixelsService.getPixelBuffer opens, ImageRegionRequestHandler
@@ -501,6 +551,7 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
             res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
         _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
         _lib.lib.omr_pinned_free(ctx.h, pin)
+        res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid)
         pb.close()
     finally:
         os.unlink(path)

@@ -167,6 +167,39 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
                                          int32_t height, int32_t flip_h, int32_t flip_v,
                                          uint32_t* argb_out, int32_t out_on_device);
 
+/* ---- request batching ------------------------------ */
+/*
+ * Concurrent render_image_region requests coalesced into GPU batches.  The reference runs each
+ * request on its own worker thread (ImageRegionMicroserviceVerticle.java:149-165) with its own
+ * Renderer (ImageRegionRequestHandler.java:436-440) and caches finished regions in Redis under
+ * ImageRegionCtx.cacheKey (ImageRegionCtx.java:165-177).  A batcher owns one GPU context and a
+ * dispatcher thread: submitted jobs are grouped by image + rendering settings + tile size + flip +
+ * format, each group is rendered by one omr_render_pixel_buffer_tiles call and encoded by one
+ * batched JPEG launch, and identical tiles in flight together are rendered once.
+ * submit/wait are thread-safe; the pixel buffer must outlive its jobs.
+ */
+enum { OMR_FORMAT_JPEG = 0, OMR_FORMAT_PNG = 1, OMR_FORMAT_ARGB = 2 /* packed int[] */ };
+typedef struct omr_tile_job {
+    const omr_pixel_buffer* pb;
+    const struct omr_quantum_def* qdef;            /* copied at submit */
+    const struct omr_channel_binding* channels;    /* size_c entries, copied (LUTs too) */
+    int32_t size_c;
+    int32_t z, t, x, y, width, height;
+    int32_t flip_h, flip_v;
+    int32_t format;                                /* OMR_FORMAT_*; others -> OMR_NOT_FOUND (404) */
+    float quality;                                 /* JPEG */
+} omr_tile_job;
+typedef struct omr_batcher omr_batcher;
+omr_status omr_batcher_create(int32_t device_ordinal, int32_t max_batch, int32_t max_wait_us,
+                              omr_batcher** out);
+void       omr_batcher_destroy(omr_batcher* b);
+omr_status omr_batcher_submit(omr_batcher* b, const omr_tile_job* job, uint64_t* ticket);
+/* Blocks until the job is done; copies its encoded bytes.  OMR_BUFFER_TOO_SMALL sets *len and
+ * keeps the result for a retry with a larger buffer. */
+omr_status omr_batcher_wait(omr_batcher* b, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
+/* jobs submitted, dispatch rounds, tiles rendered, duplicate tiles served from a sibling job */
+omr_status omr_batcher_stats(omr_batcher* b, uint64_t stats_out[4]);
+
 /* ---- render (quantize + codomain + composite + flip) ------------------ */
 /*
  * Replaces renderer.renderAsPackedInt(planeDef, null)  (ImageRegionRequestHandler.java:559)

@@ -1,0 +1,334 @@
+// omr_batcher.cpp — coalescing concurrent tile requests into GPU batches.
+//
+// The reference serves every render_image_region request on its own Vert.x worker thread
+// (ImageRegionMicroserviceVerticle.java:149-165 deploys the worker verticles; each request
+// builds its own Renderer, ImageRegionRequestHandler.java:436-440) and caches finished regions
+// in Redis under ImageRegionCtx.cacheKey (ImageRegionCtx.java:165-177).  Here worker threads
+// submit tile jobs to a batcher that owns one GPU context: a dispatcher thread takes whatever is
+// pending (up to max_batch jobs, or whatever arrived within max_wait_us of the oldest job),
+// groups jobs with the same image and rendering settings, renders each group with one pipelined
+// pixel-buffer call (omr_render_pixel_buffer_tiles, device output) and one batched JPEG encode,
+// and hands every job its own file.  Identical requests in flight together (the same cache key)
+// are rendered once.
+#include "omr_internal.h"
+
+#include <chrono>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+
+namespace omr {
+
+struct Job {
+    uint64_t ticket = 0;
+    const omr_pixel_buffer* pb = nullptr;
+    omr_quantum_def qdef{};
+    std::vector<omr_channel_binding> ch;
+    std::vector<std::vector<uint8_t>> luts;     // owned copies of the .lut tables
+    omr_tile_job spec{};
+    std::string group_key;                       // image + settings + size + flip + format
+    std::chrono::steady_clock::time_point t_submit;
+};
+
+struct Result {
+    omr_status st = OMR_OK;
+    std::string err;
+    std::vector<uint8_t> bytes;
+};
+
+}  // namespace omr
+
+struct omr_batcher {
+    int device = 0;
+    int max_batch = 64;
+    int max_wait_us = 500;
+    omr_ctx* ctx = nullptr;
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv_in, cv_out;
+    std::vector<std::unique_ptr<omr::Job>> pending;
+    std::unordered_map<uint64_t, omr::Result> done;
+    uint64_t next_ticket = 1;
+    bool stop = false;
+    uint64_t n_jobs = 0, n_batches = 0, n_rendered = 0, n_dedup = 0;
+    // device buffers of the dispatcher (grown on demand)
+    uint32_t* d_argb = nullptr;
+    size_t argb_cap = 0;
+    uint8_t* d_jpeg = nullptr;
+    size_t jpeg_cap = 0;
+    uint64_t* d_offs = nullptr;
+    uint32_t* d_lens = nullptr;
+    int32_t* d_stat = nullptr;
+    int meta_cap = 0;
+};
+
+namespace omr {
+
+static void append(std::string& k, const void* p, size_t n) { k.append(static_cast<const char*>(p), n); }
+
+static std::string settings_key(const Job& j) {
+    std::string k;
+    append(k, &j.pb, sizeof(j.pb));
+    append(k, &j.qdef, sizeof(j.qdef));
+    for (size_t c = 0; c < j.ch.size(); ++c) {
+        const omr_channel_binding& b = j.ch[c];
+        append(k, &b.active, sizeof(b.active));
+        append(k, &b.family, sizeof(b.family));
+        append(k, &b.coefficient, sizeof(b.coefficient));
+        append(k, &b.noise_reduction, sizeof(b.noise_reduction));
+        append(k, &b.reverse, sizeof(b.reverse));
+        append(k, &b.input_start, sizeof(b.input_start));
+        append(k, &b.input_end, sizeof(b.input_end));
+        append(k, &b.global_min, sizeof(b.global_min));
+        append(k, &b.global_max, sizeof(b.global_max));
+        append(k, b.rgba, 4);
+        const uint8_t has = b.lut ? 1 : 0;
+        append(k, &has, 1);
+        if (b.lut) append(k, b.lut, 768);
+    }
+    const omr_tile_job& s = j.spec;
+    const int32_t geo[5] = {s.width, s.height, s.flip_h, s.flip_v, s.format};
+    append(k, geo, sizeof(geo));
+    append(k, &s.quality, sizeof(s.quality));
+    return k;
+}
+
+static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
+    omr_ctx* c = B->ctx;
+    if (argb > B->argb_cap) {
+        if (B->d_argb) OMR_HIP(c, hipFree(B->d_argb));
+        B->d_argb = nullptr;
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_argb), argb));
+        B->argb_cap = argb;
+    }
+    if (jpeg > B->jpeg_cap) {
+        if (B->d_jpeg) OMR_HIP(c, hipFree(B->d_jpeg));
+        B->d_jpeg = nullptr;
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_jpeg), jpeg));
+        B->jpeg_cap = jpeg;
+    }
+    if (n > B->meta_cap) {
+        if (B->d_offs) OMR_HIP(c, hipFree(B->d_offs));
+        if (B->d_lens) OMR_HIP(c, hipFree(B->d_lens));
+        if (B->d_stat) OMR_HIP(c, hipFree(B->d_stat));
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_offs), sizeof(uint64_t) * n));
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_lens), sizeof(uint32_t) * n));
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_stat), sizeof(int32_t) * n));
+        B->meta_cap = n;
+    }
+    return OMR_OK;
+}
+
+// Render + encode one group (same image, settings, size, flip, format).  jobs[u] are the
+// distinct tiles; out[u] receives each one's bytes.
+static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
+    omr_ctx* c = B->ctx;
+    const Job& j0 = *jobs[0];
+    const int n = (int)jobs.size();
+    const int W = j0.spec.width, H = j0.spec.height;
+    const size_t px = (size_t)W * H;
+    std::vector<omr_tile_request> reqs(n);
+    for (int i = 0; i < n; ++i) reqs[i] = {jobs[i]->spec.z, jobs[i]->spec.t, jobs[i]->spec.x, jobs[i]->spec.y};
+    const size_t jcap = (size_t)n * (px * 4 + 65536);
+    omr_status st = grow_dev(B, px * 4 * n, j0.spec.format == OMR_FORMAT_JPEG ? jcap : 0, n);
+    if (st) return st;
+    st = omr_render_pixel_buffer_tiles(c, j0.pb, &j0.qdef, j0.ch.data(), (int32_t)j0.ch.size(), reqs.data(), n, W, H,
+                                       j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1);
+    if (st) return st;
+    out.assign(n, Result{});
+    if (j0.spec.format == OMR_FORMAT_JPEG) {
+        st = omr_encode_jpeg_batch_device(c, B->d_argb, 0, n, W, H, j0.spec.quality, B->d_jpeg, jcap, B->d_offs,
+                                          B->d_lens, B->d_stat);
+        if (st) return st;
+        std::vector<uint64_t> offs(n);
+        std::vector<uint32_t> lens(n);
+        OMR_HIP(c, hipMemcpyAsync(offs.data(), B->d_offs, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipMemcpyAsync(lens.data(), B->d_lens, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        uint64_t used = 0;
+        for (int i = 0; i < n; ++i) {
+            if (!lens[i]) return fail(c, OMR_INTERNAL, "JPEG batch buffer too small");
+            used = std::max<uint64_t>(used, offs[i] + lens[i]);
+        }
+        std::vector<uint8_t> all(used);
+        OMR_HIP(c, hipMemcpy(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
+    } else if (j0.spec.format == OMR_FORMAT_PNG) {
+        std::vector<uint8_t> buf(omr_png_max_bytes(W, H, 3));
+        for (int i = 0; i < n; ++i) {
+            size_t len = 0;
+            st = omr_encode_png_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
+            if (st) return st;
+            out[i].bytes.assign(buf.begin(), buf.begin() + len);
+        }
+    } else {                                               // OMR_FORMAT_ARGB: the packed int[] itself
+        std::vector<uint8_t> all(px * 4 * n);
+        OMR_HIP(c, hipMemcpy(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
+    }
+    return OMR_OK;
+}
+
+static void dispatch_loop(omr_batcher* B) {
+    (void)hipSetDevice(B->device);
+    std::unique_lock<std::mutex> lk(B->m);
+    for (;;) {
+        B->cv_in.wait(lk, [&] { return B->stop || !B->pending.empty(); });
+        if (B->pending.empty() && B->stop) return;
+        // gather: up to max_batch jobs, or what arrives within max_wait_us of the oldest one
+        const auto deadline = B->pending.front()->t_submit + std::chrono::microseconds(B->max_wait_us);
+        B->cv_in.wait_until(lk, deadline, [&] { return B->stop || (int)B->pending.size() >= B->max_batch; });
+        std::vector<std::unique_ptr<Job>> take;
+        const size_t nt = std::min(B->pending.size(), (size_t)B->max_batch);
+        for (size_t i = 0; i < nt; ++i) take.push_back(std::move(B->pending[i]));
+        B->pending.erase(B->pending.begin(), B->pending.begin() + nt);
+        lk.unlock();
+        // group by settings; dedupe identical tiles (the region cache key) inside each group
+        std::map<std::string, std::vector<Job*>> groups;
+        for (auto& j : take) groups[j->group_key].push_back(j.get());
+        std::vector<std::pair<uint64_t, Result>> results;
+        uint64_t rendered = 0, dedup = 0;
+        for (auto& g : groups) {
+            std::vector<Job*> uniq;
+            std::vector<int> slot(g.second.size());
+            std::map<std::tuple<int, int, int, int>, int> seen;
+            for (size_t i = 0; i < g.second.size(); ++i) {
+                const omr_tile_job& s = g.second[i]->spec;
+                auto key = std::make_tuple(s.z, s.t, s.x, s.y);
+                auto it = seen.find(key);
+                if (it == seen.end()) {
+                    seen[key] = (int)uniq.size();
+                    slot[i] = (int)uniq.size();
+                    uniq.push_back(g.second[i]);
+                } else {
+                    slot[i] = it->second;
+                    ++dedup;
+                }
+            }
+            std::vector<Result> out;
+            omr_status st = OMR_OK;
+            for (size_t b0 = 0; b0 < uniq.size() && st == OMR_OK; b0 += (size_t)B->max_batch) {
+                std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + std::min(uniq.size(), b0 + B->max_batch));
+                std::vector<Result> po;
+                st = run_group(B, part, po);
+                for (auto& r : po) out.push_back(std::move(r));
+            }
+            rendered += uniq.size();
+            const std::string err = st ? B->ctx->last_error : std::string();
+            for (size_t i = 0; i < g.second.size(); ++i) {
+                Result r;
+                if (st) { r.st = st; r.err = err; }
+                else r.bytes = out[slot[i]].bytes;
+                results.emplace_back(g.second[i]->ticket, std::move(r));
+            }
+        }
+        lk.lock();
+        for (auto& r : results) B->done[r.first] = std::move(r.second);
+        B->n_batches += 1;
+        B->n_rendered += rendered;
+        B->n_dedup += dedup;
+        B->cv_out.notify_all();
+    }
+}
+
+}  // namespace omr
+
+using namespace omr;
+
+extern "C" {
+
+omr_status omr_batcher_create(int32_t device, int32_t max_batch, int32_t max_wait_us, omr_batcher** out) {
+    if (!out || max_batch <= 0 || max_wait_us < 0) return OMR_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto* B = new omr_batcher;
+    B->device = device;
+    B->max_batch = max_batch;
+    B->max_wait_us = max_wait_us;
+    const omr_status st = omr_ctx_create(device, &B->ctx);
+    if (st) {
+        delete B;
+        return st;
+    }
+    B->th = std::thread(dispatch_loop, B);
+    *out = B;
+    return OMR_OK;
+}
+
+void omr_batcher_destroy(omr_batcher* B) {
+    if (!B) return;
+    {
+        std::lock_guard<std::mutex> g(B->m);
+        B->stop = true;
+    }
+    B->cv_in.notify_all();
+    if (B->th.joinable()) B->th.join();
+    (void)hipSetDevice(B->device);
+    for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat})
+        if (p) (void)hipFree(p);
+    omr_ctx_destroy(B->ctx);
+    delete B;
+}
+
+omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t* ticket) {
+    if (!B || !job || !ticket || !job->pb || !job->qdef || !job->channels || job->size_c <= 0)
+        return OMR_INVALID_ARGUMENT;
+    if (job->width <= 0 || job->height <= 0) return OMR_INVALID_ARGUMENT;
+    if (job->format != OMR_FORMAT_JPEG && job->format != OMR_FORMAT_PNG && job->format != OMR_FORMAT_ARGB)
+        return OMR_NOT_FOUND;                              // unknown format -> null -> 404 (:602-603)
+    auto j = std::make_unique<Job>();
+    j->pb = job->pb;
+    j->qdef = *job->qdef;
+    j->ch.assign(job->channels, job->channels + job->size_c);
+    j->luts.resize(job->size_c);
+    for (int c = 0; c < job->size_c; ++c)
+        if (j->ch[c].lut) {
+            j->luts[c].assign(j->ch[c].lut, j->ch[c].lut + 768);
+            j->ch[c].lut = j->luts[c].data();
+        }
+    j->spec = *job;
+    j->spec.qdef = nullptr;
+    j->spec.channels = nullptr;
+    j->group_key = settings_key(*j);
+    j->t_submit = std::chrono::steady_clock::now();
+    {
+        std::lock_guard<std::mutex> g(B->m);
+        j->ticket = B->next_ticket++;
+        *ticket = j->ticket;
+        B->pending.push_back(std::move(j));
+        B->n_jobs++;
+    }
+    B->cv_in.notify_one();
+    return OMR_OK;
+}
+
+omr_status omr_batcher_wait(omr_batcher* B, uint64_t ticket, uint8_t* out, size_t cap, size_t* len) {
+    if (!B || !len) return OMR_INVALID_ARGUMENT;
+    std::unique_lock<std::mutex> lk(B->m);
+    B->cv_out.wait(lk, [&] { return B->done.count(ticket) > 0; });
+    Result& r = B->done[ticket];
+    if (r.st) {
+        const omr_status st = r.st;
+        B->done.erase(ticket);
+        return st;
+    }
+    *len = r.bytes.size();
+    if (!out || cap < r.bytes.size()) return OMR_BUFFER_TOO_SMALL;   // result kept: retry with room
+    std::memcpy(out, r.bytes.data(), r.bytes.size());
+    B->done.erase(ticket);
+    return OMR_OK;
+}
+
+omr_status omr_batcher_stats(omr_batcher* B, uint64_t stats_out[4]) {
+    if (!B || !stats_out) return OMR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(B->m);
+    stats_out[0] = B->n_jobs;
+    stats_out[1] = B->n_batches;
+    stats_out[2] = B->n_rendered;
+    stats_out[3] = B->n_dedup;
+    return OMR_OK;
+}
+
+}  // extern "C"

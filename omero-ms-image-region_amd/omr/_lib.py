@@ -64,6 +64,17 @@ class TileRequest(ctypes.Structure):
     _fields_ = [("z", ctypes.c_int32), ("t", ctypes.c_int32), ("x", ctypes.c_int32), ("y", ctypes.c_int32)]
 
 
+class TileJob(ctypes.Structure):
+    _fields_ = [("pb", ctypes.c_void_p), ("qdef", ctypes.c_void_p), ("channels", ctypes.c_void_p),
+                ("size_c", ctypes.c_int32), ("z", ctypes.c_int32), ("t", ctypes.c_int32), ("x", ctypes.c_int32),
+                ("y", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("flip_h", ctypes.c_int32), ("flip_v", ctypes.c_int32), ("format", ctypes.c_int32),
+                ("quality", ctypes.c_float)]
+
+
+FORMAT_JPEG, FORMAT_PNG, FORMAT_ARGB = 0, 1, 2
+
+
 class Region(ctypes.Structure):
     _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
@@ -122,6 +133,11 @@ _SIGS = {
     "omr_pixel_buffer_plane_offset": (_i64, [_vp, _i32, _i32, _i32]),
     "omr_pixel_buffer_get_tile": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _sz]),
     "omr_ctx_set_pixel_buffer_dma": (_i32, [_vp, _i32]),
+    "omr_batcher_create": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_vp)]),
+    "omr_batcher_destroy": (None, [_vp]),
+    "omr_batcher_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "omr_batcher_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_batcher_stats": (_i32, [_vp, _vp]),
     "omr_render_pixel_buffer_tiles": (_i32, [_vp, _vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                              _i32]),
     "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,

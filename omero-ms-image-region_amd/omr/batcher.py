@@ -1,0 +1,64 @@
+"""Batcher: concurrent tile requests coalesced into GPU batches (omr_batcher_*, SURVEY.md 8(f)
+rank 4).  Worker threads call submit()/wait(); a dispatcher thread in libomr.so groups pending
+jobs by image + settings, renders and JPEG-encodes each group in one batch, and renders
+identical in-flight tiles once (ImageRegionCtx.cacheKey, ImageRegionCtx.java:165-177)."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import lib
+from .context import make_bindings
+
+FORMATS = {"jpeg": _lib.FORMAT_JPEG, "png": _lib.FORMAT_PNG, "argb": _lib.FORMAT_ARGB}
+
+
+class Batcher:
+    def __init__(self, device=0, max_batch=64, max_wait_us=500):
+        h = ctypes.c_void_p()
+        st = lib.omr_batcher_create(device, max_batch, max_wait_us, ctypes.byref(h))
+        if st != _lib.OK:
+            raise _lib.OmrError(st, "omr_batcher_create failed")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib.omr_batcher_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def submit(self, pixbuf, qdef, channels, z, t, x, y, width, height, flip_h=False, flip_v=False,
+               fmt="jpeg", quality=0.85, bindings=None):
+        arr, keep = bindings if bindings is not None else make_bindings(channels)
+        job = _lib.TileJob(pixbuf.h.value if hasattr(pixbuf.h, "value") else pixbuf.h,
+                           ctypes.addressof(qdef), ctypes.addressof(arr), len(channels), z, t, x, y, width, height,
+                           int(flip_h), int(flip_v), FORMATS.get(fmt, 99), float(quality))
+        ticket = ctypes.c_uint64()
+        _lib.check(lib.omr_batcher_submit(self.h, ctypes.byref(job), ctypes.byref(ticket)))
+        return ticket.value
+
+    def wait(self, ticket, cap=1 << 22):
+        n = ctypes.c_size_t(0)
+        out = np.empty(cap, dtype=np.uint8)
+        st = lib.omr_batcher_wait(self.h, ticket, out.ctypes.data, cap, ctypes.byref(n))
+        if st == _lib.BUFFER_TOO_SMALL:
+            out = np.empty(n.value, dtype=np.uint8)
+            st = lib.omr_batcher_wait(self.h, ticket, out.ctypes.data, n.value, ctypes.byref(n))
+        _lib.check(st)
+        return out[:n.value].tobytes()
+
+    def stats(self):
+        s = (ctypes.c_uint64 * 4)()
+        _lib.check(lib.omr_batcher_stats(self.h, s))
+        return {"jobs": s[0], "batches": s[1], "rendered": s[2], "dedup": s[3]}

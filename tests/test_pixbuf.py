@@ -70,3 +70,13 @@ def test_render_without_gpu_fails_loudly(tmp_path):
     assert _lib.lib.omr_ctx_create(0, ctypes.byref(h)) == _lib.DEVICE
     assert _lib.lib.omr_render_pixel_buffer_tiles(None, None, None, None, 0, None, 0, 8, 8, 0, 0, None, 0) \
         == _lib.INVALID_ARGUMENT
+
+
+def test_batcher_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import ctypes
+    h = ctypes.c_void_p()
+    assert _lib.lib.omr_batcher_create(0, 8, 100, ctypes.byref(h)) == _lib.DEVICE
+    assert _lib.lib.omr_batcher_create(0, 0, 100, ctypes.byref(h)) == _lib.INVALID_ARGUMENT
