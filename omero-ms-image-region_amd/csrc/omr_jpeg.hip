@@ -738,19 +738,24 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     const int m1 = min(m0 + kB1McuPerWave, A.n_mcu);
     // The next MCU's four pixels are loaded while this one is transformed (one pass of HBM
     // latency per wave instead of one per MCU).
-    uint32_t n00 = 0, n01 = 0, n10 = 0, n11 = 0;
+    // Even widths: two unconditional 8-byte loads per lane at clamped addresses; the edge
+    // replication select happens when the pixels are used, so nothing waits on the prefetch.
+    uint2 na = make_uint2(0, 0), nb = make_uint2(0, 0);
+    bool nclamp = false;
     auto fetch = [&](int m) {
         const int mx = m % A.mcux, my = m / A.mcux;
         const int x0 = mx * 16 + 2 * cx, y0 = my * 16 + 2 * cy;
         const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
         if (even_w) {
-            load_pair(img, W, min(x0, W - 1) & ~1, ya, n00, n01);
-            load_pair(img, W, min(x0, W - 1) & ~1, yb, n10, n11);
-            if (x0 > W - 1) { n00 = n01; n10 = n11; }           // both columns clamp to W-1
+            const int xl = min(x0, W - 2);                        // even, W >= 2
+            na = *reinterpret_cast<const uint2*>(img + (int64_t)ya * W + xl);
+            nb = *reinterpret_cast<const uint2*>(img + (int64_t)yb * W + xl);
+            nclamp = x0 > W - 1;                                   // both columns clamp to W-1
         } else {
             const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
-            n00 = img[(int64_t)ya * W + xa]; n01 = img[(int64_t)ya * W + xb];
-            n10 = img[(int64_t)yb * W + xa]; n11 = img[(int64_t)yb * W + xb];
+            na = make_uint2(img[(int64_t)ya * W + xa], img[(int64_t)ya * W + xb]);
+            nb = make_uint2(img[(int64_t)yb * W + xa], img[(int64_t)yb * W + xb]);
+            nclamp = false;
         }
     };
     if (m0 < m1) fetch(m0);
@@ -758,7 +763,7 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
         const int mx = m % A.mcux, my = m / A.mcux;
         {
             const int x0 = mx * 16 + 2 * cx;
-            uint32_t p00 = n00, p01 = n01, p10 = n10, p11 = n11;
+            uint32_t p00 = nclamp ? na.y : na.x, p01 = na.y, p10 = nclamp ? nb.y : nb.x, p11 = nb.y;
             if (m + 1 < m1) fetch(m + 1);
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
