@@ -224,11 +224,11 @@ __global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter)
     for (; i + 8 <= i1; i += 8, p += 8 * pchunks) {          // 8 independent 16-B loads in flight
         p32x4 q[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) q[u] = p[u * pchunks];
+        for (int u = 0; u < 8; ++u) q[u] = __builtin_nontemporal_load(p + u * pchunks);   // read once
 #pragma unroll
         for (int u = 0; u < 8; ++u) fold(q[u]);
     }
-    for (; i < i1; ++i, p += pchunks) fold(*p);
+    for (; i < i1; ++i, p += pchunks) fold(__builtin_nontemporal_load(p));
     if constexpr (SPLIT) {
         if (wave > 0) {
 #pragma unroll

@@ -127,11 +127,20 @@ struct Chunk {
 template <typename T> __device__ __forceinline__ const OMR_GLOBAL T* gload_ptr(const void* p) { return (const OMR_GLOBAL T*)(p); }
 template <typename T> __device__ __forceinline__ OMR_GLOBAL T* gstore_ptr(void* p) { return (OMR_GLOBAL T*)(p); }
 
+// K2 streams every pixel once and writes every output once: 16-byte loads are non-temporal,
+// and so are the ARGB stores when a pixel reads at least as many bytes as it writes
+// (tools/probe_stream3.hip: the C2 pattern at 6.07 TB/s with nt loads + stores vs 5.90 TB/s
+// plain; a write-only stream drops from 6.7 to 2.4 TB/s with nt stores, so the 1-byte
+// single-channel case keeps plain stores).
+#ifndef OMR_K2_NT
+#define OMR_K2_NT 1
+#endif
+
 template <int BPP, int VEC>
 __device__ __forceinline__ void load_chunk(Chunk<BPP, VEC>& c, const uint8_t* p) {
     constexpr int B = BPP * VEC;
     if constexpr (B == 16) {
-        const u32x4 v = *gload_ptr<u32x4>(p);
+        const u32x4 v = OMR_K2_NT ? __builtin_nontemporal_load(gload_ptr<u32x4>(p)) : *gload_ptr<u32x4>(p);
         c.dw[0] = v[0]; c.dw[1] = v[1]; c.dw[2] = v[2]; c.dw[3] = v[3];
     } else if constexpr (B == 8) {
         const u32x2 v = *gload_ptr<u32x2>(p);
@@ -516,7 +525,11 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
         if constexpr (VEC % 4 == 0) {
 #pragma unroll
             for (int j = 0; j < VEC; j += 4)
-                *(OMR_GLOBAL u32x4*)(o + j) = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
+            {
+                const u32x4 v = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
+                if (OMR_K2_NT && BPP * NL >= 4) __builtin_nontemporal_store(v, (OMR_GLOBAL u32x4*)(o + j));
+                else *(OMR_GLOBAL u32x4*)(o + j) = v;
+            }
         } else if constexpr (VEC == 2) {
             *(OMR_GLOBAL u32x2*)(o) = u32x2{px[0], px[1]};
         } else {
