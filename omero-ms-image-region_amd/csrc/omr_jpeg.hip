@@ -127,6 +127,7 @@ __device__ __forceinline__ void ycc(uint32_t p, int& y, int& cb, int& cr) {
 }
 
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
+#define M24(a, c) __mul24((a), (c))
 
 // jfdctint.c one 8-point pass on p[0], p[s], ..., p[7s] (pass 0 rows, pass 1 columns).
 template <int PASS>
@@ -146,14 +147,17 @@ __device__ __forceinline__ void fdct8(int* p, int s) {
         p[0] = (tmp10 + tmp11) * (1 << P1);
         p[4 * s] = (tmp10 - tmp11) * (1 << P1);
     }
-    int z1 = (tmp12 + tmp13) * 4433;
-    p[2 * s] = DESCALE(z1 + tmp13 * 6270, sh);
-    p[6 * s] = DESCALE(z1 + tmp12 * (-15137), sh);
+    // Every operand is below 2^17 in magnitude and every product below 2^31 (the jfdctint.c
+    // INT32 range for 8-bit samples), so v_mul_i32_i24 (full rate) is exact; a plain `*` lowers
+    // to quarter-rate v_mul_lo_u32 / v_mad_u64_u32.
+    int z1 = M24(tmp12 + tmp13, 4433);
+    p[2 * s] = DESCALE(z1 + M24(tmp13, 6270), sh);
+    p[6 * s] = DESCALE(z1 + M24(tmp12, -15137), sh);
     z1 = tmp4 + tmp7;
     int z2 = tmp5 + tmp6, z3 = tmp4 + tmp6, z4 = tmp5 + tmp7;
-    const int z5 = (z3 + z4) * 9633;
-    tmp4 *= 2446; tmp5 *= 16819; tmp6 *= 25172; tmp7 *= 12299;
-    z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
+    const int z5 = M24(z3 + z4, 9633);
+    tmp4 = M24(tmp4, 2446); tmp5 = M24(tmp5, 16819); tmp6 = M24(tmp6, 25172); tmp7 = M24(tmp7, 12299);
+    z1 = M24(z1, -7373); z2 = M24(z2, -20995); z3 = M24(z3, -16069); z4 = M24(z4, -3196);
     z3 += z5; z4 += z5;
     p[7 * s] = DESCALE(tmp4 + z1 + z3, sh);
     p[5 * s] = DESCALE(tmp5 + z2 + z4, sh);
@@ -677,8 +681,9 @@ __device__ __forceinline__ uint32_t wave_exclusive(uint32_t v, uint32_t& total) 
 // Exact t / d for 0 <= t < 2^16, 1 <= d <= 2040 by one high multiply with m = ceil(2^32 / d):
 // n*m/2^32 exceeds n/d by < 2^-16 < 1/d, so the floor never crosses an integer.
 __device__ __forceinline__ int quant_recip(int t, int half, uint32_t m) {
-    if (t < 0) return -(int)__umulhi((uint32_t)(-t + half), m);
-    return (int)__umulhi((uint32_t)(t + half), m);
+    const int sg = t >> 31;                                   // 0 or -1
+    const int u = (int)__umulhi((uint32_t)((t ^ sg) - sg + half), m);
+    return (u ^ sg) - sg;                                     // sign restored, no branch
 }
 
 __constant__ uint8_t c_zigzag[64] = {
@@ -734,6 +739,10 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     const uint32_t my_ = (uint32_t)((0x100000000ull + (uint64_t)(qy << 3) - 1) / (uint64_t)(qy << 3));
     const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
     const int hy = qy << 2, hc = qc << 2;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
+    const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
+    const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
     const int m0 = (blockIdx.x * 4 + wv) * kB1McuPerWave;
     const int m1 = min(m0 + kB1McuPerWave, A.n_mcu);
     // The next MCU's four pixels are loaded while this one is transformed (one pass of HBM
@@ -808,21 +817,28 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
             }
             dc[k] = q;
-            if (lane != 0) out[k * 64 + lane] = (int16_t)q;
-            // AC Huffman length: run of zeros before this coefficient from the previous non-zero
-            const uint64_t nz = __ballot(lane != 0 && q != 0);
+            out[k * 64 + lane] = (int16_t)q;    // lane 0's DC is rewritten below, after propagation
+            // AC Huffman length, branch-free: run of zeros before this coefficient from the
+            // previous non-zero (bit 0 stands for the DC, so an empty `below` gives prev = 0).
+            const bool nzl = lane != 0 && q != 0;
+            const uint64_t nz = __ballot(nzl);
             const int t = k < 4 ? 0 : 1;
-            uint32_t bits = 0;
-            if (lane != 0 && q != 0) {
-                const uint64_t below = nz & ((1ull << lane) - 1);
-                const int prev = below ? 63 - __clzll(below) : 0;
-                const int r = lane - prev - 1;
-                const int a = q < 0 ? -q : q;
-                const int nbits = 32 - __clz(a);
-                bits = (uint32_t)((r >> 4) * s_acsize[t][0xF0] + s_acsize[t][((r & 15) << 4) | nbits] + nbits);
-            }
-            if (lane == 0 && (nz >> 63) == 0) bits += s_acsize[t][0x00];   // EOB after the last non-zero
-            aclen[k] = wave_sum(bits);
+            const uint64_t below = (nz & lt_mask) | 1ull;
+            const int r = lane - (63 - __clzll(below)) - 1;
+            const int a = q < 0 ? -q : q;
+            const int nbits = 32 - __clz(a);
+            const uint32_t len = (uint32_t)(r >> 4) * (t ? zrl1 : zrl0) + s_acsize[t][((r & 15) << 4) | nbits] + nbits;
+            uint32_t bits = nzl ? len : 0u;
+            if (lane == 0 && (nz >> 63) == 0) bits = t ? eob1 : eob0;   // EOB after the last non-zero
+            aclen[k] = bits;
+        }
+        // A block's AC bits stay below 2^11 (63 x (16 + 10) + ZRLs + EOB), so two blocks share
+        // one 32-bit wave sum in 16-bit halves: three DPP scans instead of six.
+#pragma unroll
+        for (int k = 0; k < 6; k += 2) {
+            const uint32_t s2 = wave_sum(aclen[k] | (aclen[k + 1] << 16));
+            aclen[k] = s2 & 0xFFFF;
+            aclen[k + 1] = s2 >> 16;
         }
         if (lane == 0) {   // jccoefct.c dummy-block DC propagation
             const bool c1 = mx * 2 + 1 >= ywib, row1 = my * 2 + 1 >= yhib;
