@@ -970,73 +970,106 @@ struct B3Args {
 // a static register), the codes come from the LDS Huffman tables and accumulate in a 64-bit
 // register; whole 32-bit words are stored directly, the two words a block may share with its
 // neighbours are ORed in.
+constexpr int kB3LdsWords = 4096;   // a group's stream staged in LDS up to 512 bits per block
+
 __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     __shared__ HuffLds h;
+    __shared__ uint32_t s_ac[2][256];   // AC tables packed as size << 16 | code
+    __shared__ uint32_t s_words[kB3LdsWords];
     __shared__ uint32_t sw[16];
     load_huff_lds(h);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x)
+        s_ac[i >> 8][i & 255] = ((uint32_t)c_huff[1 + 2 * (i >> 8)].size[i & 255] << 16) | c_huff[1 + 2 * (i >> 8)].code[i & 255];
     const int tile = blockIdx.y;
     const int b = blockIdx.x * kGrp + threadIdx.x;
     const int64_t gb = (int64_t)tile * A.nb + b;
-    const uint32_t mybits = b < A.nb ? A.bits[gb] : 0u;
+    const bool live = b < A.nb;
+    const uint32_t mybits = live ? A.bits[gb] : 0u;
     uint32_t gtot;
-    const uint32_t boff = A.goff[(int64_t)tile * A.ngb + blockIdx.x] + block_exclusive_scan(mybits, sw, gtot);
-    if (b >= A.nb) return;
-    const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
-    uint4 q[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) q[i] = src[i];
-    const int pb = prev_block_in_tile(b);
-    const int pred = pb >= 0 ? A.dcs[(int64_t)tile * A.nb + pb] : 0;
+    const uint32_t gbit0 = A.goff[(int64_t)tile * A.ngb + blockIdx.x];
+    const uint32_t boff = gbit0 + block_exclusive_scan(mybits, sw, gtot);
+    // The group's 256 blocks form one contiguous run of the stream: when it fits, it is built in
+    // LDS (ds_or) and copied out coalesced, so HBM sees whole lines instead of one 4-byte store
+    // per lane per word; the group's first and last words are shared with neighbouring groups.
+    const uint32_t gw0 = gbit0 >> 5;
+    const uint32_t nw = (uint32_t)__builtin_amdgcn_readfirstlane((int)(gtot ? ((gbit0 + gtot - 1) >> 5) - gw0 + 1 : 0));
+    const bool staged = nw <= (uint32_t)kB3LdsWords;
     uint32_t* words = A.words + (int64_t)tile * A.slot_words;
-    uint64_t acc = 0;
-    int nacc = (int)(boff & 31);
-    uint32_t wpos = boff >> 5;
-    bool first = true;
-    auto put = [&](uint32_t v, int n) {          // n <= 16
-        acc = (acc << n) | (v & ((1u << n) - 1));
-        nacc += n;
-        if (nacc >= 32) {
-            const uint32_t w = (uint32_t)(acc >> (nacc - 32));
-            if (first) atomicOr(&words[wpos], w);   // shares bits with the previous block
-            else words[wpos] = w;
-            first = false;
-            ++wpos;
-            nacc -= 32;
-        }
-    };
-    auto coef = [&](int k) -> int {
-        const uint32_t* d = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
-        const uint32_t w = d[(k >> 1) & 3];
-        return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
-    };
-    const int kk = b % 6;
-    const int td = kk < 4 ? 0 : 2, ta = td + 1;
-    {
-        int d = coef(0) - pred, d2 = d;
-        if (d < 0) { d = -d; d2--; }
-        const int nbits = d ? 32 - __clz(d) : 0;
-        put(h.code[td][nbits], h.size[td][nbits]);
-        if (nbits) put((uint32_t)d2, nbits);
+    if (staged) {
+        for (uint32_t i = threadIdx.x; i < nw; i += kGrp) s_words[i] = 0;
+        __syncthreads();
     }
-    int r = 0;
+    if (live) {
+        const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
+        uint4 q[8];
 #pragma unroll
-    for (int k = 1; k < 64; ++k) {
-        const int c = coef(k);
-        if (c == 0) {
-            ++r;
-        } else {
-            while (r > 15) { put(h.code[ta][0xF0], h.size[ta][0xF0]); r -= 16; }
-            int a = c, a2 = c;
-            if (a < 0) { a = -a; a2--; }
-            const int nbits = 32 - __clz(a);
-            const int sym = (r << 4) + nbits;
-            put(h.code[ta][sym], h.size[ta][sym]);
-            put((uint32_t)a2, nbits);
-            r = 0;
+        for (int i = 0; i < 8; ++i) q[i] = src[i];
+        const int pb = prev_block_in_tile(b);
+        const int pred = pb >= 0 ? A.dcs[(int64_t)tile * A.nb + pb] : 0;
+        uint64_t acc = 0;
+        int nacc = (int)(boff & 31);
+        uint32_t wpos = boff >> 5;
+        const uint32_t w0 = wpos;
+        auto flush = [&](uint32_t w) {
+            if (staged) atomicOr(&s_words[wpos - gw0], w);
+            else if (wpos == w0) atomicOr(&words[wpos], w);   // shares bits with the previous block
+            else words[wpos] = w;
+        };
+        auto put = [&](uint32_t v, int n) {          // n <= 26, v < 2^n
+            acc = (acc << n) | v;
+            nacc += n;
+            if (nacc >= 32) {
+                flush((uint32_t)(acc >> (nacc - 32)));
+                ++wpos;
+                nacc -= 32;
+            }
+        };
+        auto coef = [&](int k) -> int {
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
+            const uint32_t w = d[(k >> 1) & 3];
+            return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
+        };
+        const int kk = b % 6;
+        const int td = kk < 4 ? 0 : 2, ta = kk < 4 ? 0 : 1;
+        {
+            int d = coef(0) - pred, d2 = d;
+            if (d < 0) { d = -d; d2--; }
+            const int nbits = d ? 32 - __clz(d) : 0;
+            put(((uint32_t)h.code[td][nbits] << nbits) | ((uint32_t)d2 & ((1u << nbits) - 1)), h.size[td][nbits] + nbits);
+        }
+        const uint32_t zrl = s_ac[ta][0xF0];
+        int r = 0;
+        // Branch-free per coefficient: a zero contributes a zero-length code; runs of 16+ zeros
+        // before a non-zero (ZRL) take a wave-uniform, rarely entered branch.
+#pragma unroll
+        for (int k = 1; k < 64; ++k) {
+            const int c = coef(k);
+            const bool nzk = c != 0;
+            if (__ballot(nzk && r > 15)) {
+                if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
+            }
+            const int a = c < 0 ? -c : c;
+            const int nbits = 32 - __clz(a);                       // 0 for c == 0
+            const uint32_t cs = s_ac[ta][((r & 15) << 4) | nbits];
+            const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
+            put(nzk ? v : 0u, nzk ? (int)(cs >> 16) + nbits : 0);
+            r = nzk ? 0 : r + 1;
+        }
+        if (r > 0) put(s_ac[ta][0] & 0xFFFF, (int)(s_ac[ta][0] >> 16));   // EOB
+        if (nacc > 0) {                                                   // shared with the next block
+            const uint32_t w = (uint32_t)(acc << (32 - nacc));
+            if (staged) atomicOr(&s_words[wpos - gw0], w);
+            else atomicOr(&words[wpos], w);
         }
     }
-    if (r > 0) put(h.code[ta][0], h.size[ta][0]);   // EOB
-    if (nacc > 0) atomicOr(&words[wpos], (uint32_t)(acc << (32 - nacc)));   // shared with the next block
+    if (staged) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nw; i += kGrp) {
+            const uint32_t w = s_words[i];
+            if (i == 0 || i == nw - 1) atomicOr(&words[gw0 + i], w);
+            else words[gw0 + i] = w;
+        }
+    }
 }
 
 constexpr int kStuffBytes = 16;   // bytes per chunk in B4a/B6
