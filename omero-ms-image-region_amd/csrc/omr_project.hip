@@ -189,10 +189,19 @@ __device__ __forceinline__ T px_of(typename Raw<T>::U u) {
     return t;
 }
 
-template <typename T, bool BEI, bool BEO, int ALG, bool SPLIT>
+// 32-bit sums for 8/16-bit types when at most 65535 planes are summed: exact (65535 x 65535 <
+// 2^32, 65535 x 32768 < 2^31), and one add per pixel instead of a 64-bit add pair.
+template <typename T> struct Acc32 { using type = typename Acc<T>::type; };
+template <> struct Acc32<int8_t> { using type = int32_t; };
+template <> struct Acc32<uint8_t> { using type = uint32_t; };
+template <> struct Acc32<int16_t> { using type = int32_t; };
+template <> struct Acc32<uint16_t> { using type = uint32_t; };
+constexpr uint32_t kAcc32MaxPlanes = 65535;
+
+template <typename T, bool BEI, bool BEO, int ALG, bool SPLIT, bool NARROW = false>
 __global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter) {
     using U = typename Raw<T>::U;
-    using AT = typename Acc<T>::type;
+    using AT = typename std::conditional<NARROW, typename Acc32<T>::type, typename Acc<T>::type>::type;
     constexpr int V = VecPx<T>::V;
     constexpr bool MAX = ALG == OMR_PROJECTION_MAX;
     using Part = typename std::conditional<MAX, T, AT>::type;
@@ -268,6 +277,11 @@ __global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter)
     ((OMR_GLOBAL p32x4*)(void*)(A.outs[s]))[c] = q;
 }
 
+template <typename T>
+static bool narrow_ok(uint32_t n_iter) {
+    return sizeof(T) <= 2 && !std::is_floating_point<T>::value && n_iter <= kAcc32MaxPlanes;
+}
+
 template <typename T, bool BEI, bool BEO>
 static hipError_t launch_project_v(const K3Args& a, int alg, uint32_t n_iter, bool split, uint32_t chunks16,
                                    int n, hipStream_t s) {
@@ -277,11 +291,13 @@ static hipError_t launch_project_v(const K3Args& a, int alg, uint32_t n_iter, bo
         hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MAX, true>), gs, dim3(kBlock), 0, s, a, n_iter);
         break;
     case OMR_PROJECTION_MEAN:
-        if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        if (split && narrow_ok<T>(n_iter)) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true>), gs, dim3(kBlock), 0, s, a, n_iter);
         else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, false>), g1, dim3(kBlock), 0, s, a, n_iter);
         break;
     default:
-        if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        if (split && narrow_ok<T>(n_iter)) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true>), gs, dim3(kBlock), 0, s, a, n_iter);
         else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, false>), g1, dim3(kBlock), 0, s, a, n_iter);
         break;
     }
