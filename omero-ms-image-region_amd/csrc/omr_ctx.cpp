@@ -46,7 +46,7 @@ omr_status ensure_workspace(Ctx* c, size_t bytes) {
 omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
     if (bytes == 0) return OMR_OK;
     if (bytes > c->pin_cap) {
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < Ctx::kPinSlots; ++i) {
             if (c->pin[i]) {
                 OMR_HIP(c, hipEventSynchronize(c->pin_ev[i]));
                 OMR_HIP(c, hipHostFree(c->pin[i]));
@@ -54,14 +54,18 @@ omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
             }
         }
         size_t cap = align_up(bytes, 1 << 16);
-        for (int i = 0; i < 2; ++i) OMR_HIP(c, hipHostMalloc(&c->pin[i], cap, hipHostMallocDefault));
+        for (int i = 0; i < Ctx::kPinSlots; ++i)   // fine-grained: the copy kernel must never see a stale GPU-cached line
+            OMR_HIP(c, hipHostMalloc(&c->pin[i], cap, hipHostMallocCoherent | hipHostMallocMapped));
         c->pin_cap = cap;
     }
     const int s = c->pin_slot;
-    c->pin_slot ^= 1;
+    c->pin_slot = (s + 1) % Ctx::kPinSlots;
     OMR_HIP(c, hipEventSynchronize(c->pin_ev[s]));  // previous copy out of this slot is done
     std::memcpy(c->pin[s], src, bytes);
-    OMR_HIP(c, hipMemcpyAsync(dst, c->pin[s], bytes, hipMemcpyHostToDevice, c->stream));
+    // A small kernel reads the parameter block straight from the pinned slot (device-mapped host
+    // memory): unlike hipMemcpyAsync, which hands the copy to a DMA engine and makes the next
+    // kernel wait on a cross-engine signal, it orders with the request's kernels like any launch.
+    OMR_HIP(c, launch_h2d_small(c->stream, dst, c->pin[s], bytes));
     OMR_HIP(c, hipEventRecord(c->pin_ev[s], c->stream));
     return OMR_OK;
 }
@@ -110,7 +114,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_flag, 256);
     if (e == hipSuccess) e = hipMemset(c->d_flag, 0, 256);
-    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming);
+    for (int i = 0; i < Ctx::kPinSlots && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device_ordinal) == hipSuccess) c->cu_count = prop.multiProcessorCount;
@@ -157,7 +161,7 @@ void omr_ctx_destroy(omr_ctx* c) {
     if (c->pixbuf_state && c->pixbuf_state_free) c->pixbuf_state_free(c->pixbuf_state);
     for (auto& t : c->timed) { c->event_pool.push_back(t.start); c->event_pool.push_back(t.stop); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < Ctx::kPinSlots; ++i) {
         if (c->pin_ev[i]) (void)hipEventDestroy(c->pin_ev[i]);
         if (c->pin[i]) (void)hipHostFree(c->pin[i]);
     }

@@ -68,9 +68,10 @@ struct Ctx {
     // device-side sticky status word (quantization errors of async calls)
     int32_t* d_flag = nullptr;
     // pinned staging for parameter blocks (2-slot ring)
-    void* pin[2] = {nullptr, nullptr};
+    static constexpr int kPinSlots = 8;   // parameter blocks in flight: the host runs this many ahead
+    void* pin[kPinSlots] = {};
     size_t pin_cap = 0;
-    hipEvent_t pin_ev[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[kPinSlots] = {};
     int pin_slot = 0;
     int cu_count = 256;
     // kernel timing (omr_ctx_enable_kernel_timing)
@@ -98,6 +99,9 @@ omr_status hip_fail(Ctx* c, hipError_t e, const char* what);
 // Ensure the workspace holds at least `bytes`; invalidates previous contents.
 omr_status ensure_workspace(Ctx* c, size_t bytes);
 // Copy `bytes` from host `src` to device `dst` through the pinned ring (async on ctx stream).
+// Copy `bytes` from device-accessible pinned host memory to device memory with a kernel on `s`
+// (omr_render.hip).
+hipError_t launch_h2d_small(hipStream_t s, void* dst, const void* pinned_src, size_t bytes);
 omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes);
 int bytes_per_pixel(int32_t pixel_type);
 // K3 launch over up to 32 stacks (omr_project.hip).

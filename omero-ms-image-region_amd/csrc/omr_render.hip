@@ -35,6 +35,25 @@ __device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int 
     return (r << 20) | (g << 10) | b;
 }
 
+// Parameter blocks (plans, pointer tables, headers: a few KiB) from pinned host memory.
+__global__ void __launch_bounds__(256) k_h2d_small(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                   uint64_t bytes) {
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i + 16 <= bytes && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
+        *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+        for (uint64_t j = i; j < i + 16 && j < bytes; ++j) dst[j] = src[j];
+    }
+}
+
+hipError_t launch_h2d_small(hipStream_t s, void* dst, const void* pinned_src, size_t bytes) {
+    if (bytes == 0) return hipSuccess;
+    const uint64_t blocks = (bytes + 16 * 256 - 1) / (16 * 256);
+    hipLaunchKernelGGL(k_h2d_small, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<uint8_t*>(dst),
+                       static_cast<const uint8_t*>(pinned_src), (uint64_t)bytes);
+    return hipGetLastError();
+}
+
 // grid: n_active blocks x 256 threads.  Table8 channels are indexed by the raw byte.
 __global__ void __launch_bounds__(256) k_build_contrib(const RenderPlan* __restrict__ plan,
                                                        uint32_t* __restrict__ contrib, int is_signed8) {

@@ -205,8 +205,8 @@ class Context:
 
     def render_projected_device(self, qdef, channels, stacks, pixel_type, size_x, size_y, size_z,
                                 algorithm, start, end, out, stepping=1, big_endian=False,
-                                flip_h=False, flip_v=False):
-        arr, keep = make_bindings(channels)
+                                flip_h=False, flip_v=False, bindings=None):
+        arr, keep = make_bindings(channels) if bindings is None else bindings
         ptrs = (ctypes.c_void_p * max(len(stacks), 1))(*[_ptr(s) for s in stacks])
         check(lib.omr_render_projected_device(self.h, ctypes.byref(qdef), arr, len(channels), ptrs,
                                               pixel_type, int(big_endian), size_x, size_y, size_z,
