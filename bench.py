@@ -98,6 +98,16 @@ def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
         ctx.synchronize()
         if i >= 3:
             t_dev.append(time.perf_counter() - t0)
+    # the whole render_image_region request at its default format: render + one-tile JPEG
+    # (q 0.9) copied back to the host (ImageRegionRequestHandler.java:559-582)
+    t_jpg = []
+    for i in range(iters + 3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.render_packed_int_device(qdef, chans, planes, _lib.PIXELS_UINT16, TILE, TILE, out1, big_endian=True)
+        ctx.encode_jpeg_device(out1, TILE, TILE, 0.9)
+        if i >= 3:
+            t_jpg.append(time.perf_counter() - t0)
     host = [np.ascontiguousarray(p.cpu().numpy()) for p in planes]
     t_host = []
     for i in range(iters + 3):
@@ -106,6 +116,7 @@ def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
         if i >= 3:
             t_host.append(time.perf_counter() - t0)
     return {"device_resident": round(1e3 * float(np.median(t_dev)), 4),
+            "device_resident_to_jpeg_host": round(1e3 * float(np.median(t_jpg)), 4),
             "host_fed": round(1e3 * float(np.median(t_host)), 4)}
 
 

@@ -565,6 +565,13 @@ static omr_status encode_jpeg_ws(Ctx* ctx, const uint32_t* d_argb, int W, int H,
     return OMR_OK;
 }
 
+// One tile through the batched pipeline (defined below): B1..B6 with n = 1, then the file is
+// copied to `out` (two host syncs, like the legacy J1-J6 path, at a fraction of its kernel time).
+static omr_status encode_jpeg_single_batched(Ctx* ctx, const uint32_t* d_argb, int W, int H, float quality,
+                                             uint8_t* out, size_t cap, size_t* out_len, size_t base);
+static size_t single_batched_bytes(int W, int H, size_t base);
+constexpr int kJpegBatchMaxDim = 4096;
+
 static omr_status check_jpeg_dims(Ctx* ctx, int W, int H) {
     if (W <= 0 || H <= 0 || W > 65535 || H > 65535)
         return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG dimensions must be 1..65535");
@@ -596,6 +603,8 @@ omr_status omr_encode_jpeg_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t 
     if (st) return st;
     if (!d_argb) return fail(ctx, OMR_INVALID_ARGUMENT, "null ARGB buffer");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
+    if (width <= kJpegBatchMaxDim && height <= kJpegBatchMaxDim)
+        return encode_jpeg_single_batched(ctx, d_argb, width, height, quality, out, cap, out_len, 0);
     const JpegLayout L = jpeg_layout(width, height, 0);
     st = ensure_workspace(ctx, L.total);
     if (st) return st;
@@ -610,6 +619,13 @@ omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, in
     if (!argb) return fail(ctx, OMR_INVALID_ARGUMENT, "null ARGB buffer");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const size_t img = align_up((size_t)width * height * 4, 256);
+    if (width <= kJpegBatchMaxDim && height <= kJpegBatchMaxDim) {
+        // the image goes to the workspace's first `img` bytes; the batch layout starts after it
+        omr_status gs = ensure_workspace(ctx, single_batched_bytes(width, height, img));   // no regrow below
+        if (gs) return gs;
+        OMR_HIP(ctx, hipMemcpyAsync(ctx->ws, argb, (size_t)width * height * 4, hipMemcpyHostToDevice, ctx->stream));
+        return encode_jpeg_single_batched(ctx, nullptr, width, height, quality, out, cap, out_len, img);
+    }
     const JpegLayout L = jpeg_layout(width, height, img);
     st = ensure_workspace(ctx, L.total);
     if (st) return st;
@@ -699,10 +715,11 @@ struct B1Args {
     uint16_t* aclen;      // [tile][nb] AC bits incl. ZRL/EOB
     int16_t* dcs;         // [tile][nb] DC after dummy-block propagation
     int32_t W, H, mcux, n_mcu, nb;
+    int32_t mpw;          // MCUs per wave (prefetch depth vs. waves in flight)
     QTabs qt;
 };
 
-constexpr int kB1McuPerWave = 4;
+constexpr int kB1McuPerWave = 4;   // big batches; a few tiles use 1 so the grid still fills the chip
 
 // Pixels (x, y) and (x+1, y) of one row (clamped to the image), as one 8-byte load when both
 // are inside the row.
@@ -743,8 +760,8 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
     const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
     const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
-    const int m0 = (blockIdx.x * 4 + wv) * kB1McuPerWave;
-    const int m1 = min(m0 + kB1McuPerWave, A.n_mcu);
+    const int m0 = (blockIdx.x * 4 + wv) * A.mpw;
+    const int m1 = min(m0 + A.mpw, A.n_mcu);
     // The next MCU's four pixels are loaded while this one is transformed (one pass of HBM
     // latency per wave instead of one per MCU).
     // Even widths: two unconditional 8-byte loads per lane at clamped addresses; the edge
@@ -1298,6 +1315,8 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     a1.mcux = (W + 15) / 16;
     a1.n_mcu = (int32_t)L.n_mcu;
     a1.nb = (int32_t)L.nb;
+    // 4 MCUs per wave once that still gives >= 4 waves per SIMD (16 per CU)
+    a1.mpw = (int64_t)n * L.n_mcu >= (int64_t)kB1McuPerWave * 16 * ctx->cu_count ? kB1McuPerWave : 1;
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
     uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
     B2aArgs a2{a1.aclen, a1.dcs, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
@@ -1315,7 +1334,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     KernelTimer whole(ctx, 4);
     {
         KernelTimer t(ctx, 5);
-        hipLaunchKernelGGL(k_jpeg_fdct_batch, dim3((unsigned)((L.n_mcu + 4 * kB1McuPerWave - 1) / (4 * kB1McuPerWave)),
+        hipLaunchKernelGGL(k_jpeg_fdct_batch, dim3((unsigned)((L.n_mcu + 4 * a1.mpw - 1) / (4 * a1.mpw)),
                                                     (unsigned)n), dim3(256), 0,
                            ctx->stream, a1);
     }
@@ -1339,6 +1358,37 @@ static omr_status check_jpeg_batch(Ctx* ctx, const void* d_argb, int n, int W, i
     if (W <= 0 || H <= 0 || W > 4096 || H > 4096)
         return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: tile dimensions must be 1..4096");
     if (stride < (int64_t)W * H) return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: tile stride < width*height");
+    return OMR_OK;
+}
+
+static size_t single_batched_bytes(int W, int H, size_t base) {
+    const JpegBatchLayout L = jpeg_batch_layout(W, H, 1, base);
+    return align_up(L.total, 256) + 512 + omr_jpeg_max_bytes(W, H);
+}
+
+static omr_status encode_jpeg_single_batched(Ctx* ctx, const uint32_t* d_argb, int W, int H, float quality,
+                                             uint8_t* out, size_t cap, size_t* out_len, size_t base) {
+    const JpegBatchLayout L = jpeg_batch_layout(W, H, 1, base);
+    const size_t o_offs = align_up(L.total, 256), o_lens = o_offs + 256, o_out = o_lens + 256;
+    const size_t jcap = omr_jpeg_max_bytes(W, H);
+    // (a regrow reallocates without copying: the host-input caller sized the workspace first)
+    omr_status st = ensure_workspace(ctx, single_batched_bytes(W, H, base));
+    if (st) return st;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    if (!d_argb) d_argb = reinterpret_cast<const uint32_t*>(ws);   // host-input variant staged at offset 0
+    uint64_t* d_offs = reinterpret_cast<uint64_t*>(ws + o_offs);
+    uint32_t* d_lens = reinterpret_cast<uint32_t*>(ws + o_lens);
+    st = encode_jpeg_batch_ws(ctx, d_argb, (int64_t)W * H, 1, W, H, quality, ws + o_out, jcap, d_offs, d_lens,
+                              nullptr, L);
+    if (st) return st;
+    uint32_t len = 0;
+    OMR_HIP(ctx, hipMemcpyAsync(&len, d_lens, 4, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (len == 0) return fail(ctx, OMR_DEVICE, "JPEG: stream exceeded the worst-case bound");
+    if (out_len) *out_len = len;
+    if (!out || cap < len) return fail(ctx, OMR_BUFFER_TOO_SMALL, "JPEG output buffer too small");
+    OMR_HIP(ctx, hipMemcpyAsync(out, ws + o_out, len, hipMemcpyDeviceToHost, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return OMR_OK;
 }
 
