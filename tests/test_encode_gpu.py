@@ -67,6 +67,35 @@ def test_c1_greyscale_u8_tile_to_jpeg(ctx):
     assert decode(jpg).size == (1024, 1024)
 
 
+@pytest.mark.parametrize("w,h,q", [(4096, 16, 0.9), (4100, 9, 0.9), (5000, 3, 0.5)])
+def test_jpeg_single_tile_paths_around_batch_limit(ctx, w, h, q):
+    """Up to 4096 px a single tile runs the batched B1-B6 pipeline with n = 1; wider images keep
+    the legacy single-tile kernels.  Both, from host and from device memory, byte-identical."""
+    import torch
+    rng = np.random.default_rng(w * 7 + h)
+    argb = argb_of(rng.integers(0, 256, (h, w, 3)))
+    exp = O.encode_jpeg(argb, w, h, q)
+    assert ctx.encode_jpeg(argb, w, h, q) == exp
+    assert ctx.encode_jpeg_device(torch.from_numpy(argb.view(np.int32)).to("cuda"), w, h, q) == exp
+
+
+def test_jpeg_undersized_output_reports_length(ctx):
+    """A short caller buffer gives BUFFER_TOO_SMALL and still reports the needed length."""
+    import ctypes
+    import torch
+    from omr.context import lib
+    w, h = 64, 48
+    argb = argb_of(np.random.default_rng(3).integers(0, 256, (h, w, 3)))
+    exp = O.encode_jpeg(argb, w, h, 0.9)
+    d = torch.from_numpy(argb.view(np.int32)).to("cuda")
+    out = np.zeros(16, np.uint8)
+    n = ctypes.c_size_t(0)
+    st = lib.omr_encode_jpeg_device(ctx.h, ctypes.c_void_p(d.data_ptr()), w, h, ctypes.c_float(0.9),
+                                    out.ctypes.data, out.size, ctypes.byref(n))
+    assert st == _lib.BUFFER_TOO_SMALL and n.value == len(exp)
+    assert ctx.encode_jpeg_device(d, w, h, 0.9) == exp      # the context recovers
+
+
 def test_jpeg_errors(ctx):
     with pytest.raises(_lib.OmrError):
         ctx.encode_jpeg(np.zeros((1, 1), np.uint32), 0, 1, 0.9)

@@ -435,3 +435,28 @@ def test_mixed_threshold_and_eval_channels(ctx):
             got = host_render(ctx, chans, src, pt, w, h, big_endian=be)
             assert_argb_close(got, exp, tol=1)
             assert np.mean(got == exp) > 0.99
+
+
+def test_back_to_back_settings_through_staging_ring(ctx):
+    """More in-flight calls than the 8-slot parameter ring, each with its own windows, colours and
+    flip, queued without a host sync: every output must carry its own call's settings (a reused
+    slot must never feed a later call's plan to an earlier launch, or the reverse)."""
+    import torch
+    w, h = 96, 40
+    planes = [p.astype(">u2") for p in tile_u16(11, 3, h, w)]
+    dplanes = [dev(p) for p in planes]
+    q = O.make_qdef("rgb")
+    calls = []
+    for i in range(21):
+        chans = [{"active": True, "input_start": f32(100 * i + 50 * c), "input_end": f32(20000 + 1500 * i + 700 * c),
+                  "global_min": 0.0, "global_max": 65535.0, "rgba": C2_COLORS[(i + c) % 4],
+                  "reverse": (i + c) % 3 == 0} for c in range(3)]
+        out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+        ctx.render_packed_int_device(q, chans, dplanes, _lib.PIXELS_UINT16, w, h, out, big_endian=True,
+                                     flip_h=i % 2 == 1, flip_v=i % 5 == 0)
+        calls.append((chans, out, i % 2 == 1, i % 5 == 0))
+    ctx.synchronize()
+    for i, (chans, out, fh, fv) in enumerate(calls):
+        st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, big_endian=True, flip_h=fh, flip_v=fv)
+        assert st == 0
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp, err_msg=f"call {i}")
