@@ -1223,9 +1223,13 @@ struct B6Args {
 };
 
 // B6: per group of 256 chunks: in-group scan of the 0xFF counts, stuffed bytes staged in LDS,
-// copied out coalesced.  Block 0 of each tile also writes the JFIF header.
+// copied out coalesced.  Block 0 of each tile also writes the JFIF header.  A chunk without 0xFF
+// (nearly all of them) lands as five ORed LDS words, funnel-shifted to its byte offset; a chunk
+// with 0xFF bytes ORs its expanded bytes one by one.  (Per-byte stores from every lane at a
+// 16-byte lane stride had 40 % LDS bank-conflict cycles.)
 __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
-    __shared__ uint8_t sbytes[kGrp * kStuffBytes * 2];
+    constexpr int kSW = kGrp * kStuffBytes * 2 / 4;
+    __shared__ uint32_t swords[kSW + 4];
     __shared__ uint32_t sw[16];
     const int tile = blockIdx.y;
     if (A.lengths[tile] == 0) return;          // did not fit: status says so
@@ -1240,6 +1244,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
     for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
         const uint32_t c = g * kGrp + threadIdx.x;
         const uint32_t n = c < nch ? A.cnt[(int64_t)tile * A.slot_chunks + c] : 0u;
+        for (int i = threadIdx.x; i < kSW + 4; i += kGrp) swords[i] = 0;   // ordered by the scan's barrier
         uint32_t gtot;
         const uint32_t ex = block_exclusive_scan(n, sw, gtot);
         uint32_t o = threadIdx.x * kStuffBytes + ex;
@@ -1247,15 +1252,29 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
             uint32_t w[4];
             chunk_bytes(words, c, nbytes, tb, w);
             const uint32_t e = min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes);
-            for (uint32_t i = 0; i < e; ++i) {
-                const uint32_t bv = (w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
-                sbytes[o++] = (uint8_t)bv;
-                if (bv == 0xFF) sbytes[o++] = 0;
+            if (n == 0 && e == kStuffBytes) {
+                // stream byte k -> LDS byte o + k: little-endian words, shifted by o & 3 bytes
+                const uint32_t sh = 8 * (o & 3), wi = o >> 2;
+                const uint32_t l0 = __builtin_bswap32(w[0]), l1 = __builtin_bswap32(w[1]);
+                const uint32_t l2 = __builtin_bswap32(w[2]), l3 = __builtin_bswap32(w[3]);
+                atomicOr(&swords[wi], l0 << sh);
+                atomicOr(&swords[wi + 1], (uint32_t)((((uint64_t)l1 << 32) | l0) >> (32 - sh)));
+                atomicOr(&swords[wi + 2], (uint32_t)((((uint64_t)l2 << 32) | l1) >> (32 - sh)));
+                atomicOr(&swords[wi + 3], (uint32_t)((((uint64_t)l3 << 32) | l2) >> (32 - sh)));
+                if (sh) atomicOr(&swords[wi + 4], l3 >> (32 - sh));
+            } else {
+                for (uint32_t i = 0; i < e; ++i) {
+                    const uint32_t bv = (w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
+                    atomicOr(&swords[o >> 2], bv << (8 * (o & 3)));
+                    ++o;
+                    if (bv == 0xFF) ++o;                                  // stuffed 0x00 (already zero)
+                }
             }
         }
         __syncthreads();
         const uint32_t gbytes = min(nbytes - g * kGrp * kStuffBytes, (uint32_t)(kGrp * kStuffBytes)) + gtot;
         const uint64_t base = (uint64_t)g * kGrp * kStuffBytes + A.coff[(int64_t)tile * A.slot_groups + g];
+        const uint8_t* sbytes = reinterpret_cast<const uint8_t*>(swords);
         for (uint32_t i = threadIdx.x; i < gbytes; i += kGrp) out[base + i] = sbytes[i];
         __syncthreads();
     }
@@ -1328,9 +1347,11 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     B5Args a5{u32(L.stuffed), d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
     B6Args a6{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), d_offsets, d_lengths, ws + L.hdr, d_out,
               L.slot_words, L.slot_chunks, L.slot_groups, (int32_t)hdr.size()};
-    // chunk groups of a typical stream (<= ~2 B per pixel); longer streams loop in B4a/B6
+    // chunk groups of a typical stream (<= ~1 B per pixel; q 0.9 C2 tiles are 0.37, uniform noise
+    // 0.8); longer streams loop in B4a/B6.  Workgroups past the stream end only exit, but at
+    // 2 B per pixel they were 4/5 of both grids.
     const int64_t est_groups = std::max<int64_t>(1, std::min<int64_t>(L.slot_groups,
-                                   ((int64_t)W * H * 2 / kStuffBytes + kGrp - 1) / kGrp));
+                                   ((int64_t)W * H / kStuffBytes + kGrp - 1) / kGrp));
     KernelTimer whole(ctx, 4);
     {
         KernelTimer t(ctx, 5);
