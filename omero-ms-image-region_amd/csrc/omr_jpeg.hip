@@ -787,19 +787,32 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     if (m0 < m1) fetch(m0);
     for (int m = m0; m < m1; ++m) {   // wave-uniform loop
         const int mx = m % A.mcux, my = m / A.mcux;
+        // Grey MCU (every pixel r == g == b, e.g. the greyscale model's output): IJG's Y is then
+        // (65536 v + 32768) >> 16 = v exactly and Cb = Cr = 128, so both chroma blocks are zero —
+        // the colour transform, their FDCT and their quantisation are skipped.  Wave-uniform; the
+        // bottom-edge chroma rows (odd heights) take the general path.
+        bool grey;
         {
             const int x0 = mx * 16 + 2 * cx;
             uint32_t p00 = nclamp ? na.y : na.x, p01 = na.y, p10 = nclamp ? nb.y : nb.x, p11 = nb.y;
             if (m + 1 < m1) fetch(m + 1);
+            const int chv = (H + 1) / 2;
+            const int cyg = my * 8 + cy;
+            auto isg = [](uint32_t p) { return (p & 0xFFFFu) == ((p >> 8) & 0xFFFFu); };
+            grey = __ballot(!(isg(p00) && isg(p01) && isg(p10) && isg(p11)) || cyg >= chv) == 0;
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
             const int o = ((2 * cy) & 7) * 8 + ((2 * cx) & 7);
+            if (grey) {
+                S[blk * kBS + o] = (int)(p00 & 0xFFu) - 128;
+                S[blk * kBS + o + 1] = (int)(p01 & 0xFFu) - 128;
+                S[blk * kBS + o + 8] = (int)(p10 & 0xFFu) - 128;
+                S[blk * kBS + o + 9] = (int)(p11 & 0xFFu) - 128;
+            } else {
             ycc(p00, y, cb0, cr0); S[blk * kBS + o] = y - 128;
             ycc(p01, y, cb1, cr1); S[blk * kBS + o + 1] = y - 128;
             ycc(p10, y, cb2, cr2); S[blk * kBS + o + 8] = y - 128;
             ycc(p11, y, cb3, cr3); S[blk * kBS + o + 9] = y - 128;
-            const int chv = (H + 1) / 2;
-            const int cyg = my * 8 + cy;
             if (cyg >= chv) {
                 const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
                 const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
@@ -810,15 +823,17 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
             const int bias = (cx & 1) ? 2 : 1;
             S[4 * kBS + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
             S[5 * kBS + cy * 8 + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
+            }
         }
+        const int nfd = grey ? 32 : 48;   // lanes with a block row / column to transform
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < 48) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * 8, 1);
+        if (lane < nfd) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * 8, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < 48) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), 8);
+        if (lane < nfd) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), 8);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -828,6 +843,12 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
         uint32_t aclen[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
+            if (k >= 4 && grey) {                 // zero chroma block: DC 0, EOB only
+                dc[k] = 0;
+                out[k * 64 + lane] = 0;
+                aclen[k] = lane == 0 ? eob1 : 0u;
+                continue;
+            }
             int q = k < 4 ? quant_recip(S[k * kBS + nat], hy, my_) : quant_recip(S[k * kBS + nat], hc, mc_);
             if (k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);

@@ -31,6 +31,11 @@ def content(kind, h, w, seed):
         return argb_of(img)
     if kind == "flat":                       # all-zero AC: EOB-only blocks, DC-only
         return np.full((h, w), 0xFF336699, np.uint32)
+    if kind == "grey":                       # r == g == b (greyscale model): B1's grey-MCU path,
+        v = rng.integers(0, 256, (h, w))     # with a few colour pixels so some MCUs are mixed
+        img = np.stack([v, v, v], -1)
+        img[rng.integers(0, h, 3), rng.integers(0, w, 3), 0] ^= 1
+        return argb_of(img)
     yy, xx = np.mgrid[0:h, 0:w]               # smooth gradient + mild noise
     rgb = np.stack([(xx * 255 // max(w - 1, 1)), (yy * 255 // max(h - 1, 1)), (xx + yy) % 256], -1)
     rgb = np.clip(rgb + rng.integers(-3, 4, rgb.shape), 0, 255)
@@ -45,17 +50,19 @@ def run_batch(ctx, tiles, w, h, q, stride=None):
     for i, t in enumerate(tiles):
         buf[i * stride:i * stride + w * h] = t.reshape(-1)
     d = torch.from_numpy(buf.view(np.int32)).to("cuda")
-    return ctx.encode_jpeg_batch(d, n, w, h, q, tile_stride=stride if stride != w * h else 0)
+    # room for noise at q 1.0 (over 1 B/px): the default cap assumes typical content
+    return ctx.encode_jpeg_batch(d, n, w, h, q, cap=n * (4 * w * h + 4096),
+                                 tile_stride=stride if stride != w * h else 0)
 
 
 @pytest.mark.parametrize("w,h", [(1, 1), (8, 8), (17, 9), (16, 16), (333, 77), (15, 200), (256, 256)])
 @pytest.mark.parametrize("q", [0.85, 1.0, 0.05])
 def test_batch_byte_identical_mixed_content(ctx, w, h, q):
-    kinds = ["noise", "sparse", "flat", "smooth"]
-    tiles = [content(kinds[i % 4], h, w, 1000 * w + h + i) for i in range(6)]
+    kinds = ["noise", "sparse", "flat", "smooth", "grey"]
+    tiles = [content(kinds[i % 5], h, w, 1000 * w + h + i) for i in range(6)]
     got = run_batch(ctx, tiles, w, h, q)
     for i, t in enumerate(tiles):
-        assert got[i] == O.encode_jpeg(t, w, h, q), f"tile {i} ({kinds[i % 4]})"
+        assert got[i] == O.encode_jpeg(t, w, h, q), f"tile {i} ({kinds[i % 5]})"
 
 
 def test_batch_golden_vectors(ctx):
