@@ -358,7 +358,10 @@ __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restr
     bkt[a * kBuckets + b] = e;
 }
 
-constexpr int kCPT = 2;   // chunks per thread of the fixed-channel-count kernels
+#ifndef OMR_K2_CPT
+#define OMR_K2_CPT 2
+#endif
+constexpr int kCPT = OMR_K2_CPT;   // chunks per thread of the fixed-channel-count kernels
 
 // LDS of one K2 block: contrib [na][256] u32, then (kModeThresh) thresholds [na][256] u32 and
 // buckets [na][kBuckets] u16.

@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libomr.so")
+LIB_PATH = os.environ.get("OMR_LIB") or os.path.join(_HERE, "libomr.so")   # OMR_LIB: a deployed build
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
