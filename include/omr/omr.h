@@ -302,7 +302,9 @@ size_t omr_png_max_bytes(int32_t width, int32_t height, int32_t channels);
  * standard Huffman tables) of the 24-bit RGB view of ARGB pixels
  * (ImageUtil.createBufferedImage + compressionService.compressToStream,
  *  ImageRegionRequestHandler.java:576-582).  Quality is per call.
- * Host ARGB in, host bytes out.
+ * Host ARGB in, host bytes out.  *out_len always receives the file length; a NULL `out` or
+ * cap < length returns OMR_BUFFER_TOO_SMALL (query, then call again).  Tiles up to 4096 px
+ * run the batched pipeline below with one tile; larger images the single-tile kernels.
  */
 omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, int32_t height,
                            float quality, uint8_t* out, size_t cap, size_t* out_len);
