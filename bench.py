@@ -115,9 +115,23 @@ def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
         ctx.render_packed_int(qdef, chans, host, _lib.PIXELS_UINT16, TILE, TILE, big_endian=True)
         if i >= 3:
             t_host.append(time.perf_counter() - t0)
-    return {"device_resident": round(1e3 * float(np.median(t_dev)), 4),
-            "device_resident_to_jpeg_host": round(1e3 * float(np.median(t_jpg)), 4),
-            "host_fed": round(1e3 * float(np.median(t_host)), 4)}
+    res = {"device_resident": round(1e3 * float(np.median(t_dev)), 4),
+           "device_resident_to_jpeg_host": round(1e3 * float(np.median(t_jpg)), 4),
+           "host_fed": round(1e3 * float(np.median(t_host)), 4)}
+    # the same requests from C++ through the C ABI (tools/omr_latency.cpp, built by build()):
+    # what a JNI / Panama caller sees without Python's marshalling
+    exe = os.path.join(REPO, "tools", "omr_latency")
+    if os.path.exists(exe):
+        import subprocess
+        try:
+            r = subprocess.run([exe, "200", str(dev.index or 0)], capture_output=True, text=True, timeout=120)
+            if r.returncode == 0:
+                res["native_c_abi"] = json.loads(r.stdout.strip().splitlines()[-1])
+            else:
+                log(f"omr_latency failed ({r.returncode}): {r.stderr.strip()[-300:]}")
+        except Exception as e:
+            log(f"omr_latency failed: {e}")
+    return res
 
 
 def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_cpu):

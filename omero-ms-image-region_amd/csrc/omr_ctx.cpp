@@ -43,7 +43,8 @@ omr_status ensure_workspace(Ctx* c, size_t bytes) {
     return OMR_OK;
 }
 
-omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
+omr_status stage_h2d2(Ctx* c, void* dst1, const void* src1, size_t n1, void* dst2, const void* src2, size_t n2) {
+    const size_t off2 = align_up(n1, 16), bytes = off2 + n2;
     if (bytes == 0) return OMR_OK;
     if (bytes > c->pin_cap) {
         for (int i = 0; i < Ctx::kPinSlots; ++i) {
@@ -61,13 +62,20 @@ omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
     const int s = c->pin_slot;
     c->pin_slot = (s + 1) % Ctx::kPinSlots;
     OMR_HIP(c, hipEventSynchronize(c->pin_ev[s]));  // previous copy out of this slot is done
-    std::memcpy(c->pin[s], src, bytes);
-    // A small kernel reads the parameter block straight from the pinned slot (device-mapped host
+    uint8_t* slot = static_cast<uint8_t*>(c->pin[s]);
+    if (n1) std::memcpy(slot, src1, n1);
+    if (n2) std::memcpy(slot + off2, src2, n2);
+    // A small kernel reads the parameter blocks straight from the pinned slot (device-mapped host
     // memory): unlike hipMemcpyAsync, which hands the copy to a DMA engine and makes the next
     // kernel wait on a cross-engine signal, it orders with the request's kernels like any launch.
-    OMR_HIP(c, launch_h2d_small(c->stream, dst, c->pin[s], bytes));
+    // Two blocks (e.g. plan + plane-pointer table) share one launch.
+    OMR_HIP(c, launch_h2d_small(c->stream, dst1, slot, n1, dst2, slot + off2, n2));
     OMR_HIP(c, hipEventRecord(c->pin_ev[s], c->stream));
     return OMR_OK;
+}
+
+omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes) {
+    return stage_h2d2(c, dst, src, bytes, nullptr, nullptr, 0);
 }
 
 static hipEvent_t pooled_event(Ctx* c) {
@@ -114,6 +122,8 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_flag, 256);
     if (e == hipSuccess) e = hipMemset(c->d_flag, 0, 256);
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void**>(&c->h_flag), 64, hipHostMallocCoherent | hipHostMallocMapped);
     for (int i = 0; i < Ctx::kPinSlots && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming);
     if (e == hipSuccess) {
         hipDeviceProp_t prop;
@@ -167,6 +177,7 @@ void omr_ctx_destroy(omr_ctx* c) {
     }
     if (c->ws) (void)hipFree(c->ws);
     if (c->d_flag) (void)hipFree(c->d_flag);
+    if (c->h_flag) (void)hipHostFree(c->h_flag);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -175,14 +186,12 @@ const char* omr_last_error(const omr_ctx* c) { return c ? c->last_error.c_str() 
 
 omr_status omr_ctx_synchronize(omr_ctx* c) {
     if (!c) return OMR_INVALID_ARGUMENT;
+    // the status word rides behind the queued work (and is cleared there): one sync, no
+    // separate D2H copy and second wait
+    OMR_HIP(c, launch_flag_out(c->stream, c->d_flag, c->h_flag));
     OMR_HIP(c, hipStreamSynchronize(c->stream));
-    int32_t flag = 0;
-    OMR_HIP(c, hipMemcpy(&flag, c->d_flag, sizeof(flag), hipMemcpyDeviceToHost));
-    if (flag) {
-        OMR_HIP(c, hipMemsetAsync(c->d_flag, 0, sizeof(flag), c->stream));
-        OMR_HIP(c, hipStreamSynchronize(c->stream));
-        return fail(c, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");
-    }
+    const int32_t flag = *static_cast<volatile int32_t*>(c->h_flag);
+    if (flag) return fail(c, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");
     return OMR_OK;
 }
 

@@ -67,6 +67,7 @@ struct Ctx {
     size_t ws_cap = 0;
     // device-side sticky status word (quantization errors of async calls)
     int32_t* d_flag = nullptr;
+    int32_t* h_flag = nullptr;   // fine-grained pinned word: d_flag copied here by a kernel at sync
     // pinned staging for parameter blocks (2-slot ring)
     static constexpr int kPinSlots = 8;   // parameter blocks in flight: the host runs this many ahead
     void* pin[kPinSlots] = {};
@@ -99,10 +100,16 @@ omr_status hip_fail(Ctx* c, hipError_t e, const char* what);
 // Ensure the workspace holds at least `bytes`; invalidates previous contents.
 omr_status ensure_workspace(Ctx* c, size_t bytes);
 // Copy `bytes` from host `src` to device `dst` through the pinned ring (async on ctx stream).
+// Move the sticky device status word to fine-grained host memory and clear it, on `s`
+// (omr_render.hip): omr_ctx_synchronize then needs one stream sync and no copy round trip.
+hipError_t launch_flag_out(hipStream_t s, int32_t* d_flag, int32_t* h_flag);
 // Copy `bytes` from device-accessible pinned host memory to device memory with a kernel on `s`
 // (omr_render.hip).
-hipError_t launch_h2d_small(hipStream_t s, void* dst, const void* pinned_src, size_t bytes);
+hipError_t launch_h2d_small(hipStream_t s, void* dst1, const void* pinned_src1, size_t n1,
+                            void* dst2 = nullptr, const void* pinned_src2 = nullptr, size_t n2 = 0);
 omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes);
+// Two parameter blocks through one ring slot and one copy launch.
+omr_status stage_h2d2(Ctx* c, void* dst1, const void* src1, size_t n1, void* dst2, const void* src2, size_t n2);
 int bytes_per_pixel(int32_t pixel_type);
 // K3 launch over up to 32 stacks (omr_project.hip).
 omr_status validate_projection_args(Ctx* c, int32_t pixel_type, int32_t size_x, int32_t size_y,

@@ -35,9 +35,14 @@ __device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int 
     return (r << 20) | (g << 10) | b;
 }
 
-// Parameter blocks (plans, pointer tables, headers: a few KiB) from pinned host memory.
-__global__ void __launch_bounds__(256) k_h2d_small(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                   uint64_t bytes) {
+// Parameter blocks (plans, pointer tables, headers: a few KiB) from pinned host memory;
+// blockIdx.y selects one of two (dst, src, bytes) segments.
+__global__ void __launch_bounds__(256) k_h2d_small(uint8_t* __restrict__ dst1, const uint8_t* __restrict__ src1,
+                                                   uint64_t n1, uint8_t* __restrict__ dst2,
+                                                   const uint8_t* __restrict__ src2, uint64_t n2) {
+    uint8_t* dst = blockIdx.y ? dst2 : dst1;
+    const uint8_t* src = blockIdx.y ? src2 : src1;
+    const uint64_t bytes = blockIdx.y ? n2 : n1;
     const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
     if (i + 16 <= bytes && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0) {
         *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
@@ -46,11 +51,25 @@ __global__ void __launch_bounds__(256) k_h2d_small(uint8_t* __restrict__ dst, co
     }
 }
 
-hipError_t launch_h2d_small(hipStream_t s, void* dst, const void* pinned_src, size_t bytes) {
+__global__ void k_flag_out(int32_t* __restrict__ d_flag, int32_t* __restrict__ h_flag) {
+    const int32_t f = *d_flag;
+    *h_flag = f;                    // visible to the host after the stream synchronises
+    if (f) *d_flag = 0;
+}
+
+hipError_t launch_flag_out(hipStream_t s, int32_t* d_flag, int32_t* h_flag) {
+    hipLaunchKernelGGL(k_flag_out, dim3(1), dim3(1), 0, s, d_flag, h_flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_h2d_small(hipStream_t s, void* dst1, const void* pinned_src1, size_t n1,
+                            void* dst2, const void* pinned_src2, size_t n2) {
+    const size_t bytes = std::max(n1, n2);
     if (bytes == 0) return hipSuccess;
     const uint64_t blocks = (bytes + 16 * 256 - 1) / (16 * 256);
-    hipLaunchKernelGGL(k_h2d_small, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<uint8_t*>(dst),
-                       static_cast<const uint8_t*>(pinned_src), (uint64_t)bytes);
+    hipLaunchKernelGGL(k_h2d_small, dim3((unsigned)blocks, n2 ? 2u : 1u), dim3(256), 0, s, static_cast<uint8_t*>(dst1),
+                       static_cast<const uint8_t*>(pinned_src1), (uint64_t)n1, static_cast<uint8_t*>(dst2),
+                       static_cast<const uint8_t*>(pinned_src2), (uint64_t)n2);
     return hipGetLastError();
 }
 
@@ -809,14 +828,18 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
                                  const void* const* d_plane_ptrs, int32_t size_c, int32_t n_tiles,
                                  int64_t row_stride, int32_t width, int32_t height, int32_t flip_h,
                                  int32_t flip_v, uint32_t* d_out, int32_t* d_status, bool aligned,
-                                 const RenderLayout& L, const Strided* strided = nullptr) {
+                                 const RenderLayout& L, const Strided* strided = nullptr,
+                                 const void* ptr_src = nullptr, size_t ptr_bytes = 0) {
+    // ptr_bytes > 0: the host plane-pointer table ptr_src goes to d_plane_ptrs in the same
+    // staging launch as the plan
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
     uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
     uint8_t* d_luts = ws + L.lut_off;
     // LUT offsets are relative to the LUT region; make them workspace-relative for K2.
     for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off += L.lut_off;
-    omr_status st = stage_h2d(ctx, d_plan, &pp.plan, pp.plan_bytes);
+    omr_status st = stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, const_cast<const void**>(d_plane_ptrs),
+                               ptr_src, ptr_src ? ptr_bytes : 0);
     for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off -= L.lut_off;
     if (st != OMR_OK) return st;
     const int na = pp.plan.n_active;
@@ -1042,15 +1065,14 @@ omr_status omr_render_packed_int_device(omr_ctx* ctx, const omr_quantum_def* qde
     const void** d_ptrs = reinterpret_cast<const void**>(static_cast<uint8_t*>(ctx->ws) + L.extra_off);
     std::vector<const void*> ptrs(size_c > 0 ? size_c : 1, nullptr);
     for (int c = 0; c < size_c; ++c) ptrs[c] = d_planes ? d_planes[c] : nullptr;
-    st = stage_h2d(ctx, d_ptrs, ptrs.data(), ptr_bytes);
-    if (st) return st;
     const int bpp = bytes_per_pixel(pixel_type);
     bool aligned = vec_aligned(bpp, width, row_stride);
     for (int c = 0; c < size_c && aligned; ++c)
         if (ptrs[c] && (reinterpret_cast<uintptr_t>(ptrs[c]) % 16)) aligned = false;
     if (reinterpret_cast<uintptr_t>(d_argb_out) % 16) aligned = false;
     return enqueue_render(ctx, pp, pixel_type, big_endian, d_ptrs, size_c, 1, row_stride, width, height,
-                          flip_h, flip_v, d_argb_out, nullptr, aligned, L);
+                          flip_h, flip_v, d_argb_out, nullptr, aligned, L, nullptr, ptrs.data(),
+                          sizeof(void*) * ptrs.size());
 }
 
 omr_status omr_render_packed_int(omr_ctx* ctx, const omr_quantum_def* qdef,
@@ -1089,10 +1111,9 @@ omr_status omr_render_packed_int(omr_ctx* ctx, const omr_quantum_def* qdef,
         OMR_HIP(ctx, hipMemcpy2DAsync(dst, (size_t)width * bpp, planes[c], (size_t)row_stride * bpp,
                                       (size_t)width * bpp, height, hipMemcpyHostToDevice, ctx->stream));
     }
-    st = stage_h2d(ctx, d_ptrs, ptrs.data(), sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1));
-    if (st) return st;
     st = enqueue_render(ctx, pp, pixel_type, big_endian, d_ptrs, size_c, 1, width, width, height, flip_h,
-                        flip_v, d_out, nullptr, vec_aligned(bpp, width, width), L);
+                        flip_v, d_out, nullptr, vec_aligned(bpp, width, width), L, nullptr, ptrs.data(),
+                        sizeof(void*) * ptrs.size());
     if (st) return st;
     OMR_HIP(ctx, hipMemcpyAsync(argb_out, d_out, (size_t)width * height * 4, hipMemcpyDeviceToHost, ctx->stream));
     return omr_ctx_synchronize(ctx);
@@ -1147,9 +1168,7 @@ extern "C" omr_status omr_render_projected_device(
                                 size_y, algorithm, start, end, stepping, 0);
         if (st) return st;
     }
-    st = stage_h2d(ctx, d_ptrs, ptrs.data(), sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1));
-    if (st) return st;
     const bool aligned = vec_aligned(bpp, size_x, size_x) && (reinterpret_cast<uintptr_t>(d_argb_out) % 16 == 0);
     return enqueue_render(ctx, pp, pixel_type, 0, d_ptrs, size_c, 1, size_x, size_x, size_y, flip_h, flip_v,
-                          d_argb_out, nullptr, aligned, L);
+                          d_argb_out, nullptr, aligned, L, nullptr, ptrs.data(), sizeof(void*) * ptrs.size());
 }
