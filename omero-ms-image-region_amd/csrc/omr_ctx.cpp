@@ -178,6 +178,7 @@ void omr_ctx_destroy(omr_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->d_flag) (void)hipFree(c->d_flag);
     if (c->h_flag) (void)hipHostFree(c->h_flag);
+    if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }

@@ -68,6 +68,10 @@ struct Ctx {
     // device-side sticky status word (quantization errors of async calls)
     int32_t* d_flag = nullptr;
     int32_t* h_flag = nullptr;   // fine-grained pinned word: d_flag copied here by a kernel at sync
+    // fine-grained pinned landing buffer for single-file results (one-tile JPEG): a kernel writes
+    // the file and its length here, so the caller needs one stream sync
+    uint8_t* h_out = nullptr;
+    size_t h_out_cap = 0;
     // pinned staging for parameter blocks (2-slot ring)
     static constexpr int kPinSlots = 8;   // parameter blocks in flight: the host runs this many ahead
     void* pin[kPinSlots] = {};

@@ -1403,6 +1403,22 @@ static omr_status check_jpeg_batch(Ctx* ctx, const void* d_argb, int n, int W, i
     return OMR_OK;
 }
 
+// The single tile's file and length into fine-grained pinned host memory (host_len first, then
+// the bytes at host + 16), 16 B per lane; lanes past the file exit.
+__global__ void __launch_bounds__(256) k_file_to_host(const uint8_t* __restrict__ src, const uint32_t* __restrict__ d_len,
+                                                      uint8_t* __restrict__ host) {
+    const uint32_t len = *d_len;
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i == 0) *reinterpret_cast<uint32_t*>(host) = len;
+    if (i >= len) return;
+    uint8_t* dst = host + 16;
+    if (i + 16 <= len) {
+        *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+        for (uint64_t j = i; j < len; ++j) dst[j] = src[j];
+    }
+}
+
 static size_t single_batched_bytes(int W, int H, size_t base) {
     const JpegBatchLayout L = jpeg_batch_layout(W, H, 1, base);
     return align_up(L.total, 256) + 512 + omr_jpeg_max_bytes(W, H);
@@ -1423,14 +1439,28 @@ static omr_status encode_jpeg_single_batched(Ctx* ctx, const uint32_t* d_argb, i
     st = encode_jpeg_batch_ws(ctx, d_argb, (int64_t)W * H, 1, W, H, quality, ws + o_out, jcap, d_offs, d_lens,
                               nullptr, L);
     if (st) return st;
-    uint32_t len = 0;
-    OMR_HIP(ctx, hipMemcpyAsync(&len, d_lens, 4, hipMemcpyDeviceToHost, ctx->stream));
+    // the file lands in the context's pinned buffer straight from the device (one sync, no
+    // length round trip before the copy)
+    if (ctx->h_out_cap < jcap + 16) {
+        if (ctx->h_out) {
+            OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            OMR_HIP(ctx, hipHostFree(ctx->h_out));
+            ctx->h_out = nullptr;
+            ctx->h_out_cap = 0;
+        }
+        OMR_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_out), jcap + 16,
+                                   hipHostMallocCoherent | hipHostMallocMapped));
+        ctx->h_out_cap = jcap + 16;
+    }
+    hipLaunchKernelGGL(k_file_to_host, dim3((unsigned)((jcap + 16 * 256 - 1) / (16 * 256))), dim3(256), 0,
+                       ctx->stream, ws + o_out, d_lens, ctx->h_out);
+    OMR_HIP(ctx, hipGetLastError());
     OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t len = *reinterpret_cast<volatile uint32_t*>(ctx->h_out);
     if (len == 0) return fail(ctx, OMR_DEVICE, "JPEG: stream exceeded the worst-case bound");
     if (out_len) *out_len = len;
     if (!out || cap < len) return fail(ctx, OMR_BUFFER_TOO_SMALL, "JPEG output buffer too small");
-    OMR_HIP(ctx, hipMemcpyAsync(out, ws + o_out, len, hipMemcpyDeviceToHost, ctx->stream));
-    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::memcpy(out, ctx->h_out + 16, len);
     return OMR_OK;
 }
 
