@@ -1230,6 +1230,8 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_tile_scan(B5Args A) {
     }
 }
 
+constexpr int kJpegHdrMax = 704;   // SOI + APP0 + 2 DQT + SOF0 + 4 DHT + SOS is 607 bytes
+
 struct B6Args {
     const uint32_t* words;
     const uint32_t* tile_bits;
@@ -1237,10 +1239,10 @@ struct B6Args {
     const uint32_t* coff;    // [tile][slot_groups] exclusive 0xFF count before each group
     const uint64_t* offsets;
     const uint32_t* lengths;
-    const uint8_t* hdr;
     uint8_t* out;
     int64_t slot_words, slot_chunks, slot_groups;
     int32_t hdr_len;
+    uint8_t hdr[kJpegHdrMax];   // JFIF header by value in the kernarg segment (no staging launch)
 };
 
 // B6: per group of 256 chunks: in-group scan of the 0xFF counts, stuffed bytes staged in LDS,
@@ -1341,8 +1343,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     std::vector<uint8_t> hdr;
     jpeg_header(hdr, W, H, ql, qc);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
-    omr_status sst = stage_h2d(ctx, ws + L.hdr, hdr.data(), hdr.size());   // pinned ring: async-safe
-    if (sst) return sst;
+    if (hdr.size() > (size_t)kJpegHdrMax) return fail(ctx, OMR_INTERNAL, "JPEG header larger than its kernarg slot");
     auto u32 = [&](size_t off) { return reinterpret_cast<uint32_t*>(ws + off); };
     B1Args a1;
     a1.argb = d_argb;
@@ -1366,8 +1367,9 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
                L.slot_groups};
     GroupScanArgs a4b{u32(L.csum), u32(L.ngroups), u32(L.stuffed), nullptr, u32(L.tbits), L.slot_groups, 0, 0};
     B5Args a5{u32(L.stuffed), d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
-    B6Args a6{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), d_offsets, d_lengths, ws + L.hdr, d_out,
-              L.slot_words, L.slot_chunks, L.slot_groups, (int32_t)hdr.size()};
+    B6Args a6{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), d_offsets, d_lengths, d_out,
+              L.slot_words, L.slot_chunks, L.slot_groups, (int32_t)hdr.size(), {}};
+    std::memcpy(a6.hdr, hdr.data(), hdr.size());
     // chunk groups of a typical stream (<= ~1 B per pixel; q 0.9 C2 tiles are 0.37, uniform noise
     // 0.8); longer streams loop in B4a/B6.  Workgroups past the stream end only exit, but at
     // 2 B per pixel they were 4/5 of both grids.
