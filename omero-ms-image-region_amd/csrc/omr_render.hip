@@ -411,9 +411,9 @@ __device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_con
 // (CPT*NA 16-B loads in flight per lane); plain loads (measured faster than non-temporal here,
 // tools/probe_stream.hip).  NA == 0: runtime channel count, one chunk per thread, clamp per add.
 // STAGE: load the LDS tables here, after the pixel loads are in flight (one-pass grids).
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, bool STAGE>
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, bool STAGE, int CPTT>
 __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* s_contrib) {
-    constexpr int CPT = NA > 0 ? kCPT : 1;
+    constexpr int CPT = NA > 0 ? CPTT : 1;
     constexpr int NL = NA > 0 ? NA : 1;
     const int na = NA > 0 ? NA : A.n_active;
     const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
@@ -582,18 +582,24 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
 // Integer / 8-bit modes: one full (non-persistent) grid, one work block per workgroup, tables
 // staged behind the pixel loads.  Eval mode (float / 32-bit; threshold + bucket tables up to
 // 6 KiB per channel): a grid of a few workgroups per CU that stage the tables once and stride
-// over the work blocks.
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
+// over the work blocks.  CPTT: chunks per thread when NA > 0 — kCPT for batches, 1 for launches
+// too small to fill the chip at kCPT (a one-tile request, a C3 composite), twice the workgroups.
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, int CPTT = kCPT>
 __global__ void __launch_bounds__(kBlock) k_render(const K2Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
     if constexpr (MODE == kK2Eval || MODE == kK2Thresh) {
         k2_stage_tables<MODE, BPP>(A, s_contrib, NA > 0 ? NA : A.n_active);
         __syncthreads();
         for (uint32_t wb = blockIdx.x; wb < A.n_work; wb += gridDim.x)
-            k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, false>(A, wb, s_contrib);
+            k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, false, CPTT>(A, wb, s_contrib);
     } else {
-        k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, true>(A, blockIdx.x, s_contrib);
+        k2_work<BPP, VEC, BE, SIGNED, PT, NA, MODE, true, CPTT>(A, blockIdx.x, s_contrib);
     }
+}
+
+// Small-launch threshold: below this many kCPT work blocks K2 runs one chunk per thread.
+static inline bool k2_small_launch(uint64_t total_chunks, int cu_count) {
+    return kCPT > 1 && total_chunks < (uint64_t)kBlock * kCPT * (uint64_t)cu_count * 4;
 }
 
 // ------------------------------------------------------------------------------- host side
@@ -747,8 +753,19 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
 }
 
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
-static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_t s) {
+static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s) {
     const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
+    if constexpr (BPP <= 2 && kCPT > 1) {   // grid-stride eval modes size their own grid
+        if (small) {
+            switch (na) {
+            case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            default: break;
+            }
+        }
+    }
     switch (na) {
     case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
     case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
@@ -760,37 +777,38 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, hipStream_
 }
 
 template <int BPP, int VEC, bool BE>
-static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, int grid, hipStream_t s) {
+static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, int grid, bool small, hipStream_t s) {
     if constexpr (BPP == 1) {
-        return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8, kK2Table8>(a, na, grid, s)
-                                     : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8, kK2Table8>(a, na, grid, s);
+        return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8, kK2Table8>(a, na, grid, small, s)
+                                     : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8, kK2Table8>(a, na, grid, small, s);
     } else if constexpr (BPP == 2) {
         if (pt == OMR_PIXELS_INT16) {
-            if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Fast16>(a, na, grid, s);
-            return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Linear16>(a, na, grid, s)
-                                         : launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Mixed16>(a, na, grid, s);
+            if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Fast16>(a, na, grid, small, s);
+            return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Linear16>(a, na, grid, small, s)
+                                         : launch_render_na<2, VEC, BE, true, OMR_PIXELS_INT16, kK2Mixed16>(a, na, grid, small, s);
         }
-        if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Fast16>(a, na, grid, s);
-        return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, s)
-                                     : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, s);
+        if (mode16 == kK2Fast16) return launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Fast16>(a, na, grid, small, s);
+        return mode16 == kK2Linear16 ? launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Linear16>(a, na, grid, small, s)
+                                     : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, small, s);
     } else if constexpr (BPP == 4) {
         if (mode16 == kK2Thresh) {
-            if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Thresh>(a, na, grid, s);
-            if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Thresh>(a, na, grid, s);
-            return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Thresh>(a, na, grid, s);
+            if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Thresh>(a, na, grid, small, s);
+            if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Thresh>(a, na, grid, small, s);
+            return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Thresh>(a, na, grid, small, s);
         }
-        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, s);
-        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, s);
-        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, s);
+        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, small, s);
+        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, small, s);
+        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, small, s);
     } else {
-        return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE, kK2Eval>(a, na, grid, s);
+        return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE, kK2Eval>(a, na, grid, small, s);
     }
 }
 
 template <int BPP, int VEC>
-static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int mode16, int grid, hipStream_t s) {
-    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, mode16, grid, s)
-              : launch_render_pt<BPP, VEC, false>(a, pt, na, mode16, grid, s);
+static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int mode16, int grid, bool small,
+                                   hipStream_t s) {
+    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, mode16, grid, small, s)
+              : launch_render_pt<BPP, VEC, false>(a, pt, na, mode16, grid, small, s);
 }
 
 // kK2Fast16 preconditions (see fast16): default codomain, increasing window, finite slope,
@@ -906,7 +924,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cd_end = pp.plan.cd_end;
     a.cds8 = pp.plan.cd_start & 0xFF;
     a.cde8 = pp.plan.cd_end & 0xFF;
-    const int cpt_thread = (na >= 1 && na <= 4) ? kCPT : 1;
+    // one chunk per thread for launches too small to fill the chip (launch_render_na)
+    const bool small = bpp <= 2 && k2_small_launch(total, ctx->cu_count);
+    const int cpt_thread = (na >= 1 && na <= 4 && !small) ? kCPT : 1;
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.total = (uint32_t)total;
     a.cpt = make_fastdiv((uint32_t)cpt);
@@ -945,17 +965,17 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     KernelTimer timer(ctx, 2);
     if (aligned) {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
         }
     } else {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
-        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, mode16, grid, ctx->stream); break;
+        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
         }
     }
     OMR_HIP(ctx, e);
