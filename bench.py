@@ -317,16 +317,41 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
     qd = make_qdef("rgb")
     out = torch.empty((S, S), dtype=torch.int32, device=dev)
     binds = make_bindings(chans)   # marshalled once, as a Java caller would hold its Renderer state
+    import omr
+    ctx2 = omr.Context(ctx.device)
     res = {}
     for name, alg, end in (("max", _lib.PROJECTION_MAX, Z - 1), ("mean", _lib.PROJECTION_MEAN, Z - 1)):
         def step():
             ctx.render_projected_device(qd, chans, stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, out,
                                         big_endian=True, bindings=binds)
         el, avg = _timed(torch, ctx, step, steps, warmup)
+        # Two contexts (two HIP streams, as two Vert.x workers each holding one) taking alternate
+        # requests: one request's K3 overlaps the other's launch gaps and small K1/K2 launches.
+        outs = [out, torch.empty_like(out)]
+        ctxs = [ctx, ctx2]
+        k = [0]
+
+        def step2():
+            i = k[0] & 1
+            k[0] += 1
+            ctxs[i].render_projected_device(qd, chans, stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end,
+                                            outs[i], big_endian=True, bindings=binds)
+        for _ in range(warmup):
+            step2()
+        ctx.synchronize()
+        ctx2.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(2 * steps):
+            step2()
+        ctx.synchronize()
+        ctx2.synchronize()
+        el2 = time.perf_counter() - t0
+        assert torch.equal(outs[0], outs[1]), "two-stream C3 renders differ"
         k3 = avg.get(3, float("nan"))
         used_z = Z if alg == _lib.PROJECTION_MAX else Z - 1
         alg_bytes = C * (used_z * S * S * 2 + S * S * 2)
         r = {"requests_per_s": round(steps / el, 1), "ms_per_request": round(1e3 * el / steps, 4),
+             "requests_per_s_two_streams": round(2 * steps / el2, 1),
              "kernel_ms": {"K3_project": round(k3, 5), "K2_render": round(avg.get(2, float("nan")), 5)},
              "roofline": {"bound": "hbm", "kernel": f"k_project<u16,BE,{name}> (K3)",
                           "achieved": round(alg_bytes / (k3 * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -353,6 +378,7 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
             except Exception as e:
                 log(f"c3 cpu baseline failed: {e}")
         res[name] = r
+    ctx2.close()
     return res
 
 
