@@ -73,26 +73,24 @@ hipError_t launch_h2d_small(hipStream_t s, void* dst1, const void* pinned_src1, 
     return hipGetLastError();
 }
 
-// grid: n_active blocks x 256 threads.  Table8 channels are indexed by the raw byte.
-__global__ void __launch_bounds__(256) k_build_contrib(const RenderPlan* __restrict__ plan,
-                                                       uint32_t* __restrict__ contrib, int is_signed8) {
-    const int a = blockIdx.x;
+// Contribution-table entry t of active channel a (K1, and K2's in-LDS build for small launches).
+// Table8 channels are indexed by the raw byte.
+__device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__ plan, int a, int t, int is_signed8) {
     const ChanParam& p = plan->ch[a];
-    const int t = threadIdx.x;
     const int cds = plan->cd_start, cde = plan->cd_end;
-    uint32_t e;
     if (p.mode == kModeTable8) {
         const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
-        if (value < p.gmin || value > p.gmax) {
-            e = kErrBit;
-        } else {
-            const int v = quantize_eval((double)value, p, cds, cde);
-            e = pack_contrib(p, v, cds, cde, plan->greyscale);
-        }
-    } else {
-        e = pack_contrib(p, t, cds, cde, plan->greyscale);
+        if (value < p.gmin || value > p.gmax) return kErrBit;
+        const int v = quantize_eval((double)value, p, cds, cde);
+        return pack_contrib(p, v, cds, cde, plan->greyscale);
     }
-    contrib[a * 256 + t] = e;
+    return pack_contrib(p, t, cds, cde, plan->greyscale);
+}
+
+// grid: n_active blocks x 256 threads.
+__global__ void __launch_bounds__(256) k_build_contrib(const RenderPlan* __restrict__ plan,
+                                                       uint32_t* __restrict__ contrib, int is_signed8) {
+    contrib[blockIdx.x * 256 + threadIdx.x] = contrib_entry(plan, blockIdx.x, threadIdx.x, is_signed8);
 }
 
 // grid: (ceil(n/256), n_active); builds the byte LUT of every kModeLut16 channel.
@@ -460,8 +458,14 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
         }
     }
     if constexpr (STAGE) {
-        // tables -> LDS, issued after the pixel loads so their latencies overlap
-        k2_stage_tables<MODE, BPP>(A, s_contrib, na);
+        // tables -> LDS, issued after the pixel loads so their latencies overlap.  Small launches
+        // (CPTT 1, integer modes) build them from the plan here instead: no K1 launch per request.
+        if constexpr (CPTT == 1 && kCPT > 1 && BPP <= 2) {
+            for (int i = threadIdx.x; i < na * 256; i += kBlock)
+                s_contrib[i] = contrib_entry(A.plan, i >> 8, i & 255, PT == OMR_PIXELS_INT8 ? 1 : 0);
+        } else {
+            k2_stage_tables<MODE, BPP>(A, s_contrib, na);
+        }
         __syncthreads();
     }
     uint32_t* const s_thr = s_contrib + na * 256;
@@ -861,10 +865,21 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off -= L.lut_off;
     if (st != OMR_OK) return st;
     const int na = pp.plan.n_active;
+    const int bpp = bytes_per_pixel(pixel_type);
+    const int vec = aligned ? (bpp <= 2 ? 8 : 16 / bpp) : 1;
+    const uint64_t cpr = (uint64_t)width / vec;
+    const uint64_t cpt = cpr * (uint64_t)height;
+    const uint64_t total = cpt * (uint64_t)n_tiles;
+    // one chunk per thread for launches too small to fill the chip (launch_render_na); those
+    // K2 instantiations (1..4 active channels) build the contribution tables in LDS themselves
+    const bool small = bpp <= 2 && k2_small_launch(total, ctx->cu_count);
+    const bool k2_builds_contrib = small && na >= 1 && na <= 4;
     if (na > 0) {
-        hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
-                           pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
-        OMR_HIP(ctx, hipGetLastError());
+        if (!k2_builds_contrib) {
+            hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
+                               pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
+            OMR_HIP(ctx, hipGetLastError());
+        }
         if (pp.n_lut > 0) {
             hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan, ws);
             OMR_HIP(ctx, hipGetLastError());
@@ -887,11 +902,6 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         OMR_HIP(ctx, hipGetLastError());
     }
     (void)d_luts;
-    const int bpp = bytes_per_pixel(pixel_type);
-    const int vec = aligned ? (bpp <= 2 ? 8 : 16 / bpp) : 1;
-    const uint64_t cpr = (uint64_t)width / vec;
-    const uint64_t cpt = cpr * (uint64_t)height;
-    const uint64_t total = cpt * (uint64_t)n_tiles;
     if (total == 0) return OMR_OK;
     if (total >= (1ull << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "batch too large for one launch");
     K2Args a;
@@ -924,8 +934,6 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cd_end = pp.plan.cd_end;
     a.cds8 = pp.plan.cd_start & 0xFF;
     a.cde8 = pp.plan.cd_end & 0xFF;
-    // one chunk per thread for launches too small to fill the chip (launch_render_na)
-    const bool small = bpp <= 2 && k2_small_launch(total, ctx->cu_count);
     const int cpt_thread = (na >= 1 && na <= 4 && !small) ? kCPT : 1;
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.total = (uint32_t)total;

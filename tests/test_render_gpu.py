@@ -460,3 +460,38 @@ def test_back_to_back_settings_through_staging_ring(ctx):
         st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, w, h, big_endian=True, flip_h=fh, flip_v=fv)
         assert st == 0
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp, err_msg=f"call {i}")
+
+
+@pytest.mark.parametrize("pt,na", [(_lib.PIXELS_UINT8, 1), (_lib.PIXELS_INT8, 2), (_lib.PIXELS_UINT16, 4),
+                                   (_lib.PIXELS_INT16, 3)])
+@pytest.mark.parametrize("n", [63, 64])
+def test_small_and_full_launch_boundary(ctx, pt, na, n):
+    """K2 runs one chunk per lane, with the contribution tables built in LDS instead of by K1,
+    below 4 work blocks per CU (k2_small_launch: 256² 8/16-bit tiles give 8192 chunks, so 63
+    tiles are small and 64 are not on a 256-CU part).  Both sides bit-exact against the oracle,
+    with a reversed channel, a LUT channel and a flip."""
+    import torch
+    h = w = 256
+    bpp = 1 if pt in (_lib.PIXELS_UINT8, _lib.PIXELS_INT8) else 2
+    dt = {_lib.PIXELS_UINT8: np.uint8, _lib.PIXELS_INT8: np.int8, _lib.PIXELS_UINT16: np.uint16,
+          _lib.PIXELS_INT16: np.int16}[pt]
+    info = np.iinfo(dt)
+    rng = np.random.default_rng(100 + pt * 10 + na)
+    host = rng.integers(info.min, int(info.max) + 1, (n, na, h, w)).astype(dt)
+    chans = c2_channels(na)
+    for i, c in enumerate(chans):
+        lo, hi = float(info.min), float(info.max)
+        c["global_min"], c["global_max"] = lo, hi
+        c["input_start"], c["input_end"] = f32(lo + (hi - lo) * 0.1 * (i + 1)), f32(hi - (hi - lo) * 0.05 * i)
+    chans[0]["reverse"] = True
+    if na > 1:
+        chans[1]["lut"] = np.stack([np.arange(256), 255 - np.arange(256), np.arange(256) // 2], -1).astype(np.uint8)
+    out = torch.empty((n, h, w), dtype=torch.int32, device="cuda")
+    pb = h * w * bpp
+    ctx.render_batch_strided_device(O.make_qdef("rgb"), chans, dev(host), na * pb, pb, n, pt, w, h, out,
+                                    flip_h=True)
+    got = out.cpu().numpy().view(np.uint32)
+    for t in (0, n // 2, n - 1):
+        st, exp = O.render(chans, [np.ascontiguousarray(host[t, c]) for c in range(na)], pt, w, h, flip_h=True)
+        assert st == 0
+        np.testing.assert_array_equal(got[t], exp, err_msg=f"tile {t}")
