@@ -60,27 +60,64 @@ def pmc_traffic(batch):
         return None
 
 
-def cpu_baseline(torch, uniq, seconds, threads):
-    """Reference-CPU proxy on a bounded sample: per-request LUT rebuild + render, thread pool."""
+def host_cores():
+    """(threads, nproc, quota): the CPUs this process may run on (what `nproc` prints), the
+    cgroup CPU quota if one is set (cpu.max: quota/period CPUs' worth of time), and the thread
+    count the CPU baseline uses — nproc, capped at the quota: on the GPU box nproc is the whole
+    machine (256) while the job may use 16 CPUs' worth of time, and 256 threads time-sliced onto
+    16 CPUs run the C2 baseline at 455 tiles/s against ~1000 with 16 (gpurun_out r02a)."""
+    import math
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(p), 2)
+    except Exception:
+        pass
+    threads = min(n, max(1, math.ceil(quota))) if quota else n
+    return threads, n, quota
+
+
+def _oracle():
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    import numpy as np
     import oracle_lib
+    return oracle_lib
+
+
+def cpu_baseline(torch, uniq, seconds, threads):
+    """Reference-CPU proxy on a bounded sample: per-request LUT rebuild + render, on `threads`
+    (= nproc) worker threads, and the same work on one thread."""
+    import numpy as np
+    oracle_lib = _oracle()
     from omr import _lib
     from omr.synthetic import c2_channels
     host = uniq.cpu().numpy().view(np.uint16)      # big-endian bytes in uint16 storage
     tiles = [[np.ascontiguousarray(host[t, c]) for c in range(CHANNELS)] for t in range(host.shape[0])]
     chans = c2_channels(CHANNELS)
-    n = threads
-    secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
-                                         _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
-                                         n_threads=threads, keep_output=False)
-    n = max(threads, int(n * seconds / max(secs, 1e-3)) // threads * threads)
-    secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
-                                         _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
-                                         n_threads=threads, keep_output=False)
+
+    def run(nthreads, secs_target):
+        n = nthreads
+        secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
+                                             _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
+                                             n_threads=nthreads, keep_output=False, fast=True)
+        n = max(nthreads, int(n * secs_target / max(secs, 1e-3)) // nthreads * nthreads)
+        secs, _ = oracle_lib.render_tiles_mt(chans, [tiles[t % len(tiles)] for t in range(n)], n,
+                                             _lib.PIXELS_UINT16, TILE, TILE, big_endian=True,
+                                             n_threads=nthreads, keep_output=False, fast=True)
+        return n, secs
+    n, secs = run(threads, seconds)
+    n1, secs1 = run(1, min(4.0, seconds / 2))
+    _, nproc, quota = host_cores()
     return {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cgroup_cpu_quota": quota, "build": oracle_lib.FAST_BUILD,
+            "single_thread": {"value": round(n1 / secs1, 3), "unit": "tiles/s", "cores": 1,
+                              "sample": f"{n1} tiles in {secs1:.2f} s"},
             "sample": f"{n} C2 tiles (4ch uint16 1024^2 BE, per-request LUT rebuild + composite) "
-                      f"in {secs:.2f} s on {threads} threads (oracle/omr_oracle.c, -O3)"}
+                      f"in {secs:.2f} s on {threads} threads (nproc {nproc}, cgroup quota {quota} CPUs) "
+                      f"(oracle/omr_oracle.c, "
+                      f"{oracle_lib.FAST_BUILD})"}
 
 
 def latencies(torch, omr, ctx, qdef, chans, data, iters=30):
@@ -227,33 +264,38 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
 
 
 def jpeg_cpu_baseline(torch, name, src, chans, pt, be, q, seconds, threads):
-    """CPU restatement render + JPEG per request on a thread pool (ctypes releases the GIL)."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from concurrent.futures import ThreadPoolExecutor
+    """Per request: CPU-restatement render (ISA-tuned build) + an IJG-grade JPEG encoder
+    (PIL / libjpeg-turbo, SIMD islow FDCT + Huffman) at the Java ImageIO quality tables, 4:2:0 —
+    the libjpeg lineage of the JDK writer behind compressToStream (ImageRegionRequestHandler.java:
+    581).  Thread pool of nproc workers (ctypes and PIL's encoder release the GIL), and one thread."""
+    import io
     import numpy as np
-    import oracle_lib
+    from PIL import Image, features
+    oracle_lib = _oracle()
     model = "greyscale" if len(chans) == 1 else "rgb"
     host = src[:4].cpu().numpy()
     if host.ndim == 4:
         tiles = [[np.ascontiguousarray(host[t, c]) for c in range(host.shape[1])] for t in range(host.shape[0])]
     else:
         tiles = [[np.ascontiguousarray(host[t])] for t in range(host.shape[0])]
+    ql, qc = oracle_lib.quant_tables(q)
+    qtables = [[int(v) for v in ql], [int(v) for v in qc]]
 
     def one(i):
-        st, argb = oracle_lib.render(chans, tiles[i % len(tiles)], pt, TILE, TILE, model=model, big_endian=be)
-        return len(oracle_lib.encode_jpeg(argb, TILE, TILE, q))
+        st, argb = oracle_lib.render(chans, tiles[i % len(tiles)], pt, TILE, TILE, model=model, big_endian=be,
+                                     fast=True)
+        rgb = argb.view(np.uint8).reshape(TILE, TILE, 4)[:, :, 2::-1]      # BGRA bytes -> RGB
+        buf = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(rgb), "RGB").save(buf, "JPEG", qtables=qtables, subsampling=2)
+        return buf.tell()
 
-    with ThreadPoolExecutor(threads) as ex:
-        t0 = time.perf_counter()
-        list(ex.map(one, range(threads)))
-        first = time.perf_counter() - t0
-        n = max(threads, int(threads * seconds / max(first, 1e-3)) // threads * threads)
-        t0 = time.perf_counter()
-        list(ex.map(one, range(n)))
-        secs = time.perf_counter() - t0
+    n, secs = _cpu_pool(one, seconds, threads)
+    n1, secs1 = _cpu_pool(one, min(3.0, seconds / 2), 1)
     return {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
+            "single_thread": {"value": round(n1 / secs1, 3), "unit": "tiles/s", "cores": 1},
             "sample": f"{n} tiles ({name}: render + JPEG q={q}) in {secs:.2f} s on {threads} threads "
-                      f"(oracle/omr_oracle.c, -O3)"}
+                      f"(render: oracle/omr_oracle.c {oracle_lib.FAST_BUILD}; JPEG: libjpeg-turbo "
+                      f"{features.version('libjpeg_turbo')} via PIL)"}
 
 
 def _timed(torch, ctx, step, steps, warmup):
@@ -359,22 +401,22 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
                           "algorithmic_bytes_per_launch": alg_bytes}}
         if with_cpu:
             try:
-                sys.path.insert(0, os.path.join(REPO, "tests"))
-                import oracle_lib
+                oracle_lib = _oracle()
                 host = [s.cpu().numpy().view(np.uint16) for s in stacks]
 
                 def one(i):
                     planes = []
                     for c in range(C):
                         st, p = oracle_lib.project(host[c], _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, be_in=True,
-                                                   be_out=True)
+                                                   be_out=True, fast=True)
                         planes.append(p.view(np.uint16))
-                    oracle_lib.render(chans, planes, _lib.PIXELS_UINT16, S, S, big_endian=True)
+                    oracle_lib.render(chans, planes, _lib.PIXELS_UINT16, S, S, big_endian=True, fast=True)
                 n, secs = _cpu_pool(one, cpu_seconds, threads)
                 r["cpu_baseline"] = {"value": round(n / secs, 3), "unit": "requests/s", "cores": threads,
                                      "kind": "port",
                                      "sample": f"{n} C3 {name} requests (3x project 512x512x64 u16 + composite) "
-                                               f"in {secs:.2f} s on {threads} threads (oracle/omr_oracle.c, -O3)"}
+                                               f"in {secs:.2f} s on {threads} threads (oracle/omr_oracle.c, "
+                                               f"{oracle_lib.FAST_BUILD})"}
             except Exception as e:
                 log(f"c3 cpu baseline failed: {e}")
         res[name] = r
@@ -428,16 +470,15 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
                       "algorithmic_bytes_per_launch": per_tile * B, "avg_launch_ms": round(k2, 5)}}
     if with_cpu:
         try:
-            sys.path.insert(0, os.path.join(REPO, "tests"))
-            import oracle_lib
+            oracle_lib = _oracle()
             tiles = [[np.ascontiguousarray(be_host[t, c]) for c in range(3)] for t in range(uniq)]
 
             def one(i):
-                oracle_lib.render(chans, tiles[i % uniq], _lib.PIXELS_FLOAT, TILE, TILE, big_endian=True)
+                oracle_lib.render(chans, tiles[i % uniq], _lib.PIXELS_FLOAT, TILE, TILE, big_endian=True, fast=True)
             n, secs = _cpu_pool(one, cpu_seconds, threads)
             r["cpu_baseline"] = {"value": round(n / secs, 3), "unit": "tiles/s", "cores": threads, "kind": "port",
                                  "sample": f"{n} C5 tiles (3ch f32 1024^2, log/poly/lut/reverse) in {secs:.2f} s "
-                                           f"on {threads} threads (oracle/omr_oracle.c, -O3)"}
+                                           f"on {threads} threads (oracle/omr_oracle.c, {oracle_lib.FAST_BUILD})"}
         except Exception as e:
             log(f"c5 cpu baseline failed: {e}")
     # render_shape_mask: 1024x1024 mask of random ellipses, FF000080, flip hv (host API, p50)
@@ -629,6 +670,50 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
     return res
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes (RANK/LOCAL_RANK/
+    WORLD_SIZE/MASTER_* as torch.distributed.run sets them) and wait for them.  Called before
+    this process touches the GPU (it never imports torch); only rank 0 prints the JSON line.
+    Returns the exit code (first failing rank's, after the others are stopped)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    import threading
+    procs, pumps = [], []
+
+    def pump(stream):       # the JSON line to stdout; anything else a rank prints (gloo banners) to stderr
+        for line in iter(stream.readline, ""):
+            (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+            (sys.stdout if line.startswith("{") else sys.stderr).flush()
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        p = subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             stdout=subprocess.PIPE, text=True)
+        procs.append(p)
+        pumps.append(threading.Thread(target=pump, args=(p.stdout,), daemon=True))
+        pumps[-1].start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:          # a rank failed: stop the others (our own children)
+                    q.terminate()
+        time.sleep(0.05)
+    for t in pumps:
+        t.join(timeout=5)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -650,25 +735,43 @@ def main():
                     help="skip the C3 (projection) and C5 (float32 families, shape mask) sections")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-tile latency probe (profiling runs: batch launches only)")
+    ap.add_argument("--prewarm-ms", type=float, default=300.0,
+                    help="untimed device warm-up before the W warm-up steps: the first ~25 K2 launches "
+                         "after idle run 0.77 -> 0.60 ms while the GPU clocks ramp (profiles/r02/"
+                         "k2_series_*.json); 0 disables")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     import torch
-    torch.cuda.set_device(local_rank)
+    n_dev = torch.cuda.device_count()
+    if n_dev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    dev_index = local_rank % n_dev          # more ranks than GPUs (a rehearsal): ranks share cards
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     dist = None
+    backend = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        # RCCL needs one rank per GPU; ranks sharing a card meet over gloo (the only traffic is
+        # the timing barrier and one max-reduction: no collective touches pixel data)
+        backend = "nccl" if local_world <= n_dev else "gloo"
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     import omr
     from omr import _lib
     from omr.context import make_bindings, make_qdef
     from omr.synthetic import c2_channels
 
-    ctx = omr.Context(local_rank)
+    ctx = omr.Context(dev_index)
     qdef = make_qdef("rgb")
     chans = c2_channels(CHANNELS)
     bindings = make_bindings(chans)
@@ -692,30 +795,58 @@ def main():
             ctx.render_batch_device(qdef, chans, table, B, _lib.PIXELS_UINT16, TILE, TILE, out,
                                     big_endian=True, bindings=bindings)
 
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    # Device warm-up: the GPU leaves its idle clock state over the first ~15 ms of load (K2
+    # launches after idle: 0.77, 0.74, 0.72, ... 0.60 ms, then 0.55 sustained; tools/k2_series.py).
+    # A serving node under load runs at the sustained clocks, so the bench reaches them first:
+    # back-to-back steps for --prewarm-ms, untimed, then the W warm-up steps, then the K timed steps.
+    n_pre = 0
+    if args.prewarm_ms > 0:
+        t_end = time.perf_counter() + args.prewarm_ms / 1e3
+        while time.perf_counter() < t_end:
+            step()
+            n_pre += 1
+            if n_pre % 4 == 0:
+                ctx.synchronize()
+        ctx.synchronize()
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
-    ctx.kernel_timings()
 
-    ctx.enable_kernel_timing(True)
-    if dist:
-        dist.barrier()
+    # Timed region: K steps, kernel timing OFF (no per-launch event records).  Two HIP events on
+    # the context's stream bracket the region as a device-side cross-check of the wall clock.
+    ext = torch.cuda.ExternalStream(ctx.stream, device=device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(ext)
+    for _ in range(args.steps):
+        step()
+    ev1.record(ext)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    region_ms = ev0.elapsed_time(ev1)
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # Second pass, same K steps, kernel timing ON: per-launch K2 durations (HIP events around
+    # each K2 launch on its stream) for the roofline.
+    ctx.kernel_timings()
+    ctx.enable_kernel_timing(True)
     for _ in range(args.steps):
         step()
     ctx.synchronize()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
     ctx.enable_kernel_timing(False)
-    k2 = [ms for ms, kind in ctx.kernel_timings() if kind == 2]
-
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    k2 = sorted(ms for ms, kind in ctx.kernel_timings() if kind == 2)
 
     tiles = (args.total_tiles or world * B) * args.steps
     value = tiles / elapsed
@@ -725,9 +856,9 @@ def main():
 
     extra = {}
     if rank == 0 and world == 1:
+        threads, _, _ = host_cores()
         if not args.no_latency:
             extra["p50_tile_latency_ms"] = latencies(torch, omr, ctx, qdef, chans, data)
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         if not args.no_jpeg:
             extra["jpeg"] = jpeg_section(torch, ctx, data, min(args.jpeg_batch, B), args.jpeg_steps,
                                          2, args.cpu_seconds / 2, threads, not args.no_cpu_baseline)
@@ -785,6 +916,10 @@ def main():
                 "colors": "0000FF,00FF00,FF0000,FFFFFF",
                 "parallelism": f"dp{world} (independent tile batches per GPU, no collectives)",
                 "batch_descriptor": args.addr,
+                "ranks": world,
+                "devices_visible": n_dev,
+                "ranks_share_devices": world > n_dev,
+                "control_backend": backend,
             },
             "roofline": {
                 "bound": "hbm",
@@ -796,9 +931,18 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": BYTES_PER_TILE * B,
                 "avg_launch_ms": round(k2_ms, 5),
+                "min_launch_ms": round(k2[0], 5) if k2 else None,
+                "median_launch_ms": round(k2[len(k2) // 2], 5) if k2 else None,
+                "max_launch_ms": round(k2[-1], 5) if k2 else None,
                 "launches": len(k2),
+                "timing": "second pass of the same K steps with per-launch HIP events on the "
+                          "K2 stream; the throughput pass runs with kernel timing off",
+                "region_event_ms_per_step": round(region_ms / args.steps, 5),
             },
             "hbm_gbs": round(achieved, 1),
+            "prewarm": {"ms": args.prewarm_ms, "steps": n_pre,
+                        "why": "untimed, before the W warm-up steps: GPU clock ramp out of idle "
+                               "(first ~25 K2 launches 0.77 -> 0.60 ms vs 0.55 sustained)"},
         }
         line.update(extra)
         if "cpu_baseline" not in line:

@@ -127,6 +127,34 @@ int32_t     omr_ctx_kernel_timings(omr_ctx* ctx, float* ms_out, int32_t* kind_ou
 void*       omr_pinned_alloc(omr_ctx* ctx, size_t bytes);
 void        omr_pinned_free(omr_ctx* ctx, void* p);
 
+/*
+ * Un-vendored upstream semantics.  The quantization, compositing and
+ * JPEG-table arithmetic lives in omero:server 5.4.10 jars that are absent here, so every choice
+ * that could not be pinned is a named switch; 0 (all off) is the restatement the repo defaults
+ * to (DESIGN.md §2 gives the reasoning per switch).  The CPU restatement (oracle/) implements the
+ * same switches, and the GPU tests cover each one against it.
+ */
+enum {
+    /* Quantization_8_16_bit LUT window ends as Java (int) casts of the double window
+     * (x < (int)start -> cdStart, x >= (int)end -> cdEnd) instead of double compares
+     * (x < start, x >= end).  Integer pixel types (the LUT path) only. */
+    OMR_SEM_WINDOW_INT_BOUNDS = 1u << 0,
+    /* Channel colour scaling in two truncating steps, colour then alpha,
+     * (int)((int)(c/255f * v) * (a/255f)), instead of (int)((c/255f * a/255f) * v).  (The
+     * one-step order (int)((c/255f * v) * (a/255f)) needs no switch: it equals the default for
+     * every c, a, v in 0..255, tests/test_semantics.py.) */
+    OMR_SEM_ALPHA_SEPARATE = 1u << 1,
+    /* Greyscale model: a .lut channel renders (R[v],G[v],B[v]) instead of ignoring the LUT. */
+    OMR_SEM_GREYSCALE_LUT = 1u << 2,
+    /* JPEG chroma base table K2Div2Chrominance (Annex K chroma halved, JPEGQTable) scaled by the
+     * quality instead of K2Chrominance. */
+    OMR_SEM_JPEG_CHROMA_DIV2 = 1u << 3,
+    OMR_SEM_ALL = 0xFu
+};
+/* Semantics of every later call on this context (renders, projections' renders, JPEG). */
+omr_status omr_ctx_set_semantics(omr_ctx* ctx, uint32_t flags);
+uint32_t   omr_ctx_get_semantics(const omr_ctx* ctx);
+
 /* ---- pixel buffer: ROMIO repository file -> pinned staging -> HBM ---------- */
 /*
  * Replaces pixelsService.getPixelBuffer(pixels, false) (ImageRegionRequestHandler.java:302-309)
@@ -199,6 +227,8 @@ omr_status omr_batcher_submit(omr_batcher* b, const omr_tile_job* job, uint64_t*
 omr_status omr_batcher_wait(omr_batcher* b, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
 /* jobs submitted, dispatch rounds, tiles rendered, duplicate tiles served from a sibling job */
 omr_status omr_batcher_stats(omr_batcher* b, uint64_t stats_out[4]);
+/* OMR_SEM_* flags of the batcher's context (call before submitting). */
+omr_status omr_batcher_set_semantics(omr_batcher* b, uint32_t flags);
 
 /* ---- render (quantize + codomain + composite + flip) ------------------ */
 /*
@@ -331,6 +361,8 @@ omr_status omr_encode_jpeg_batch(omr_ctx* ctx, const uint32_t* d_argb, int64_t t
                                  uint8_t* out, size_t cap, uint64_t* offsets, uint32_t* lengths);
 /* Java ImageIO quality -> quantisation tables (natural order), JPEGQTable.getScaledInstance. */
 omr_status omr_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]);
+/* Same under OMR_SEM_* flags (OMR_SEM_JPEG_CHROMA_DIV2 selects the chroma base table). */
+omr_status omr_jpeg_quant_tables_sem(float quality, uint32_t semantics, uint8_t luma[64], uint8_t chroma[64]);
 
 /* PNG RGB8 of ARGB pixels (ImageIO.write(image, "png"), ImageRegionRequestHandler.java:598). */
 omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int32_t height,

@@ -62,6 +62,7 @@ struct omr_batcher {
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
     int32_t* d_stat = nullptr;
+    int32_t* d_rstat = nullptr;    // per-tile render status (QuantizationException per tile)
     int meta_cap = 0;
 };
 
@@ -114,6 +115,8 @@ static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
         if (B->d_offs) OMR_HIP(c, hipFree(B->d_offs));
         if (B->d_lens) OMR_HIP(c, hipFree(B->d_lens));
         if (B->d_stat) OMR_HIP(c, hipFree(B->d_stat));
+        if (B->d_rstat) OMR_HIP(c, hipFree(B->d_rstat));
+        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_rstat), sizeof(int32_t) * n));
         OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_offs), sizeof(uint64_t) * n));
         OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_lens), sizeof(uint32_t) * n));
         OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_stat), sizeof(int32_t) * n));
@@ -123,7 +126,9 @@ static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
 }
 
 // Render + encode one group (same image, settings, size, flip, format).  jobs[u] are the
-// distinct tiles; out[u] receives each one's bytes.
+// distinct tiles; out[u] receives each one's bytes, or OMR_QUANTIZATION for a tile with a pixel
+// outside the LUT domain — only that tile fails, as only that request's Renderer would throw
+// in the reference (one Renderer per request, ImageRegionRequestHandler.java:436-440, :479-480).
 static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
     omr_ctx* c = B->ctx;
     const Job& j0 = *jobs[0];
@@ -135,10 +140,18 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
     const size_t jcap = (size_t)n * (px * 4 + 65536);
     omr_status st = grow_dev(B, px * 4 * n, j0.spec.format == OMR_FORMAT_JPEG ? jcap : 0, n);
     if (st) return st;
-    st = omr_render_pixel_buffer_tiles(c, j0.pb, &j0.qdef, j0.ch.data(), (int32_t)j0.ch.size(), reqs.data(), n, W, H,
-                                       j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1);
+    st = render_pixel_buffer_tiles(c, j0.pb, &j0.qdef, j0.ch.data(), (int32_t)j0.ch.size(), reqs.data(), n, W, H,
+                                   j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1, B->d_rstat);
     if (st) return st;
     out.assign(n, Result{});
+    std::vector<int32_t> rstat(n);
+    OMR_HIP(c, hipMemcpyAsync(rstat.data(), B->d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    OMR_HIP(c, hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i)
+        if (rstat[i]) {
+            out[i].st = rstat[i];
+            out[i].err = "pixel value outside the quantization LUT domain";
+        }
     if (j0.spec.format == OMR_FORMAT_JPEG) {
         st = omr_encode_jpeg_batch_device(c, B->d_argb, 0, n, W, H, j0.spec.quality, B->d_jpeg, jcap, B->d_offs,
                                           B->d_lens, B->d_stat);
@@ -155,10 +168,12 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
         }
         std::vector<uint8_t> all(used);
         OMR_HIP(c, hipMemcpy(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost));
-        for (int i = 0; i < n; ++i) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
+        for (int i = 0; i < n; ++i)
+            if (!out[i].st) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
     } else if (j0.spec.format == OMR_FORMAT_PNG) {
         std::vector<uint8_t> buf(omr_png_max_bytes(W, H, 3));
         for (int i = 0; i < n; ++i) {
+            if (out[i].st) continue;
             size_t len = 0;
             st = omr_encode_png_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
             if (st) return st;
@@ -167,7 +182,8 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
     } else {                                               // OMR_FORMAT_ARGB: the packed int[] itself
         std::vector<uint8_t> all(px * 4 * n);
         OMR_HIP(c, hipMemcpy(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost));
-        for (int i = 0; i < n; ++i) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
+        for (int i = 0; i < n; ++i)
+            if (!out[i].st) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
     }
     return OMR_OK;
 }
@@ -221,6 +237,7 @@ static void dispatch_loop(omr_batcher* B) {
             for (size_t i = 0; i < g.second.size(); ++i) {
                 Result r;
                 if (st) { r.st = st; r.err = err; }
+                else if (out[slot[i]].st) { r.st = out[slot[i]].st; r.err = out[slot[i]].err; }
                 else r.bytes = out[slot[i]].bytes;
                 results.emplace_back(g.second[i]->ticket, std::move(r));
             }
@@ -266,7 +283,8 @@ void omr_batcher_destroy(omr_batcher* B) {
     B->cv_in.notify_all();
     if (B->th.joinable()) B->th.join();
     (void)hipSetDevice(B->device);
-    for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat})
+    for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat,
+                    (void*)B->d_rstat})
         if (p) (void)hipFree(p);
     omr_ctx_destroy(B->ctx);
     delete B;
@@ -319,6 +337,12 @@ omr_status omr_batcher_wait(omr_batcher* B, uint64_t ticket, uint8_t* out, size_
     std::memcpy(out, r.bytes.data(), r.bytes.size());
     B->done.erase(ticket);
     return OMR_OK;
+}
+
+omr_status omr_batcher_set_semantics(omr_batcher* B, uint32_t flags) {
+    if (!B) return OMR_INVALID_ARGUMENT;
+    std::lock_guard<std::mutex> g(B->m);   // the dispatcher reads it between rounds
+    return omr_ctx_set_semantics(B->ctx, flags);
 }
 
 omr_status omr_batcher_stats(omr_batcher* B, uint64_t stats_out[4]) {

@@ -6,6 +6,7 @@
 #include "omr_internal.h"
 
 #include <cstdio>
+#include <cstdlib>
 
 namespace omr {
 
@@ -134,6 +135,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
         return e == hipErrorOutOfMemory ? OMR_OOM : OMR_DEVICE;
     }
     c->stream = c->own_stream;
+    if (const char* v = std::getenv("OMR_K2_NT_STORE")) c->k2_nt_store = std::atoi(v) != 0;
     *out = c;
     return OMR_OK;
 }
@@ -201,6 +203,15 @@ omr_status omr_ctx_set_stream(omr_ctx* c, void* s) {
     c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
     return OMR_OK;
 }
+
+omr_status omr_ctx_set_semantics(omr_ctx* c, uint32_t flags) {
+    if (!c) return OMR_INVALID_ARGUMENT;
+    if (flags & ~(uint32_t)OMR_SEM_ALL) return fail(c, OMR_INVALID_ARGUMENT, "unknown semantics flag");
+    c->sem = flags;
+    return OMR_OK;
+}
+
+uint32_t omr_ctx_get_semantics(const omr_ctx* c) { return c ? c->sem : 0u; }
 
 void* omr_ctx_get_stream(omr_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 

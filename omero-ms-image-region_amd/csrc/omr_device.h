@@ -28,10 +28,13 @@ __device__ __forceinline__ double family_map(int family, double x, double k) {
     }
 }
 
-// q(x): window, noise reduction, family map, two rounding stages (S3/S4).
+// q(x) of an integer pixel (the LUT types): window, noise reduction, family map, two rounding
+// stages (S3/S4).  The window ends are the integer thresholds p.lo / p.hi the host derived from
+// the double window under the OMR_SEM_WINDOW_INT_BOUNDS choice (x < ws <=> x < ceil(ws) for
+// integer x by default; x < (int)ws with the switch).
 __device__ __forceinline__ int quantize_eval(double x, const ChanParam& p, int cds, int cde) {
-    if (x < p.ws) return cds & 0xFF;
-    if (x >= p.we) return cde & 0xFF;
+    if (x < (double)p.lo) return cds & 0xFF;
+    if (x >= (double)p.hi) return cde & 0xFF;
     if (p.nr) {
         if (x < p.ws + p.dec) return cds & 0xFF;
         if (x >= p.we - p.dec) return cde & 0xFF;

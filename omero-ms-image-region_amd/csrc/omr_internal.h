@@ -15,6 +15,8 @@
 
 #include "omr/omr.h"
 
+struct omr_ctx;
+
 namespace omr {
 
 constexpr int kMaxActive = 32;        // active channels per render call
@@ -45,6 +47,8 @@ struct ChanParam {
     double ys, a0, a1;  // f(ws), bitRes/(f(we)-f(ws)), (cdEnd-cdStart)/bitRes
     double dec;         // noise-reduction decile width
     float ratio[3];     // (c/255f)*(alpha/255f)
+    float alpha;        // alpha/255f (OMR_SEM_ALPHA_SEPARATE)
+    float cratio[3];    // c/255f     (OMR_SEM_ALPHA_SEPARATE)
     float pad1;
     uint64_t lut_off;   // byte offset of this channel's quantization LUT in the workspace
     uint8_t lut_rgb[768];  // LutReader colours (valid when has_lut)
@@ -54,6 +58,8 @@ struct RenderPlan {
     int32_t n_active;
     int32_t cd_start, cd_end;
     int32_t greyscale;
+    uint32_t sem;       // OMR_SEM_* flags
+    int32_t pad[3];
     ChanParam ch[kMaxActive];
 };
 
@@ -79,6 +85,8 @@ struct Ctx {
     hipEvent_t pin_ev[kPinSlots] = {};
     int pin_slot = 0;
     int cu_count = 256;
+    bool k2_nt_store = true;
+    uint32_t sem = 0;            // OMR_SEM_* (omr_ctx_set_semantics)     // env OMR_K2_NT_STORE=0: plain ARGB stores (measurement switch)
     // kernel timing (omr_ctx_enable_kernel_timing)
     bool timing = false;
     struct Timed { hipEvent_t start, stop; int kind; };
@@ -123,6 +131,14 @@ omr_status enqueue_projection(Ctx* c, const void* const* d_stacks, void* const* 
                               int32_t pixel_type, int32_t be_in, int32_t size_x, int32_t size_y,
                               int32_t algorithm, int32_t start, int32_t end, int32_t stepping,
                               int32_t be_out);
+
+// omr_render_pixel_buffer_tiles with optional per-tile statuses (device int32[n], OMR_OK /
+// OMR_QUANTIZATION): then a QuantizationException fails only the tiles it hit (omr_pixbuf.cpp).
+omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, const omr_quantum_def* qdef,
+                                     const omr_channel_binding* channels, int32_t size_c,
+                                     const omr_tile_request* reqs, int32_t n, int32_t width, int32_t height,
+                                     int32_t flip_h, int32_t flip_v, uint32_t* argb_out, int32_t out_on_device,
+                                     int32_t* d_status);
 
 #define OMR_HIP(ctx, expr)                                          \
     do {                                                            \

@@ -100,20 +100,26 @@ struct QTabs {
     uint16_t q[2][64];  // natural order
 };
 
-// javax.imageio JPEG.convertToLinearQuality + JPEGQTable.getScaledInstance(scale, true).
-static void quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]) {
+// JPEGQTable.getScaledInstance(scale, forceBaseline=true): (int)(q*scale + 0.5f) in [1, 255].
+static int scale_entry(int q, float scale) {
+    volatile float a = (float)q * scale;      // one float multiply, then the add (no contraction)
+    const int sv = (int)(a + 0.5f);
+    return sv < 1 ? 1 : sv > 255 ? 255 : sv;
+}
+
+// javax.imageio JPEG.convertToLinearQuality + JPEGQTable.getScaledInstance(scale, true) of the
+// Annex K luminance table and, by OMR_SEM_JPEG_CHROMA_DIV2, of K2Chrominance (default) or
+// K2Div2Chrominance (= K2Chrominance.getScaledInstance(0.5f, true)).
+static void quant_tables(float quality, uint32_t sem, uint8_t luma[64], uint8_t chroma[64]) {
     float qf = quality;
     if (qf <= 0.0f) qf = 0.01f;
     if (qf > 1.00f) qf = 1.00f;
     if (qf < 0.5f) qf = 0.5f / qf;
     else qf = 2.0f - (qf * 2.0f);
     for (int i = 0; i < 64; ++i) {
-        volatile float a = (float)kStdLuma[i] * qf;
-        int sv = (int)(a + 0.5f);
-        luma[i] = (uint8_t)(sv < 1 ? 1 : sv > 255 ? 255 : sv);
-        volatile float b = (float)kStdChroma[i] * qf;
-        sv = (int)(b + 0.5f);
-        chroma[i] = (uint8_t)(sv < 1 ? 1 : sv > 255 ? 255 : sv);
+        luma[i] = (uint8_t)scale_entry(kStdLuma[i], qf);
+        const int cbase = (sem & OMR_SEM_JPEG_CHROMA_DIV2) ? scale_entry(kStdChroma[i], 0.5f) : kStdChroma[i];
+        chroma[i] = (uint8_t)scale_entry(cbase, qf);
     }
 }
 
@@ -510,7 +516,7 @@ static JpegLayout jpeg_layout(int W, int H, size_t base) {
 static omr_status encode_jpeg_ws(Ctx* ctx, const uint32_t* d_argb, int W, int H, float quality, uint8_t* out,
                                  size_t cap, size_t* out_len, const JpegLayout& L) {
     uint8_t ql[64], qc[64];
-    quant_tables(quality, ql, qc);
+    quant_tables(quality, ctx->sem, ql, qc);
     std::vector<uint8_t> hdr;
     jpeg_header(hdr, W, H, ql, qc);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
@@ -591,8 +597,12 @@ size_t omr_jpeg_max_bytes(int32_t width, int32_t height) {
 }
 
 omr_status omr_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]) {
+    return omr_jpeg_quant_tables_sem(quality, 0, luma, chroma);
+}
+
+omr_status omr_jpeg_quant_tables_sem(float quality, uint32_t semantics, uint8_t luma[64], uint8_t chroma[64]) {
     if (!luma || !chroma) return OMR_INVALID_ARGUMENT;
-    quant_tables(quality, luma, chroma);
+    quant_tables(quality, semantics, luma, chroma);
     return OMR_OK;
 }
 
@@ -1339,7 +1349,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
                                        int H, float quality, uint8_t* d_out, uint64_t cap, uint64_t* d_offsets,
                                        uint32_t* d_lengths, int32_t* d_status, const JpegBatchLayout& L) {
     uint8_t ql[64], qc[64];
-    quant_tables(quality, ql, qc);
+    quant_tables(quality, ctx->sem, ql, qc);
     std::vector<uint8_t> hdr;
     jpeg_header(hdr, W, H, ql, qc);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);

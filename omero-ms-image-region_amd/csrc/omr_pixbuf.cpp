@@ -30,9 +30,13 @@ struct omr_pixel_buffer {
     int fd = -1;
     int32_t sx = 0, sy = 0, sz = 0, sc = 0, st = 0, pt = 0, bpp = 0;
     int64_t row_bytes = 0, plane_bytes = 0, total = 0;
-    // Read-only shared mapping of the file: getTile copies rows out of the page cache, and once
+    // Read-only shared mapping of the file, only for files up to kMaxRegisterBytes: once
     // registered with HIP (hipHostRegister, first pipelined render) the copy engines read tile
-    // rows straight from it — no CPU copy at all.
+    // rows straight from it — no CPU copy at all.  Registration pins every page of the mapping
+    // while the buffer is open, hence the cap; larger files (and getTile) use pread, which turns a
+    // file truncated underneath us into an I/O error (the reference's IOException) rather than
+    // a SIGBUS from a mapped read.  Requirement: a registered file is not truncated while open
+    // (its pages stay pinned; the DMA then reads the old contents).
     const uint8_t* map = nullptr;
     std::mutex reg_m;
     int reg_state = 0;   // 0 untried, 1 registered, -1 not registrable (pread/memcpy path)
@@ -41,6 +45,11 @@ struct omr_pixel_buffer {
 namespace omr {
 
 // Fixed pool of reader threads (one per context, created on first use).
+// run() hands out the indices of one generation through a single 64-bit ticket
+// (generation << 32 | next index): a worker claims an index with a compare-and-swap that fails
+// once the generation has moved on, so a straggler of generation k can never take (and run a
+// second time) an index of generation k+1.  Exactly n claims succeed per generation, done_
+// counts exactly n, and run() returns only after every claimed job of its generation finished.
 class ReadPool {
 public:
     explicit ReadPool(int n) {
@@ -55,17 +64,20 @@ public:
         for (auto& t : th_) t.join();
     }
     // Runs job(i) for i in [0, n) on the pool and the calling thread; returns when all are done.
+    // One caller at a time (the owning context's thread).
     void run(int n, const std::function<void(int)>& job) {
+        if (n <= 0) return;
+        uint32_t gen;
         {
             std::lock_guard<std::mutex> g(m_);
+            gen = ++gen_;
             job_ = &job;
             n_ = n;
-            next_.store(0);
             done_ = 0;
-            ++gen_;
+            ticket_.store((uint64_t)gen << 32);
         }
         cv_.notify_all();
-        work();
+        work(gen, n, &job);
         std::unique_lock<std::mutex> lk(m_);
         done_cv_.wait(lk, [&] { return done_ == n_; });
         job_ = nullptr;
@@ -73,34 +85,45 @@ public:
     int size() const { return (int)th_.size(); }
 
 private:
-    void work() {
+    void work(uint32_t gen, int n, const std::function<void(int)>* job) {
         for (;;) {
-            const int i = next_.fetch_add(1);
-            if (i >= n_) return;
-            (*job_)(i);
+            uint64_t t = ticket_.load();
+            int i;
+            for (;;) {
+                if ((uint32_t)(t >> 32) != gen) return;          // generation over
+                i = (int)(uint32_t)t;
+                if (i >= n) return;
+                if (ticket_.compare_exchange_weak(t, t + 1)) break;
+            }
+            (*job)(i);
             std::lock_guard<std::mutex> g(m_);
             if (++done_ == n_) done_cv_.notify_all();
         }
     }
     void loop() {
-        uint64_t seen = 0;
+        uint32_t seen = 0;
         for (;;) {
+            uint32_t gen;
+            int n;
+            const std::function<void(int)>* job;
             {
                 std::unique_lock<std::mutex> lk(m_);
                 cv_.wait(lk, [&] { return stop_ || (gen_ != seen && job_); });
                 if (stop_) return;
-                seen = gen_;
+                seen = gen = gen_;
+                n = n_;
+                job = job_;
             }
-            work();
+            work(gen, n, job);
         }
     }
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(int)>* job_ = nullptr;
-    std::atomic<int> next_{0};
+    std::atomic<uint64_t> ticket_{0};
     int n_ = 0, done_ = 0;
-    uint64_t gen_ = 0;
+    uint32_t gen_ = 0;
     bool stop_ = false;
 };
 
@@ -204,15 +227,14 @@ static int64_t plane_offset(const omr_pixel_buffer* pb, int32_t z, int32_t c, in
     return (((int64_t)t * pb->sc + c) * pb->sz + z) * pb->plane_bytes;
 }
 
-// Rows y..y+h of the plane, columns x..x+w, packed into dst.
+// Files above this size are never mapped or registered (see omr_pixel_buffer::map).
+constexpr int64_t kMaxRegisterBytes = (int64_t)1 << 30;
+
+// Rows y..y+h of the plane, columns x..x+w, packed into dst (pread: see omr_pixel_buffer::map).
 static bool read_tile(const omr_pixel_buffer* pb, int32_t z, int32_t c, int32_t t, int32_t x, int32_t y, int32_t w,
                       int32_t h, uint8_t* dst) {
     const int64_t base = plane_offset(pb, z, c, t) + (int64_t)y * pb->row_bytes + (int64_t)x * pb->bpp;
     const size_t seg = (size_t)w * pb->bpp;
-    if (pb->map) {
-        for (int32_t r = 0; r < h; ++r) std::memcpy(dst + seg * r, pb->map + base + (int64_t)r * pb->row_bytes, seg);
-        return true;
-    }
     if (w == pb->sx) return read_full(pb->fd, dst, seg * (size_t)h, base);   // one contiguous band
     for (int32_t r = 0; r < h; ++r)
         if (!read_full(pb->fd, dst + seg * r, seg, base + (int64_t)r * pb->row_bytes)) return false;
@@ -262,8 +284,10 @@ omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_
         delete pb;
         return OMR_INVALID_ARGUMENT;
     }
-    void* m = ::mmap(nullptr, (size_t)pb->total, PROT_READ, MAP_SHARED, fd, 0);
-    if (m != MAP_FAILED) pb->map = static_cast<const uint8_t*>(m);
+    if (pb->total <= kMaxRegisterBytes) {
+        void* m = ::mmap(nullptr, (size_t)pb->total, PROT_READ, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) pb->map = static_cast<const uint8_t*>(m);
+    }
     *out = pb;
     return OMR_OK;
 }
@@ -297,10 +321,15 @@ omr_status omr_ctx_set_pixel_buffer_dma(omr_ctx* ctx, int32_t enable) {
     return OMR_OK;
 }
 
-omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, const omr_quantum_def* qdef,
-                                         const omr_channel_binding* channels, int32_t size_c,
-                                         const omr_tile_request* reqs, int32_t n, int32_t width, int32_t height,
-                                         int32_t flip_h, int32_t flip_v, uint32_t* argb_out, int32_t out_on_device) {
+}  // extern "C"
+
+namespace omr {
+
+omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, const omr_quantum_def* qdef,
+                                     const omr_channel_binding* channels, int32_t size_c,
+                                     const omr_tile_request* reqs, int32_t n, int32_t width, int32_t height,
+                                     int32_t flip_h, int32_t flip_v, uint32_t* argb_out, int32_t out_on_device,
+                                     int32_t* d_status) {
     if (!ctx) return OMR_INVALID_ARGUMENT;
     if (!pb || !qdef || !channels || !reqs || !argb_out || n < 0) return fail(ctx, OMR_INVALID_ARGUMENT, "null argument");
     if (size_c != pb->sc) return fail(ctx, OMR_INVALID_ARGUMENT, "channel bindings do not match the pixel buffer's sizeC");
@@ -395,7 +424,8 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
         OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d[s], 0));
         uint32_t* dout = out_on_device ? argb_out + (size_t)t0 * width * height : static_cast<uint32_t*>(P->d_out[s]);
         st = omr_render_batch_device(ctx, qdef, channels, size_c, reinterpret_cast<const void* const*>(din), cnt, 0,
-                                     pb->pt, 1, width, height, flip_h, flip_v, dout, nullptr);
+                                     pb->pt, 1, width, height, flip_h, flip_v, dout,
+                                     d_status ? d_status + t0 : nullptr);
         if (st) return st;
         OMR_HIP(ctx, hipEventRecord(P->rend[s], ctx->stream));
         if (host_out) {
@@ -413,7 +443,19 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
         st = finish_host(ngroups - 1);
         if (st) return st;
     }
-    return omr_ctx_synchronize(ctx);
+    st = omr_ctx_synchronize(ctx);
+    // with per-tile statuses the QuantizationException belongs to the flagged tiles only
+    if (st == OMR_QUANTIZATION && d_status) st = OMR_OK;
+    return st;
 }
 
-}  // extern "C"
+}  // namespace omr
+
+extern "C" omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb,
+                                                    const omr_quantum_def* qdef, const omr_channel_binding* channels,
+                                                    int32_t size_c, const omr_tile_request* reqs, int32_t n,
+                                                    int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                                                    uint32_t* argb_out, int32_t out_on_device) {
+    return omr::render_pixel_buffer_tiles(ctx, pb, qdef, channels, size_c, reqs, n, width, height, flip_h, flip_v,
+                                          argb_out, out_on_device, nullptr);
+}

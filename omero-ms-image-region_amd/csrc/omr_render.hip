@@ -21,12 +21,17 @@
 namespace omr {
 
 // ------------------------------------------------------------------------------- K1
-__device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey) {
+__device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey, uint32_t sem) {
     const int vv = p.reverse ? ((cde - v + cds) & 0xFF) : v;
-    if (grey) return ((uint32_t)vv << 20) | ((uint32_t)vv << 10) | (uint32_t)vv;
+    if (grey && !(p.has_lut && (sem & OMR_SEM_GREYSCALE_LUT)))
+        return ((uint32_t)vv << 20) | ((uint32_t)vv << 10) | (uint32_t)vv;
     uint32_t r, g, b;
     if (p.has_lut) {
         r = p.lut_rgb[vv]; g = p.lut_rgb[256 + vv]; b = p.lut_rgb[512 + vv];
+    } else if (sem & OMR_SEM_ALPHA_SEPARATE) {
+        r = (uint32_t)(int)((float)(int)(p.cratio[0] * (float)vv) * p.alpha);
+        g = (uint32_t)(int)((float)(int)(p.cratio[1] * (float)vv) * p.alpha);
+        b = (uint32_t)(int)((float)(int)(p.cratio[2] * (float)vv) * p.alpha);
     } else {
         r = (uint32_t)(int)(p.ratio[0] * (float)vv);
         g = (uint32_t)(int)(p.ratio[1] * (float)vv);
@@ -82,9 +87,9 @@ __device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__
         const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
         if (value < p.gmin || value > p.gmax) return kErrBit;
         const int v = quantize_eval((double)value, p, cds, cde);
-        return pack_contrib(p, v, cds, cde, plan->greyscale);
+        return pack_contrib(p, v, cds, cde, plan->greyscale, plan->sem);
     }
-    return pack_contrib(p, t, cds, cde, plan->greyscale);
+    return pack_contrib(p, t, cds, cde, plan->greyscale, plan->sem);
 }
 
 // grid: n_active blocks x 256 threads.
@@ -140,6 +145,7 @@ struct K2Args {
     int32_t flip_h, flip_v;
     int32_t n_active, cd_start, cd_end, cds8, cde8;
     int32_t tile_uniform;       // every block lies inside one tile (chunks per tile % block chunks == 0)
+    int32_t nt_store;           // non-temporal ARGB stores (OMR_K2_NT_STORE=0 disables; measurement switch)
     uint32_t total;             // work items (chunks of VEC pixels)
     FastDiv cpt, cpr;           // chunks per tile, chunks per row
     K2Chan ch[kMaxActive];
@@ -572,7 +578,7 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
             for (int j = 0; j < VEC; j += 4)
             {
                 const u32x4 v = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
-                if (OMR_K2_NT && BPP * NL >= 4) __builtin_nontemporal_store(v, (OMR_GLOBAL u32x4*)(o + j));
+                if (OMR_K2_NT && BPP * NL >= 4 && A.nt_store) __builtin_nontemporal_store(v, (OMR_GLOBAL u32x4*)(o + j));
                 else *(OMR_GLOBAL u32x4*)(o + j) = v;
             }
         } else if constexpr (VEC == 2) {
@@ -623,6 +629,13 @@ static double host_family_map(int family, double x, double k) {
     }
 }
 
+static int32_t java_d2i_host(double v) {   // Java (int) of a double: NaN -> 0, saturating
+    if (v != v) return 0;
+    if (v >= 2147483647.0) return INT32_MAX;
+    if (v <= -2147483648.0) return INT32_MIN;
+    return (int32_t)v;
+}
+
 static int32_t ceil_to_i32(double v) {
     if (v != v) return INT32_MIN;
     const double c = ceil(v);
@@ -669,6 +682,7 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
     P.cd_start = q->cd_start;
     P.cd_end = q->cd_end;
     P.greyscale = q->model == OMR_MODEL_GREYSCALE;
+    P.sem = ctx->sem;
     int na = 0;
     size_t lut_off = 0;
     for (int c = 0; c < size_c; ++c) {
@@ -694,11 +708,20 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
         p.a1 = (double)(q->cd_end - q->cd_start) / (double)q->bit_resolution;
         p.dec = (p.we - p.ws) / 10.0;
         p.second = !(p.a1 == 1.0 && q->cd_start == 0);
-        p.lo = ceil_to_i32(p.ws);
-        p.hi = ceil_to_i32(p.we);
-        if (p.we != p.we) p.hi = INT32_MAX;
+        if (P.sem & OMR_SEM_WINDOW_INT_BOUNDS) {   // x < (int)ws, x >= (int)we (Java d2i)
+            p.lo = java_d2i_host(p.ws);
+            p.hi = java_d2i_host(p.we);
+        } else {                                   // x < ws <=> x < ceil(ws) for integer x
+            p.lo = ceil_to_i32(p.ws);
+            p.hi = ceil_to_i32(p.we);
+            if (p.we != p.we) p.hi = INT32_MAX;
+        }
         const float alpha = (float)b.rgba[3] / 255.0f;
-        for (int k = 0; k < 3; ++k) p.ratio[k] = ((float)b.rgba[k] / 255.0f) * alpha;
+        p.alpha = alpha;
+        for (int k = 0; k < 3; ++k) {
+            p.cratio[k] = (float)b.rgba[k] / 255.0f;
+            p.ratio[k] = p.cratio[k] * alpha;
+        }
         if (bpp <= 2) {
             const double gmin = std::trunc(b.global_min), gmax = std::trunc(b.global_max);
             if (!(gmin == gmin) || !(gmax == gmax) || gmax < gmin || gmin < -2147483648.0 || gmax > 2147483647.0)
@@ -819,6 +842,7 @@ static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int
 // and no integer x in the window with a0*(x - ws) == 0.49999999999999994 (Java's
 // Math.round special case, where floor(d + 0.5) would differ).
 static bool fast_linear_ok(const ChanParam& c, const RenderPlan& P) {
+    if (P.sem & OMR_SEM_WINDOW_INT_BOUNDS) return false;   // the window may start below ws: d < 0 wraps
     if (P.cd_start != 0 || P.cd_end != 255 || c.second || !(c.we > c.ws) || !(c.a0 > 0) || !std::isfinite(c.a0))
         return false;
     const double x0 = std::floor(c.ws + 0.5 / c.a0);
@@ -936,6 +960,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cde8 = pp.plan.cd_end & 0xFF;
     const int cpt_thread = (na >= 1 && na <= 4 && !small) ? kCPT : 1;
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
+    a.nt_store = ctx->k2_nt_store ? 1 : 0;
     a.total = (uint32_t)total;
     a.cpt = make_fastdiv((uint32_t)cpt);
     a.cpr = make_fastdiv((uint32_t)cpr);

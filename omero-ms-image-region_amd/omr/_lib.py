@@ -38,6 +38,9 @@ PIXELS_INT8, PIXELS_UINT8, PIXELS_INT16, PIXELS_UINT16, PIXELS_INT32, PIXELS_UIN
 FAMILY_LINEAR, FAMILY_POLYNOMIAL, FAMILY_LOGARITHMIC, FAMILY_EXPONENTIAL = range(4)
 MODEL_GREYSCALE, MODEL_RGB = 0, 1
 PROJECTION_MAX, PROJECTION_MEAN, PROJECTION_SUM = 0, 1, 2
+# OMR_SEM_* switches of the un-vendored upstream semantics (include/omr/omr.h)
+SEM_WINDOW_INT_BOUNDS, SEM_ALPHA_SEPARATE, SEM_GREYSCALE_LUT, SEM_JPEG_CHROMA_DIV2 = 1, 2, 4, 8
+SEM_ALL = 0xF
 
 PIXEL_TYPE_NAMES = {"int8": PIXELS_INT8, "uint8": PIXELS_UINT8, "int16": PIXELS_INT16,
                     "uint16": PIXELS_UINT16, "int32": PIXELS_INT32, "uint32": PIXELS_UINT32,
@@ -124,6 +127,8 @@ _SIGS = {
     "omr_ctx_synchronize": (_i32, [_vp]),
     "omr_ctx_set_stream": (_i32, [_vp, _vp]),
     "omr_ctx_get_stream": (_vp, [_vp]),
+    "omr_ctx_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
+    "omr_ctx_get_semantics": (ctypes.c_uint32, [_vp]),
     "omr_ctx_enable_kernel_timing": (_i32, [_vp, _i32]),
     "omr_ctx_kernel_timings": (_i32, [_vp, _vp, _vp, _i32]),
     "omr_pinned_alloc": (_vp, [_vp, _sz]),
@@ -138,6 +143,7 @@ _SIGS = {
     "omr_batcher_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
     "omr_batcher_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_batcher_stats": (_i32, [_vp, _vp]),
+    "omr_batcher_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
     "omr_render_pixel_buffer_tiles": (_i32, [_vp, _vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                              _i32]),
     "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
@@ -163,6 +169,7 @@ _SIGS = {
     "omr_encode_jpeg_batch_device": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
     "omr_encode_jpeg_batch": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp]),
     "omr_jpeg_quant_tables": (_i32, [_f32, _vp, _vp]),
+    "omr_jpeg_quant_tables_sem": (_i32, [_f32, ctypes.c_uint32, _vp, _vp]),
     "omr_tiff_max_bytes": (_sz, [_i32, _i32]),
     "omr_encode_tiff": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_encode_tiff_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),

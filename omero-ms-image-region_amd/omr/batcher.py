@@ -48,6 +48,10 @@ class Batcher:
         _lib.check(lib.omr_batcher_submit(self.h, ctypes.byref(job), ctypes.byref(ticket)))
         return ticket.value
 
+    def set_semantics(self, flags):
+        """OMR_SEM_* switches of the batcher's context (before submitting)."""
+        _lib.check(lib.omr_batcher_set_semantics(self.h, int(flags)))
+
     def wait(self, ticket, cap=1 << 22):
         n = ctypes.c_size_t(0)
         out = np.empty(cap, dtype=np.uint8)

@@ -62,6 +62,11 @@ def make_qdef(model, cd_start=0, cd_end=255, bit_resolution=255):
 
 
 class Context:
+    """One omr_ctx.  Its launches run on the context's own non-blocking HIP stream, which does
+    not order with torch's streams: call order_after_torch() before a call that reads tensors
+    torch has just written (or a caller-side synchronize), and keep tensors alive (or
+    record_stream them) until synchronize() when torch might reuse their memory."""
+
     def __init__(self, device=0):
         h = ctypes.c_void_p()
         st = lib.omr_ctx_create(int(device), ctypes.byref(h))
@@ -96,6 +101,22 @@ class Context:
 
     def synchronize(self):
         check(lib.omr_ctx_synchronize(self.h), self.h)
+
+    def order_after_torch(self):
+        """The context's stream waits for the work queued so far on torch's current stream."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        torch.cuda.ExternalStream(self.stream, device=dev).wait_event(ev)
+
+    def set_semantics(self, flags):
+        """OMR_SEM_* switches (omr._lib.SEM_*) for later calls on this context."""
+        check(lib.omr_ctx_set_semantics(self.h, int(flags)), self.h)
+
+    @property
+    def semantics(self):
+        return int(lib.omr_ctx_get_semantics(self.h))
 
     def enable_kernel_timing(self, enable=True):
         check(lib.omr_ctx_enable_kernel_timing(self.h, int(enable)), self.h)

@@ -41,6 +41,15 @@
  *          channel renders 0xFF000000.
  *   S9 [H] projection exactly as ProjectionService.java:176-291 (max over [start,end] from 0,
  *          mean/sum over [start,end), double sum, clamp to type max, Java narrowing store).
+ *   S10[M] JPEG tables: JPEG.convertToLinearQuality + JPEGQTable.getScaledInstance of the
+ *          Annex K luminance and chrominance tables.
+ *
+ * SWITCHES (oracle_set_semantics; the same OMR_SEM_* flags libomr.so takes per context, so a
+ * corrected upstream rule is a one-flag change in both):
+ *   OMR_SEM_WINDOW_INT_BOUNDS  S3 for LUT types: x < (int)start -> cdStart, x >= (int)end -> cdEnd.
+ *   OMR_SEM_ALPHA_SEPARATE     S7: (int)((int)(c/255f * v) * (alpha/255f)).
+ *   OMR_SEM_GREYSCALE_LUT      S8: a .lut channel in greyscale renders (R[v],G[v],B[v]).
+ *   OMR_SEM_JPEG_CHROMA_DIV2   S10: chroma base table K2Div2Chrominance = K2.getScaledInstance(0.5f).
  */
 #include "omr_oracle.h"
 
@@ -71,6 +80,11 @@ int64_t oracle_java_round(double a) {
     return java_d2l(floor(a + 0.5));
 }
 
+static uint32_t g_sem = 0;   /* OMR_SEM_* switches (set before use; not per thread) */
+
+void oracle_set_semantics(uint32_t flags) { g_sem = flags; }
+uint32_t oracle_get_semantics(void) { return g_sem; }
+
 /* ------------------------------------------------------------------ quantization (S2-S5) */
 
 static double family_map(int family, double x, double k) {
@@ -82,10 +96,14 @@ static double family_map(int family, double x, double k) {
     }
 }
 
-int32_t oracle_quantize(double x, const omr_channel_binding* cb, const omr_quantum_def* q) {
+/* lut_type: the value is an entry of the Quantization_8_16_bit LUT (integer pixel types). */
+static int32_t quantize_impl(double x, const omr_channel_binding* cb, const omr_quantum_def* q, int lut_type) {
     const double ws = cb->input_start, we = cb->input_end;
-    if (x < ws) return q->cd_start & 0xFF;
-    if (x >= we) return q->cd_end & 0xFF;
+    const int int_bounds = lut_type && (g_sem & OMR_SEM_WINDOW_INT_BOUNDS);
+    const double lo = int_bounds ? (double)java_d2i(ws) : ws;
+    const double hi = int_bounds ? (double)java_d2i(we) : we;
+    if (x < lo) return q->cd_start & 0xFF;
+    if (x >= hi) return q->cd_end & 0xFF;
     if (cb->noise_reduction) {
         const double dec = (we - ws) / 10.0;
         if (x < ws + dec) return q->cd_start & 0xFF;
@@ -100,11 +118,15 @@ int32_t oracle_quantize(double x, const omr_channel_binding* cb, const omr_quant
     return (int32_t)(oracle_java_round(a1 * v + (double)q->cd_start) & 0xFF);
 }
 
+int32_t oracle_quantize(double x, const omr_channel_binding* cb, const omr_quantum_def* q) {
+    return quantize_impl(x, cb, q, 0);
+}
+
 /* LUT over [globalMin, globalMax] (S5): lut[x - gMin] = q(x). */
 omr_status oracle_build_lut(const omr_channel_binding* cb, const omr_quantum_def* q,
                             uint8_t* lut, int64_t n) {
     const int64_t gmin = (int64_t)cb->global_min;
-    for (int64_t i = 0; i < n; ++i) lut[i] = (uint8_t)oracle_quantize((double)(gmin + i), cb, q);
+    for (int64_t i = 0; i < n; ++i) lut[i] = (uint8_t)quantize_impl((double)(gmin + i), cb, q, 1);
     return OMR_OK;
 }
 
@@ -166,7 +188,9 @@ typedef struct {
     int active;
     uint8_t* lut;      /* per-request LUT for <=16-bit types */
     int64_t gmin, gmax;
-    float ratio[3];
+    float ratio[3];    /* (c/255f)*(alpha/255f) */
+    float cratio[3];   /* c/255f */
+    float alpha;       /* alpha/255f */
 } chan_state;
 
 omr_status oracle_render_packed_int(const omr_quantum_def* q, const omr_channel_binding* ch,
@@ -195,7 +219,11 @@ omr_status oracle_render_packed_int(const omr_quantum_def* q, const omr_channel_
             oracle_build_lut(&ch[c], q, st[c].lut, n);
         }
         const float alpha = (float)ch[c].rgba[3] / 255.0f;
-        for (int k = 0; k < 3; ++k) st[c].ratio[k] = ((float)ch[c].rgba[k] / 255.0f) * alpha;
+        st[c].alpha = alpha;
+        for (int k = 0; k < 3; ++k) {
+            st[c].cratio[k] = (float)ch[c].rgba[k] / 255.0f;
+            st[c].ratio[k] = st[c].cratio[k] * alpha;
+        }
     }
     for (int y = 0; y < height; ++y) {
         for (int x = 0; x < width; ++x) {
@@ -214,10 +242,21 @@ omr_status oracle_render_packed_int(const omr_quantum_def* q, const omr_channel_
                     v = oracle_quantize(xv, &ch[c], q);
                 }
                 if (ch[c].reverse) v = (q->cd_end - v + q->cd_start) & 0xFF;
-                if (q->model == OMR_MODEL_GREYSCALE) { r = g = b = v; break; }
+                if (q->model == OMR_MODEL_GREYSCALE) {
+                    if (ch[c].lut && (g_sem & OMR_SEM_GREYSCALE_LUT)) {
+                        r = ch[c].lut[v]; g = ch[c].lut[256 + v]; b = ch[c].lut[512 + v];
+                    } else {
+                        r = g = b = v;
+                    }
+                    break;
+                }
                 int cr, cg, cb;
                 if (ch[c].lut) {
                     cr = ch[c].lut[v]; cg = ch[c].lut[256 + v]; cb = ch[c].lut[512 + v];
+                } else if (g_sem & OMR_SEM_ALPHA_SEPARATE) {
+                    cr = (int)((float)(int)(st[c].cratio[0] * (float)v) * st[c].alpha);
+                    cg = (int)((float)(int)(st[c].cratio[1] * (float)v) * st[c].alpha);
+                    cb = (int)((float)(int)(st[c].cratio[2] * (float)v) * st[c].alpha);
                 } else {
                     cr = (int)(st[c].ratio[0] * (float)v);
                     cg = (int)(st[c].ratio[1] * (float)v);
@@ -398,7 +437,14 @@ static const uint8_t kValAcC[162] = {
     0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8,
     0xf9, 0xfa};
 
-/* javax.imageio JPEG.convertToLinearQuality + JPEGQTable.getScaledInstance(scale, true). */
+/* JPEGQTable.getScaledInstance(scale, true): (int)(q*scale + 0.5f) clamped to [1, 255]. */
+static int qscale(int qv, float scale) {
+    volatile float a = (float)qv * scale;
+    const int sv = (int)(a + 0.5f);
+    return sv < 1 ? 1 : sv > 255 ? 255 : sv;
+}
+
+/* javax.imageio JPEG.convertToLinearQuality + JPEGQTable.getScaledInstance(scale, true) (S10). */
 void oracle_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]) {
     float qf = quality;
     if (qf <= 0.0f) qf = 0.01f;
@@ -406,12 +452,9 @@ void oracle_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64
     if (qf < 0.5f) qf = 0.5f / qf;
     else qf = 2.0f - (qf * 2.0f);
     for (int i = 0; i < 64; ++i) {
-        volatile float a = (float)kStdLuma[i] * qf;
-        int sv = (int)(a + 0.5f);
-        luma[i] = (uint8_t)(sv < 1 ? 1 : sv > 255 ? 255 : sv);
-        volatile float b = (float)kStdChroma[i] * qf;
-        sv = (int)(b + 0.5f);
-        chroma[i] = (uint8_t)(sv < 1 ? 1 : sv > 255 ? 255 : sv);
+        luma[i] = (uint8_t)qscale(kStdLuma[i], qf);
+        const int cbase = (g_sem & OMR_SEM_JPEG_CHROMA_DIV2) ? qscale(kStdChroma[i], 0.5f) : kStdChroma[i];
+        chroma[i] = (uint8_t)qscale(cbase, qf);
     }
 }
 

@@ -32,6 +32,9 @@ omr_status oracle_project_stack(const void* stack, int32_t pixel_type, int32_t b
                                 int32_t big_endian_out);
 omr_status oracle_mask_indices(const uint8_t* bits, size_t n_bytes, int32_t width,
                                int32_t height, int32_t flip_h, int32_t flip_v, uint8_t* idx);
+/* OMR_SEM_* switches (include/omr/omr.h) for every later call; process-wide. */
+void oracle_set_semantics(uint32_t flags);
+uint32_t oracle_get_semantics(void);
 void oracle_jpeg_quant_tables(float quality, uint8_t luma[64], uint8_t chroma[64]);
 /* Baseline JPEG (IJG 6b restatement).  Returns bytes written or 0 if cap too small. */
 size_t oracle_encode_jpeg(const uint32_t* argb, int32_t width, int32_t height, float quality,

@@ -16,6 +16,32 @@ if not os.path.exists(PATH):
     raise ImportError(f"{PATH} missing: run `make -C oracle`")
 lib = ctypes.CDLL(PATH)
 
+
+def _cpu_flags():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("flags"):
+                    return set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    return set()
+
+
+# The timed CPU baseline (bench.py cpu_baseline legs) runs an ISA-tuned build of the same
+# source: -O3 -march=x86-64-v4 (AVX-512) when this host has it, else x86-64-v3 (AVX2/FMA;
+# -ffp-contract=off keeps the arithmetic identical).  Parity checks use the portable build.
+_V4 = {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"}
+_flags = _cpu_flags()
+FAST_BUILD = "-O3 (portable)"
+fast_lib = lib
+for _tag, _need in (("v4", _V4), ("v3", {"avx2", "fma", "bmi2"})):
+    _p_fast = os.path.join(REPO, "oracle", f"liboracle_{_tag}.so")
+    if _need <= _flags and os.path.exists(_p_fast):
+        fast_lib = ctypes.CDLL(_p_fast)
+        FAST_BUILD = f"-O3 -march=x86-64-{_tag}"
+        break
+
 _vp, _i32, _i64, _sz, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float
 _QD = ctypes.POINTER(_lib.QuantumDef)
 _CB = ctypes.POINTER(_lib.ChannelBinding)
@@ -29,18 +55,36 @@ for name, res, args in [
     ("oracle_project_stack", _i32, [_vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32]),
     ("oracle_mask_indices", _i32, [_vp, _sz, _i32, _i32, _i32, _i32, _vp]),
     ("oracle_jpeg_quant_tables", None, [_f32, _vp, _vp]),
+    ("oracle_set_semantics", None, [ctypes.c_uint32]),
+    ("oracle_get_semantics", ctypes.c_uint32, []),
     ("oracle_encode_jpeg", _sz, [_vp, _i32, _i32, _f32, _vp, _sz]),
     ("oracle_jpeg_coefficients", _i64, [_vp, _i32, _i32, _f32, _vp, _i64]),
     ("oracle_render_tiles_mt", ctypes.c_double, [_QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32,
                                                  _i32, _i32, _vp, _i32]),
 ]:
-    fn = getattr(lib, name)
-    fn.restype = res
-    fn.argtypes = args
+    for _l in {id(lib): lib, id(fast_lib): fast_lib}.values():
+        fn = getattr(_l, name)
+        fn.restype = res
+        fn.argtypes = args
 
 
 def _p(a):
     return None if a is None else a.ctypes.data
+
+
+class semantics:
+    """with oracle_lib.semantics(flags): ... — OMR_SEM_* switches of the restatement."""
+
+    def __init__(self, flags):
+        self.flags = int(flags)
+
+    def __enter__(self):
+        self.prev = lib.oracle_get_semantics()
+        lib.oracle_set_semantics(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        lib.oracle_set_semantics(self.prev)
 
 
 def java_round(x):
@@ -62,13 +106,13 @@ def build_lut(channel, n):
 
 
 def render(channels, planes, pixel_type, width, height, model="rgb", big_endian=False,
-           flip_h=False, flip_v=False, row_stride=0, qdef=None):
+           flip_h=False, flip_v=False, row_stride=0, qdef=None, fast=False):
     """renderAsPackedInt + flip on the CPU. Returns (status, argb[h, w])."""
     arr, keep = make_bindings(channels)
     q = qdef or make_qdef(model)
     ptrs = (ctypes.c_void_p * max(len(planes), 1))(*[_p(p) for p in planes])
     out = np.zeros((height, width), dtype=np.uint32)
-    st = lib.oracle_render_packed_int(ctypes.byref(q), arr, len(channels), ptrs, row_stride,
+    st = (fast_lib if fast else lib).oracle_render_packed_int(ctypes.byref(q), arr, len(channels), ptrs, row_stride,
                                       pixel_type, int(big_endian), width, height, out.ctypes.data)
     if st == 0 and (flip_h or flip_v):
         f = np.empty_like(out)
@@ -84,10 +128,11 @@ def flip_int(src, w, h, fh, fv):
     return st, out
 
 
-def project(stack, pixel_type, sx, sy, sz, alg, start, end, stepping=1, be_in=False, be_out=False):
+def project(stack, pixel_type, sx, sy, sz, alg, start, end, stepping=1, be_in=False, be_out=False,
+            fast=False):
     bpp = _lib.BYTES_PER_PIXEL[pixel_type]
     out = np.zeros(sx * sy * bpp, dtype=np.uint8)
-    st = lib.oracle_project_stack(_p(stack), pixel_type, int(be_in), sx, sy, sz, alg, start, end,
+    st = (fast_lib if fast else lib).oracle_project_stack(_p(stack), pixel_type, int(be_in), sx, sy, sz, alg, start, end,
                                   stepping, out.ctypes.data, int(be_out))
     return st, out
 
@@ -124,10 +169,12 @@ def jpeg_coefficients(argb, w, h, q):
 
 
 def render_tiles_mt(channels, tile_planes, n_tiles, pixel_type, width, height, model="rgb",
-                    big_endian=False, flip_h=False, flip_v=False, n_threads=1, keep_output=True):
+                    big_endian=False, flip_h=False, flip_v=False, n_threads=1, keep_output=True,
+                    fast=False):
     """Reference-CPU proxy: per-request LUT rebuild + render (+flip) over a thread pool.
     tile_planes: list (per tile) of lists (per channel) of numpy planes.  Returns (seconds, out);
-    keep_output=False renders into per-thread scratch (bounded memory for timing samples)."""
+    keep_output=False renders into per-thread scratch (bounded memory for timing samples);
+    fast=True runs the ISA-tuned build (timing only)."""
     arr, keep = make_bindings(channels)
     q = make_qdef(model)
     size_c = len(channels)
@@ -136,7 +183,8 @@ def render_tiles_mt(channels, tile_planes, n_tiles, pixel_type, width, height, m
         flat.extend(_p(p) for p in tile_planes[t])
     ptrs = (ctypes.c_void_p * max(len(flat), 1))(*flat)
     out = np.zeros((n_tiles, height, width), dtype=np.uint32) if keep_output else None
-    secs = lib.oracle_render_tiles_mt(ctypes.byref(q), arr, size_c, ptrs, n_tiles, pixel_type,
+    L = fast_lib if fast else lib
+    secs = L.oracle_render_tiles_mt(ctypes.byref(q), arr, size_c, ptrs, n_tiles, pixel_type,
                                       int(big_endian), width, height, int(flip_h), int(flip_v),
                                       _p(out), n_threads)
     return secs, out

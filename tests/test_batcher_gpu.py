@@ -97,3 +97,73 @@ def test_duplicates_rendered_once_and_errors(romio):
             b.wait(t)
         assert e.value.status == _lib.INVALID_ARGUMENT
     pb.close()
+
+
+def _oracle_argb(px, ch, model, z, x, y, flip):
+    planes = [np.ascontiguousarray(px[0, c, z, y:y + TH, x:x + TW]).astype(">u2") for c in range(C)]
+    s, exp = O.render(ch, planes, _lib.PIXELS_UINT16, TW, TH, big_endian=True, flip_h=flip, model=model)
+    assert s == 0
+    return exp
+
+
+def test_every_format_against_the_oracle(romio):
+    """Batched ARGB words, JPEG bytes and PNG pixels vs the CPU restatement (not vs the GPU's own
+    one-request path)."""
+    import io
+    from PIL import Image
+    path, px = romio
+    pb = PixelBuffer(path, X, Y, Z, C, T, _lib.PIXELS_UINT16)
+    jobs = [dict(model=m, z=z, x=x, y=y, flip=f, fmt=fmt, q=q)
+            for i, (m, z, x, y, f, fmt, q) in enumerate([
+                ("rgb", 0, 0, 0, False, "argb", 0.9), ("rgb", 1, 256, 256, True, "argb", 0.9),
+                ("rgb", 0, 512, 0, False, "jpeg", 0.9), ("rgb", 1, 768, 512, True, "jpeg", 0.9),
+                ("greyscale", 0, 256, 512, False, "jpeg", 0.5), ("rgb", 1, 0, 256, False, "png", 0.9),
+                ("greyscale", 0, 512, 512, True, "png", 0.9), ("greyscale", 1, 768, 0, False, "argb", 0.9)])]
+    ch = c2_channels(3)
+    with Batcher(0, max_batch=16, max_wait_us=20000) as b:
+        tickets = [b.submit(pb, O.make_qdef(j["model"]), ch, j["z"], 0, j["x"], j["y"], TW, TH, flip_h=j["flip"],
+                            fmt=j["fmt"], quality=j["q"]) for j in jobs]
+        outs = [b.wait(t) for t in tickets]
+    for j, got in zip(jobs, outs):
+        exp = _oracle_argb(px, ch, j["model"], j["z"], j["x"], j["y"], j["flip"])
+        if j["fmt"] == "argb":
+            np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(TH, TW), exp)
+        elif j["fmt"] == "jpeg":
+            assert got == O.encode_jpeg(exp, TW, TH, j["q"]), j
+        else:
+            rgb = np.asarray(Image.open(io.BytesIO(got)).convert("RGB"))
+            np.testing.assert_array_equal(rgb, exp.view(np.uint8).reshape(TH, TW, 4)[..., 2::-1])
+    pb.close()
+
+
+def test_quantization_error_fails_only_its_tile(tmp_path):
+    """One tile holds a pixel above the channel's LUT domain (globalMax): that request fails with
+    QuantizationException (500); the tiles batched with it still render (each request has its own
+    Renderer in the reference, ImageRegionRequestHandler.java:436-440, :479-480)."""
+    rng = np.random.default_rng(5)
+    px = rng.integers(0, 50000, (T, C, 1, 512, 1024), dtype=np.uint16)
+    px[0, 1, 0, 300, 700] = 65000                                  # inside tile (x=512, y=256)
+    path = tmp_path / "pixels"
+    write_romio(path, px, _lib.PIXELS_UINT16)
+    pb = PixelBuffer(path, 1024, 512, 1, C, T, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    for c in ch:
+        c["global_max"] = 60000.0
+    tiles = [(x, y) for y in (0, 256) for x in (0, 256, 512, 768)]
+    with Batcher(0, max_batch=16, max_wait_us=20000) as b:
+        tickets = [b.submit(pb, O.make_qdef("rgb"), ch, 0, 0, x, y, TW, TH, fmt="argb") for x, y in tiles]
+        res = []
+        for t in tickets:
+            try:
+                res.append(b.wait(t))
+            except _lib.OmrError as e:
+                res.append(e.status)
+    for (x, y), r in zip(tiles, res):
+        if (x, y) == (512, 256):
+            assert r == _lib.QUANTIZATION
+        else:
+            planes = [np.ascontiguousarray(px[0, c, 0, y:y + TH, x:x + TW]).astype(">u2") for c in range(C)]
+            s, exp = O.render(ch, planes, _lib.PIXELS_UINT16, TW, TH, big_endian=True)
+            assert s == 0
+            np.testing.assert_array_equal(np.frombuffer(r, np.uint32).reshape(TH, TW), exp)
+    pb.close()
