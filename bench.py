@@ -284,9 +284,10 @@ def jpeg_cpu_baseline(torch, name, src, chans, pt, be, q, seconds, threads):
     def one(i):
         st, argb = oracle_lib.render(chans, tiles[i % len(tiles)], pt, TILE, TILE, model=model, big_endian=be,
                                      fast=True)
-        rgb = argb.view(np.uint8).reshape(TILE, TILE, 4)[:, :, 2::-1]      # BGRA bytes -> RGB
+        # BGRA bytes -> RGB by PIL's C unpacker (ImageUtil.createBufferedImage drops alpha)
+        img = Image.frombuffer("RGB", (TILE, TILE), argb, "raw", "BGRX", 0, 1)
         buf = io.BytesIO()
-        Image.fromarray(np.ascontiguousarray(rgb), "RGB").save(buf, "JPEG", qtables=qtables, subsampling=2)
+        img.save(buf, "JPEG", qtables=qtables, subsampling=2)
         return buf.tell()
 
     n, secs = _cpu_pool(one, seconds, threads)

@@ -149,7 +149,13 @@ enum {
     /* JPEG chroma base table K2Div2Chrominance (Annex K chroma halved, JPEGQTable) scaled by the
      * quality instead of K2Chrominance. */
     OMR_SEM_JPEG_CHROMA_DIV2 = 1u << 3,
-    OMR_SEM_ALL = 0xFu
+    /* Projection glue: render every active channel.  By default
+     * omr_render_projected_device reproduces the reference, whose InMemoryPlanarPixelBuffer is
+     * sized sizeC = #active channels (ImageRegionRequestHandler.java:538-555) but read at the
+     * original channel index (:525, :549): a rendered channel whose index is >= #active fails its
+     * bounds check (DimensionsOutOfBoundsException -> 500, here OMR_INTERNAL). */
+    OMR_SEM_PROJECTION_ALL_ACTIVE = 1u << 4,
+    OMR_SEM_ALL = 0x1Fu
 };
 /* Semantics of every later call on this context (renders, projections' renders, JPEG). */
 omr_status omr_ctx_set_semantics(omr_ctx* ctx, uint32_t flags);

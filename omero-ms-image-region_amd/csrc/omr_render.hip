@@ -145,7 +145,7 @@ struct K2Args {
     int32_t flip_h, flip_v;
     int32_t n_active, cd_start, cd_end, cds8, cde8;
     int32_t tile_uniform;       // every block lies inside one tile (chunks per tile % block chunks == 0)
-    int32_t nt_store;           // non-temporal ARGB stores (OMR_K2_NT_STORE=0 disables; measurement switch)
+    int32_t nt_store;           // non-temporal ARGB stores (OMR_K2_NT_STORE=1; measurement switch)
     uint32_t total;             // work items (chunks of VEC pixels)
     FastDiv cpt, cpr;           // chunks per tile, chunks per row
     K2Chan ch[kMaxActive];
@@ -169,11 +169,12 @@ struct Chunk {
 template <typename T> __device__ __forceinline__ const OMR_GLOBAL T* gload_ptr(const void* p) { return (const OMR_GLOBAL T*)(p); }
 template <typename T> __device__ __forceinline__ OMR_GLOBAL T* gstore_ptr(void* p) { return (OMR_GLOBAL T*)(p); }
 
-// K2 streams every pixel once and writes every output once: 16-byte loads are non-temporal,
-// and so are the ARGB stores when a pixel reads at least as many bytes as it writes
-// (tools/probe_stream3.hip: the C2 pattern at 6.07 TB/s with nt loads + stores vs 5.90 TB/s
-// plain; a write-only stream drops from 6.7 to 2.4 TB/s with nt stores, so the 1-byte
-// single-channel case keeps plain stores).
+// K2 streams every pixel once and writes every output once: 16-byte loads are non-temporal.
+// The ARGB stores are plain by default: non-temporal stores cost 10 % extra HBM write traffic
+// (PMC WRITE_SIZE 1.103x the algorithmic bytes, profiles/pmc_render_c2.json) for no measured
+// gain once the clocks are up (sustained K2 0.549 vs 0.547 ms, profiles/r02/k2_series_*.json);
+// OMR_K2_NT_STORE=1 turns them back on for measurement (never for the 1-byte single-channel
+// case: a write-only stream drops from 6.7 to 2.4 TB/s with nt stores).
 #ifndef OMR_K2_NT
 #define OMR_K2_NT 1
 #endif
@@ -1194,6 +1195,17 @@ extern "C" omr_status omr_render_projected_device(
     const int na = pp.plan.n_active;
     for (int a = 0; a < na; ++a)
         if (!d_stacks || !d_stacks[pp.plan.ch[a].index]) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack for active channel");
+    if (!(ctx->sem & OMR_SEM_PROJECTION_ALL_ACTIVE)) {
+        // :507-555: the projected buffer holds sizeC = #active channels but is read at each rendered
+        // channel's original index (Appendix B quirk 3) -> the buffer's bounds check fails
+        int projected_size_c = 0;
+        for (int c = 0; c < size_c; ++c) projected_size_c += channels[c].active ? 1 : 0;
+        for (int a = 0; a < na; ++a)
+            if (pp.plan.ch[a].index >= projected_size_c)
+                return fail(ctx, OMR_INTERNAL, "DimensionsOutOfBoundsException: C '" +
+                                                   std::to_string(pp.plan.ch[a].index) + "' greater than sizeC '" +
+                                                   std::to_string(projected_size_c) + "'");
+    }
     if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const int bpp = bytes_per_pixel(pixel_type);

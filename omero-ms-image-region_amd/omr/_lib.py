@@ -40,7 +40,8 @@ MODEL_GREYSCALE, MODEL_RGB = 0, 1
 PROJECTION_MAX, PROJECTION_MEAN, PROJECTION_SUM = 0, 1, 2
 # OMR_SEM_* switches of the un-vendored upstream semantics (include/omr/omr.h)
 SEM_WINDOW_INT_BOUNDS, SEM_ALPHA_SEPARATE, SEM_GREYSCALE_LUT, SEM_JPEG_CHROMA_DIV2 = 1, 2, 4, 8
-SEM_ALL = 0xF
+SEM_PROJECTION_ALL_ACTIVE = 16
+SEM_ALL = 0x1F
 
 PIXEL_TYPE_NAMES = {"int8": PIXELS_INT8, "uint8": PIXELS_UINT8, "int16": PIXELS_INT16,
                     "uint16": PIXELS_UINT16, "int32": PIXELS_INT32, "uint32": PIXELS_UINT32,

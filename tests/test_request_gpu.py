@@ -137,6 +137,30 @@ def test_render_image_region_lut_channel(ctx, image, tmp_path):
     np.testing.assert_array_equal(np.asarray(Image.open(io.BytesIO(got)).convert("RGB")), rgb(exp))
 
 
+def test_projection_channel_index_quirk(ctx, image):
+    """the projected buffer holds sizeC = #active channels but is read
+    at the original channel index (ImageRegionRequestHandler.java:507-555).  With only channel 3
+    active the reference's bounds check fails (500); OMR_SEM_PROJECTION_ALL_ACTIVE renders it."""
+    from PIL import Image
+    kw = dict(p="intmax", format="png", c="-1|0:65535$FF0000,-2|1755:51199$00FF00,3|3218:26623$0000FF")
+    irc = ImageRegionCtx(params(**kw))
+    with pytest.raises(_lib.OmrError) as e:
+        ImageRegionRequestHandler(ctx, irc).render_image_region(buffer(image))
+    assert e.value.status == _lib.INTERNAL and "DimensionsOutOfBounds" in ctx.last_error()
+    ctx.set_semantics(_lib.SEM_PROJECTION_ALL_ACTIVE)
+    try:
+        got = ImageRegionRequestHandler(ctx, irc).render_image_region(buffer(image))
+    finally:
+        ctx.set_semantics(0)
+    exp = oracle_argb(irc, image[0])
+    np.testing.assert_array_equal(np.asarray(Image.open(io.BytesIO(got)).convert("RGB")), rgb(exp))
+    # channel 1 alone (index 0 < sizeC 1) renders under both settings
+    irc = ImageRegionCtx(params(p="intmax", format="png", c="1|0:65535$FF0000,-2|0:1$00FF00,-3|0:1$0000FF"))
+    got = ImageRegionRequestHandler(ctx, irc).render_image_region(buffer(image))
+    np.testing.assert_array_equal(np.asarray(Image.open(io.BytesIO(got)).convert("RGB")),
+                                  rgb(oracle_argb(irc, image[0])))
+
+
 def test_unknown_format_is_none_and_settings_errors(ctx, image):
     irc = ImageRegionCtx(params(format="gif"))
     assert ImageRegionRequestHandler(ctx, irc).render_image_region(buffer(image)) is None   # -> 404

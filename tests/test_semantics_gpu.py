@@ -87,7 +87,8 @@ def test_window_int_bounds_batch_fast_path(sem_ctx):
     for c, (s, e) in enumerate([(0.5, 65534.5), (1755.5, 51199.5), (3218.75, 26623.25), (100.5, 4000.5)]):
         chans[c]["input_start"], chans[c]["input_end"] = f32(s), f32(e)
     tiles = [[p.astype(">u2") for p in tile_u16(40 + t, 4, h, w, uniform=True)] for t in range(n)]
-    data = torch.from_numpy(np.stack([np.stack(t) for t in tiles]).view(np.uint8).copy()).to("cuda")
+    be = np.stack([np.stack(t) for t in tiles]).astype(">u2")      # np.stack returns native order
+    data = torch.from_numpy(be.view(np.uint8).copy()).to("cuda")
     out = torch.empty((n, h, w), dtype=torch.int32, device="cuda")
     plane = h * w * 2
     for flags in (0, _lib.SEM_WINDOW_INT_BOUNDS):
