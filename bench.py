@@ -235,10 +235,24 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
         assert (bufs[1][4].cpu().numpy() == 0).all(), "JPEG batch did not fit its buffer"
         ln = lens.cpu().numpy().astype(np.int64)
         assert (stat.cpu().numpy() == 0).all(), "JPEG batch did not fit its buffer"
+        ref_files = d_out.cpu().numpy()
+        ref_offs = offs.cpu().numpy()
+
+        # Fused: render + JPEG in one call (F1 = render + colour + FDCT in one kernel, the ARGB tile
+        # never reaches HBM), omr_render_jpeg_batch_strided_device.
+        def step_fused():
+            ctx.render_jpeg_batch_strided_device(qd, chans, src, tstride, cstride, B, pt, TILE, TILE, q, d_out, offs,
+                                                 lens, stat, big_endian=be, bindings=binds)
+        el_f, avg_f = _timed(torch, ctx, step_fused, steps, warmup)
+        fo, fl = offs.cpu().numpy(), lens.cpu().numpy()
+        fb = d_out.cpu().numpy()
+        assert all(fb[fo[i]:fo[i] + fl[i]].tobytes() == ref_files[ref_offs[i]:ref_offs[i] + ln[i]].tobytes()
+                   for i in range(B)), "fused render->JPEG differs from render + JPEG"
+        # B1 / F1 are VALU-bound: instructions per MCU from the SQ counters (profiles/r02), the
+        # rate 1 wave-instruction per 4 cycles per SIMD (wave64 on SIMD16)
+        mcus = B * (TILE // 16) ** 2
         px = TILE * TILE
         nblk = (TILE // 16) ** 2 * 6
-        j1_bytes = B * (px * 4 + nblk * (128 + 4))               # ARGB in; coefs + aclen + dc out
-        j3_bytes = B * nblk * (128 + 2 + 4) + int(ln.sum())     # coefs + dc + offsets in; bitstream out
         res[name] = {
             "tiles_per_s": round(B * steps / el, 1),
             "ms_per_step": round(1e3 * el / steps, 4),
@@ -250,8 +264,15 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
                           "jpeg_total": round(avg.get(4, float("nan")), 5),
                           "J1_fdct": round(avg.get(5, float("nan")), 5),
                           "J3_huffman": round(avg.get(6, float("nan")), 5)},
-            "J1_hbm_gbs": round(j1_bytes / (avg.get(5, float("nan")) * 1e-3) / 1e9, 1),
-            "J3_hbm_gbs": round(j3_bytes / (avg.get(6, float("nan")) * 1e-3) / 1e9, 1),
+            "fused": {"tiles_per_s": round(B * steps / el_f, 1), "ms_per_step": round(1e3 * el_f / steps, 4),
+                      "kernel_ms": {"F1_render_fdct": round(avg_f.get(5, float("nan")), 5),
+                                    "jpeg_total": round(avg_f.get(4, float("nan")), 5),
+                                    "J3_huffman": round(avg_f.get(6, float("nan")), 5)},
+                      "F1_plane_read_gbs": round(B * tstride / (avg_f.get(5, float("nan")) * 1e-3) / 1e9, 1),
+                      "byte_identical_to_unfused": True},
+            "mcus_per_step": mcus,
+            "J1_ns_per_mcu": round(avg.get(5, float("nan")) * 1e6 / mcus, 4),
+            "F1_ns_per_mcu": round(avg_f.get(5, float("nan")) * 1e6 / mcus, 4),
         }
         if with_cpu:
             try:

@@ -361,6 +361,33 @@ omr_status omr_encode_jpeg_batch_device(omr_ctx* ctx, const uint32_t* d_argb, in
                                         int32_t n_tiles, int32_t width, int32_t height, float quality,
                                         uint8_t* d_out, size_t out_cap, uint64_t* d_offsets,
                                         uint32_t* d_lengths, int32_t* d_status);
+/*
+ * render_image_region's default response for a batch of tiles in one call: render (quantize,
+ * codomain, composite, flip: renderAsPackedInt + flip, :559, :574-575) and JPEG-encode
+ * (createBufferedImage + compressToStream, :576-582) n_tiles same-settings tiles whose planes
+ * are already in HBM.  Output exactly as omr_encode_jpeg_batch_device (byte-identical files);
+ * d_status[i] (optional) also reports OMR_QUANTIZATION for a tile with a pixel outside its LUT
+ * domain.  8/16-bit integer pixels with 1..4 active channels on tiles whose sides are multiples
+ * of 16 render inside the encoder's first kernel (the ARGB tile never reaches HBM); other
+ * requests render with K2 first.  Plane rows must start 4-byte aligned (16-bit) / 2-byte
+ * aligned (8-bit) for the fused path.  Asynchronous on the context stream.
+ */
+omr_status omr_render_jpeg_batch_strided_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                                const omr_channel_binding* channels, int32_t size_c,
+                                                const void* d_base, int64_t tile_stride_bytes,
+                                                int64_t channel_stride_bytes, int32_t n_tiles, int64_t row_stride,
+                                                int32_t pixel_type, int32_t big_endian, int32_t width, int32_t height,
+                                                int32_t flip_h, int32_t flip_v, float quality, uint8_t* d_out,
+                                                size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                                int32_t* d_status);
+/* Same with a device plane-pointer table [tile][channel] (omr_render_batch_device's layout). */
+omr_status omr_render_jpeg_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                        const omr_channel_binding* channels, int32_t size_c,
+                                        const void* const* d_plane_ptrs, int32_t n_tiles, int64_t row_stride,
+                                        int32_t pixel_type, int32_t big_endian, int32_t width, int32_t height,
+                                        int32_t flip_h, int32_t flip_v, float quality, uint8_t* d_out,
+                                        size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                        int32_t* d_status);
 /* Same, host output: files packed in out (cap bytes), offsets/lengths host arrays; synchronous. */
 omr_status omr_encode_jpeg_batch(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
                                  int32_t n_tiles, int32_t width, int32_t height, float quality,

@@ -44,6 +44,19 @@ omr_status ensure_workspace(Ctx* c, size_t bytes) {
     return OMR_OK;
 }
 
+omr_status ensure_aux(Ctx* c, size_t bytes) {
+    if (bytes <= c->aux_cap) return OMR_OK;
+    if (c->aux) {
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        OMR_HIP(c, hipFree(c->aux));
+        c->aux = nullptr;
+        c->aux_cap = 0;
+    }
+    OMR_HIP(c, hipMalloc(&c->aux, bytes));
+    c->aux_cap = bytes;
+    return OMR_OK;
+}
+
 omr_status stage_h2d2(Ctx* c, void* dst1, const void* src1, size_t n1, void* dst2, const void* src2, size_t n2) {
     const size_t off2 = align_up(n1, 16), bytes = off2 + n2;
     if (bytes == 0) return OMR_OK;
@@ -178,6 +191,7 @@ void omr_ctx_destroy(omr_ctx* c) {
         if (c->pin[i]) (void)hipHostFree(c->pin[i]);
     }
     if (c->ws) (void)hipFree(c->ws);
+    if (c->aux) (void)hipFree(c->aux);
     if (c->d_flag) (void)hipFree(c->d_flag);
     if (c->h_flag) (void)hipHostFree(c->h_flag);
     if (c->h_out) (void)hipHostFree(c->h_out);

@@ -71,6 +71,10 @@ struct Ctx {
     // device workspace (grow-only bump arena, reset per call)
     void* ws = nullptr;
     size_t ws_cap = 0;
+    // device buffer for intermediate results that must outlive the workspace's reuse within one
+    // call (the unfused render -> JPEG path's ARGB batch); grow-only
+    void* aux = nullptr;
+    size_t aux_cap = 0;
     // device-side sticky status word (quantization errors of async calls)
     int32_t* d_flag = nullptr;
     int32_t* h_flag = nullptr;   // fine-grained pinned word: d_flag copied here by a kernel at sync
@@ -111,6 +115,8 @@ omr_status fail(Ctx* c, omr_status s, const std::string& msg);
 omr_status hip_fail(Ctx* c, hipError_t e, const char* what);
 // Ensure the workspace holds at least `bytes`; invalidates previous contents.
 omr_status ensure_workspace(Ctx* c, size_t bytes);
+// Ensure ctx->aux holds at least `bytes` (contents not preserved across growth).
+omr_status ensure_aux(Ctx* c, size_t bytes);
 // Copy `bytes` from host `src` to device `dst` through the pinned ring (async on ctx stream).
 // Move the sticky device status word to fine-grained host memory and clear it, on `s`
 // (omr_render.hip): omr_ctx_synchronize then needs one stream sync and no copy round trip.

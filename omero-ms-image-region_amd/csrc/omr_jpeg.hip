@@ -13,6 +13,9 @@
 //   J4  one lane per block: re-encode and OR the bits into a big-endian word stream
 //   J5  count 0xFF per 16-byte chunk -> scan -> J6 scatter with 0x00 stuffing + 1-bit pad
 #include "omr_device.h"
+#include "omr_k2.h"
+
+#include <memory>
 
 namespace omr {
 
@@ -747,40 +750,22 @@ __device__ __forceinline__ void load_pair(const uint32_t* img, int W, int x, int
 // rows of stride 8, then on columns) hit 48 distinct banks; 64 gave 6-way conflicts.
 constexpr int kBS = 73;
 
-__global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
-    __shared__ int s[4][6 * kBS + 8];
-    __shared__ uint8_t s_acsize[2][256];
-    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
-    __syncthreads();
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int tile = blockIdx.y;
-    int* S = s[wv];
-    const int W = A.W, H = A.H;
-    // 8-byte pixel-pair loads need every row start 8-byte aligned
-    const bool even_w = (W & 1) == 0 && (A.tile_stride & 1) == 0 && ((uintptr_t)A.argb & 7) == 0;
-    const int cx = lane & 7, cy = lane >> 3;
-    const uint32_t* img = A.argb + (int64_t)tile * A.tile_stride;
-    const int ywib = (W + 7) / 8, yhib = (H + 7) / 8;
-    const int nat = c_zigzag[lane];                 // this lane owns zig-zag position `lane`
-    const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
-    const uint32_t my_ = (uint32_t)((0x100000000ull + (uint64_t)(qy << 3) - 1) / (uint64_t)(qy << 3));
-    const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
-    const int hy = qy << 2, hc = qc << 2;
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
-    const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
-    const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
-    const int m0 = (blockIdx.x * 4 + wv) * A.mpw;
-    const int m1 = min(m0 + A.mpw, A.n_mcu);
-    // The next MCU's four pixels are loaded while this one is transformed (one pass of HBM
-    // latency per wave instead of one per MCU).
-    // Even widths: two unconditional 8-byte loads per lane at clamped addresses; the edge
-    // replication select happens when the pixels are used, so nothing waits on the prefetch.
+// B1's pixel source: rendered ARGB tiles in HBM.  issue(m) loads the four pixels this lane
+// needs for MCU m (the next MCU's loads are in flight while the current one is transformed);
+// take() hands them over at the start of that MCU.
+struct ArgbSource {
+    const uint32_t* img;
+    int W, H;
+    bool even_w;
     uint2 na = make_uint2(0, 0), nb = make_uint2(0, 0);
     bool nclamp = false;
-    auto fetch = [&](int m) {
-        const int mx = m % A.mcux, my = m / A.mcux;
-        const int x0 = mx * 16 + 2 * cx, y0 = my * 16 + 2 * cy;
+    __device__ ArgbSource(const B1Args& A, int tile)
+        : img(A.argb + (int64_t)tile * A.tile_stride), W(A.W), H(A.H),
+          // 8-byte pixel-pair loads need every row start 8-byte aligned
+          even_w((A.W & 1) == 0 && (A.tile_stride & 1) == 0 && ((uintptr_t)A.argb & 7) == 0) {}
+    // Even widths: two unconditional 8-byte loads per lane at clamped addresses; the edge
+    // replication select happens when the pixels are used, so nothing waits on the prefetch.
+    __device__ __forceinline__ void issue(int x0, int y0) {
         const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
         if (even_w) {
             const int xl = min(x0, W - 2);                        // even, W >= 2
@@ -793,6 +778,130 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
             nb = make_uint2(img[(int64_t)yb * W + xa], img[(int64_t)yb * W + xb]);
             nclamp = false;
         }
+    }
+    __device__ __forceinline__ void take(uint32_t& p00, uint32_t& p01, uint32_t& p10, uint32_t& p11) {
+        p00 = nclamp ? na.y : na.x; p01 = na.y; p10 = nclamp ? nb.y : nb.x; p11 = nb.y;
+    }
+    __device__ __forceinline__ uint32_t at(int x, int y) const { return img[(int64_t)y * W + x]; }
+};
+
+// Fused render -> JPEG: B1 reads the raw channel planes and renders its pixels as K2 does
+// (same quantization helpers, contribution tables in LDS), so the ARGB tile never goes through
+// HBM (the unfused path writes 4 B and reads 4 B per pixel between K2 and B1).  Tiles whose
+// sides are multiples of 16 only (no edge replication); flips map output to source pixels.
+struct FusedArgs {
+    FusedRender R;
+    const uint8_t* sbase;        // strided batches: plane(t, c) = sbase + t*tile_stride + c*chan_stride
+    const void* const* planes;   // pointer-table batches: planes[t*size_c + c]
+    int64_t tile_stride, chan_stride, row_stride;   // bytes, bytes, pixels
+    int32_t strided, size_c, flip_h, flip_v;
+    int32_t* rstat;              // [tile] OMR_QUANTIZATION when a pixel left its LUT domain
+};
+
+template <int BPP, bool BE>
+struct PlaneSource {
+    const FusedArgs& F;
+    const uint32_t* s_contrib;   // LDS [n_active][256]
+    const uint8_t* base[kFusedMaxActive];
+    uint32_t raw[kFusedMaxActive][2];
+    int W, H;
+    bool err = false;
+    __device__ PlaneSource(const FusedArgs& f, const uint32_t* sc, int tile, int w, int h)
+        : F(f), s_contrib(sc), W(w), H(h) {
+#pragma unroll
+        for (int a = 0; a < kFusedMaxActive; ++a) {
+            const int c = F.R.ch[a].index;
+            base[a] = F.strided ? F.sbase + (int64_t)tile * F.tile_stride + (int64_t)c * F.chan_stride
+                                : static_cast<const uint8_t*>(F.planes[(int64_t)tile * F.size_c + c]);
+        }
+    }
+    // Output pixels (x0, x0+1) x (y0, y0+1), x0 even, come from the source pair starting at sx
+    // (reversed under flip_h) on rows sy0, sy1.
+    __device__ __forceinline__ void issue(int x0, int y0) {
+        const int sx = F.flip_h ? W - 2 - x0 : x0;
+        const int64_t r0 = (int64_t)(F.flip_v ? H - 1 - y0 : y0) * F.row_stride + sx;
+        const int64_t r1 = (int64_t)(F.flip_v ? H - 2 - y0 : y0 + 1) * F.row_stride + sx;
+#pragma unroll
+        for (int a = 0; a < kFusedMaxActive; ++a) {
+            if (a >= F.R.n_active) break;                                // uniform
+            if constexpr (BPP == 2) {
+                raw[a][0] = *reinterpret_cast<const uint32_t*>(base[a] + r0 * 2);
+                raw[a][1] = *reinterpret_cast<const uint32_t*>(base[a] + r1 * 2);
+            } else {
+                raw[a][0] = *reinterpret_cast<const uint16_t*>(base[a] + r0);
+                raw[a][1] = *reinterpret_cast<const uint16_t*>(base[a] + r1);
+            }
+        }
+    }
+    // contribution-table entry of pixel j (0: lower address, 1: upper) of raw word w, channel a
+    __device__ __forceinline__ uint32_t entry(int a, uint32_t w, int j) {
+        const uint32_t* tab = s_contrib + a * 256;
+        if constexpr (BPP == 1) {
+            const uint32_t e = tab[(w >> (8 * j)) & 0xFF];
+            err |= (e & kErrBit) != 0;
+            return e & ~kErrBit;
+        } else {
+            if constexpr (BE) w = bswap16x2(w);
+            const uint32_t h = j ? (w >> 16) : (w & 0xFFFF);
+            const int x = F.R.is_signed ? (int)(int16_t)h : (int)h;
+            const K2Chan& p = F.R.ch[a];
+            if (p.check) err |= (x < p.gmin) | (x > p.gmax);
+            uint32_t v;
+            if (F.R.mode == kFusedFast16) {                            // uniform branches
+                v = fast16(x, p);
+            } else if (F.R.mode == kFusedLinear16 || p.mode == kModeLinear16) {
+                v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
+            } else {
+                const int xi = min(max(x, p.gmin), p.gmax);
+                v = F.R.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
+            }
+            return tab[v];
+        }
+    }
+    __device__ __forceinline__ void take(uint32_t& p00, uint32_t& p01, uint32_t& p10, uint32_t& p11) {
+        uint32_t acc[4] = {0, 0, 0, 0};
+        const int jl = F.flip_h ? 1 : 0;        // which half of the pair is the left output pixel
+#pragma unroll
+        for (int a = 0; a < kFusedMaxActive; ++a) {
+            if (a >= F.R.n_active) break;
+            acc[0] += entry(a, raw[a][0], jl);
+            acc[1] += entry(a, raw[a][0], jl ^ 1);
+            acc[2] += entry(a, raw[a][1], jl);
+            acc[3] += entry(a, raw[a][1], jl ^ 1);
+        }
+        uint32_t px[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t c = clamp_fields(acc[j]);
+            px[j] = 0xFF000000u | ((c >> 4) & 0xFF0000u) | ((c >> 2) & 0xFF00u) | (c & 0xFFu);
+        }
+        p00 = px[0]; p01 = px[1]; p10 = px[2]; p11 = px[3];
+    }
+    __device__ __forceinline__ uint32_t at(int, int) const { return 0; }   // never: H % 16 == 0
+};
+
+// The B1 body for one pixel source (see k_jpeg_fdct_batch below).
+template <class Src>
+__device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8_t (*s_acsize)[256]) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tile = blockIdx.y;
+    const int W = A.W, H = A.H;
+    const int cx = lane & 7, cy = lane >> 3;
+    const int ywib = (W + 7) / 8, yhib = (H + 7) / 8;
+    const int nat = c_zigzag[lane];                 // this lane owns zig-zag position `lane`
+    const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
+    const uint32_t my_ = (uint32_t)((0x100000000ull + (uint64_t)(qy << 3) - 1) / (uint64_t)(qy << 3));
+    const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
+    const int hy = qy << 2, hc = qc << 2;
+    const uint64_t lt_mask = (1ull << lane) - 1;
+    // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
+    const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
+    const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
+    const int m0 = (blockIdx.x * 4 + wv) * A.mpw;
+    const int m1 = min(m0 + A.mpw, A.n_mcu);
+    auto fetch = [&](int m) {
+        const int mx = m % A.mcux, my = m / A.mcux;
+        src.issue(mx * 16 + 2 * cx, my * 16 + 2 * cy);
     };
     if (m0 < m1) fetch(m0);
     for (int m = m0; m < m1; ++m) {   // wave-uniform loop
@@ -804,7 +913,8 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
         bool grey;
         {
             const int x0 = mx * 16 + 2 * cx;
-            uint32_t p00 = nclamp ? na.y : na.x, p01 = na.y, p10 = nclamp ? nb.y : nb.x, p11 = nb.y;
+            uint32_t p00, p01, p10, p11;
+            src.take(p00, p01, p10, p11);
             if (m + 1 < m1) fetch(m + 1);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
@@ -826,8 +936,8 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
             if (cyg >= chv) {
                 const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
                 const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
-                p00 = img[(int64_t)r0 * W + xa]; p01 = img[(int64_t)r0 * W + xb];
-                p10 = img[(int64_t)r1 * W + xa]; p11 = img[(int64_t)r1 * W + xb];
+                p00 = src.at(xa, r0); p01 = src.at(xb, r0);
+                p10 = src.at(xa, r1); p11 = src.at(xb, r1);
                 ycc(p00, y, cb0, cr0); ycc(p01, y, cb1, cr1); ycc(p10, y, cb2, cr2); ycc(p11, y, cb3, cr3);
             }
             const int bias = (cx & 1) ? 2 : 1;
@@ -903,6 +1013,35 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+__global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
+    __shared__ int s[4][6 * kBS + 8];
+    __shared__ uint8_t s_acsize[2][256];
+    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
+    __syncthreads();
+    ArgbSource src(A, blockIdx.y);
+    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
+}
+
+// F1: fused render + B1 (see PlaneSource).  The contribution tables are staged once per
+// workgroup; a pixel outside its channel's LUT domain flags the tile (QuantizationException).
+template <int BPP, bool BE>
+__global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F) {
+    __shared__ int s[4][6 * kBS + 8];
+    __shared__ uint8_t s_acsize[2][256];
+    __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
+    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
+    for (int i = threadIdx.x; i < F.R.n_active * 256; i += 256) s_contrib[i] = F.R.contrib[i];
+    __syncthreads();
+    PlaneSource<BPP, BE> src(F, s_contrib, blockIdx.y, A.W, A.H);
+    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
+    if (__ballot(src.err)) {
+        if ((threadIdx.x & 63) == 0) {
+            atomicOr(F.R.flag, 1);
+            if (F.rstat) F.rstat[blockIdx.y] = OMR_QUANTIZATION;
+        }
     }
 }
 
@@ -1210,6 +1349,7 @@ struct B5Args {
     uint8_t* out;
     uint64_t cap;
     int32_t n_tiles, hdr_len;
+    const int32_t* rstat;  // [tile] render status of the fused path (optional; wins over OMR_OK)
 };
 
 __global__ void __launch_bounds__(kTileThreads) k_jpeg_tile_scan(B5Args A) {
@@ -1228,7 +1368,7 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_tile_scan(B5Args A) {
             const bool fits = off + len <= A.cap;
             A.offsets[t] = off;
             A.lengths[t] = fits ? (uint32_t)len : 0;
-            if (A.status) A.status[t] = fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
+            if (A.status) A.status[t] = (A.rstat && A.rstat[t]) ? A.rstat[t] : fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
             if (fits) {                            // EOI
                 A.out[off + len - 2] = 0xFF;
                 A.out[off + len - 1] = 0xD9;
@@ -1345,9 +1485,17 @@ static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
     return L;
 }
 
+// Fused render -> JPEG: F1 instead of B1 (fused != nullptr; d_argb unused).
+struct FusedLaunch {
+    FusedArgs args;
+    int bpp;
+    bool be;
+};
+
 static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t tile_stride, int n, int W,
                                        int H, float quality, uint8_t* d_out, uint64_t cap, uint64_t* d_offsets,
-                                       uint32_t* d_lengths, int32_t* d_status, const JpegBatchLayout& L) {
+                                       uint32_t* d_lengths, int32_t* d_status, const JpegBatchLayout& L,
+                                       const FusedLaunch* fused = nullptr, const int32_t* rstat = nullptr) {
     uint8_t ql[64], qc[64];
     quant_tables(quality, ctx->sem, ql, qc);
     std::vector<uint8_t> hdr;
@@ -1376,7 +1524,8 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     B4aArgs a4{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), u32(L.ngroups), L.slot_words, L.slot_chunks,
                L.slot_groups};
     GroupScanArgs a4b{u32(L.csum), u32(L.ngroups), u32(L.stuffed), nullptr, u32(L.tbits), L.slot_groups, 0, 0};
-    B5Args a5{u32(L.stuffed), d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size()};
+    B5Args a5{u32(L.stuffed), d_offsets, d_lengths, d_status, d_out, cap, n, (int32_t)hdr.size(),
+              fused ? fused->args.rstat : rstat};
     B6Args a6{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), d_offsets, d_lengths, d_out,
               L.slot_words, L.slot_chunks, L.slot_groups, (int32_t)hdr.size(), {}};
     std::memcpy(a6.hdr, hdr.data(), hdr.size());
@@ -1388,9 +1537,15 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     KernelTimer whole(ctx, 4);
     {
         KernelTimer t(ctx, 5);
-        hipLaunchKernelGGL(k_jpeg_fdct_batch, dim3((unsigned)((L.n_mcu + 4 * a1.mpw - 1) / (4 * a1.mpw)),
-                                                    (unsigned)n), dim3(256), 0,
-                           ctx->stream, a1);
+        const dim3 g1((unsigned)((L.n_mcu + 4 * a1.mpw - 1) / (4 * a1.mpw)), (unsigned)n);
+        if (!fused) {
+            hipLaunchKernelGGL(k_jpeg_fdct_batch, g1, dim3(256), 0, ctx->stream, a1);
+        } else if (fused->bpp == 2) {
+            if (fused->be) hipLaunchKernelGGL((k_jpeg_render_fdct<2, true>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
+            else hipLaunchKernelGGL((k_jpeg_render_fdct<2, false>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
+        } else {
+            hipLaunchKernelGGL((k_jpeg_render_fdct<1, false>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
+        }
     }
     hipLaunchKernelGGL(k_jpeg_block_bits, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a2);
     hipLaunchKernelGGL(k_jpeg_group_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a2b);
@@ -1404,6 +1559,15 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     hipLaunchKernelGGL(k_jpeg_stuff_batch, dim3((unsigned)est_groups, (unsigned)n), dim3(kGrp), 0, ctx->stream, a6);
     OMR_HIP(ctx, hipGetLastError());
     return OMR_OK;
+}
+
+// The unfused render -> JPEG path: B1 on rendered ARGB, B5 merging the render's per-tile status.
+static omr_status encode_jpeg_batch_ws_rstat(Ctx* ctx, const uint32_t* d_argb, int64_t tile_stride, int n, int W,
+                                             int H, float quality, uint8_t* d_out, uint64_t cap, uint64_t* d_offsets,
+                                             uint32_t* d_lengths, int32_t* d_status, const JpegBatchLayout& L,
+                                             const int32_t* rstat) {
+    return encode_jpeg_batch_ws(ctx, d_argb, tile_stride, n, W, H, quality, d_out, cap, d_offsets, d_lengths,
+                                d_status, L, nullptr, rstat);
 }
 
 static omr_status check_jpeg_batch(Ctx* ctx, const void* d_argb, int n, int W, int H, int64_t stride) {
@@ -1479,6 +1643,113 @@ static omr_status encode_jpeg_single_batched(Ctx* ctx, const uint32_t* d_argb, i
 }  // namespace omr
 
 extern "C" {
+
+}  // extern "C"
+
+namespace omr {
+
+// Render + JPEG of a batch (omr_render_jpeg_batch_*_device).  The fused path (F1 = render + B1 in
+// one kernel) covers 8/16-bit integer pixels with 1..4 active channels on tiles whose sides are
+// multiples of 16; anything else renders with K2 into a context buffer and encodes that.
+static omr_status render_jpeg_batch(Ctx* ctx, const omr_quantum_def* qdef, const omr_channel_binding* channels,
+                                    int32_t size_c, const void* d_base, int64_t tile_stride, int64_t chan_stride,
+                                    const void* const* d_ptrs, int32_t n, int64_t row_stride, int32_t pt,
+                                    int32_t be, int32_t W, int32_t H, int32_t fh, int32_t fv, float quality,
+                                    uint8_t* d_out, size_t cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                    int32_t* d_status) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (n <= 0 || n > (1 << 20)) return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: n_tiles out of range");
+    if (W <= 0 || H <= 0 || W > kJpegBatchMaxDim || H > kJpegBatchMaxDim)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG batch: tile dimensions must be 1..4096");
+    if (!d_out || !d_offsets || !d_lengths) return fail(ctx, OMR_INVALID_ARGUMENT, "null batch output");
+    if (!d_base && !d_ptrs) return fail(ctx, OMR_INVALID_ARGUMENT, "null plane batch");
+    if (row_stride == 0) row_stride = W;
+    if (row_stride < W) return fail(ctx, OMR_INVALID_ARGUMENT, "row stride smaller than width");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    std::unique_ptr<FusedPlanBuf, void (*)(FusedPlanBuf*)> fp(fused_plan_new(), fused_plan_free);
+    omr_status st = OMR_OK;
+    const bool plan_ok = render_fused_plan(ctx, qdef, channels, size_c, pt, fp.get(), &st);
+    if (st) return st;
+    const int bpp = bytes_per_pixel(pt);
+    const int64_t al = bpp == 2 ? 4 : 2;     // the fused loads read pixel pairs
+    const bool aligned = (row_stride * bpp) % al == 0 &&
+                         (!d_base || ((uintptr_t)d_base % al == 0 && tile_stride % al == 0 && chan_stride % al == 0));
+    const bool fused = plan_ok && W % 16 == 0 && H % 16 == 0 && aligned;
+    const size_t rstat_bytes = align_up((size_t)n * 4, 256);
+    if (fused) {
+        const size_t r_bytes = align_up(render_fused_ws_bytes(fp.get()), 256);
+        const JpegBatchLayout L = jpeg_batch_layout(W, H, n, r_bytes + rstat_bytes);
+        st = ensure_workspace(ctx, L.total);
+        if (st) return st;
+        FusedLaunch fl;
+        std::memset(&fl, 0, sizeof(fl));
+        st = render_fused_stage(ctx, fp.get(), 0, fl.args.R);
+        if (st) return st;
+        fl.args.sbase = static_cast<const uint8_t*>(d_base);
+        fl.args.planes = d_ptrs;
+        fl.args.strided = d_base ? 1 : 0;
+        fl.args.tile_stride = tile_stride;
+        fl.args.chan_stride = chan_stride;
+        fl.args.row_stride = row_stride;
+        fl.args.size_c = size_c;
+        fl.args.flip_h = fh ? 1 : 0;
+        fl.args.flip_v = fv ? 1 : 0;
+        fl.args.rstat = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(ctx->ws) + r_bytes);
+        fl.bpp = bpp;
+        fl.be = be != 0;
+        OMR_HIP(ctx, hipMemsetAsync(fl.args.rstat, 0, (size_t)n * 4, ctx->stream));
+        return encode_jpeg_batch_ws(ctx, nullptr, 0, n, W, H, quality, d_out, cap, d_offsets, d_lengths, d_status,
+                                    L, &fl);
+    }
+    // unfused: K1 + K2 into the context's ARGB buffer, then the batched encoder
+    const size_t argb_bytes = align_up((size_t)n * W * H * 4, 256);
+    st = ensure_aux(ctx, argb_bytes + rstat_bytes);
+    if (st) return st;
+    uint32_t* argb = static_cast<uint32_t*>(ctx->aux);
+    int32_t* rstat = reinterpret_cast<int32_t*>(static_cast<uint8_t*>(ctx->aux) + argb_bytes);
+    omr_ctx* cx = static_cast<omr_ctx*>(ctx);
+    st = d_base ? omr_render_batch_strided_device(cx, qdef, channels, size_c, d_base, tile_stride, chan_stride, n,
+                                                  row_stride, pt, be, W, H, fh, fv, argb, rstat)
+                : omr_render_batch_device(cx, qdef, channels, size_c, d_ptrs, n, row_stride, pt, be, W, H, fh, fv,
+                                          argb, rstat);
+    if (st) return st;
+    const JpegBatchLayout L = jpeg_batch_layout(W, H, n, 0);
+    st = ensure_workspace(ctx, L.total);
+    if (st) return st;
+    return encode_jpeg_batch_ws_rstat(ctx, argb, (int64_t)W * H, n, W, H, quality, d_out, cap, d_offsets, d_lengths,
+                                      d_status, L, rstat);
+}
+
+}  // namespace omr
+
+extern "C" {
+
+omr_status omr_render_jpeg_batch_strided_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                                const omr_channel_binding* channels, int32_t size_c,
+                                                const void* d_base, int64_t tile_stride_bytes,
+                                                int64_t channel_stride_bytes, int32_t n_tiles, int64_t row_stride,
+                                                int32_t pixel_type, int32_t big_endian, int32_t width, int32_t height,
+                                                int32_t flip_h, int32_t flip_v, float quality, uint8_t* d_out,
+                                                size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                                int32_t* d_status) {
+    if (!d_base) return ctx ? omr::fail(ctx, OMR_INVALID_ARGUMENT, "null batch base") : OMR_INVALID_ARGUMENT;
+    return omr::render_jpeg_batch(ctx, qdef, channels, size_c, d_base, tile_stride_bytes, channel_stride_bytes,
+                                  nullptr, n_tiles, row_stride, pixel_type, big_endian, width, height, flip_h, flip_v,
+                                  quality, d_out, out_cap, d_offsets, d_lengths, d_status);
+}
+
+omr_status omr_render_jpeg_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
+                                        const omr_channel_binding* channels, int32_t size_c,
+                                        const void* const* d_plane_ptrs, int32_t n_tiles, int64_t row_stride,
+                                        int32_t pixel_type, int32_t big_endian, int32_t width, int32_t height,
+                                        int32_t flip_h, int32_t flip_v, float quality, uint8_t* d_out,
+                                        size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                        int32_t* d_status) {
+    if (!d_plane_ptrs) return ctx ? omr::fail(ctx, OMR_INVALID_ARGUMENT, "null plane table") : OMR_INVALID_ARGUMENT;
+    return omr::render_jpeg_batch(ctx, qdef, channels, size_c, nullptr, 0, 0, d_plane_ptrs, n_tiles, row_stride,
+                                  pixel_type, big_endian, width, height, flip_h, flip_v, quality, d_out, out_cap,
+                                  d_offsets, d_lengths, d_status);
+}
 
 omr_status omr_encode_jpeg_batch_device(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
                                         int32_t n_tiles, int32_t width, int32_t height, float quality,

@@ -1,0 +1,79 @@
+// omr_k2.h — K2's per-channel quantization as device helpers, shared by the render kernel
+// (omr_render.hip) and the fused render -> JPEG kernel (omr_jpeg.hip), plus the host interface
+// the fused path uses to prepare a render without launching K2.
+#pragma once
+
+#include "omr_device.h"
+
+namespace omr {
+
+// Per-active-channel parameters K2 reads from the kernarg segment (scalar loads, no
+// per-pixel memory traffic for settings).
+struct K2Chan {
+    int32_t index;      // plane-table column (channel index)
+    int32_t mode;       // kModeTable8 / kModeLinear16 / kModeLut16 / kModeEval
+    int32_t lo, hi;     // window thresholds for integer x: x < lo -> cdStart, x >= hi -> cdEnd
+    int32_t gmin, gmax; // LUT domain
+    int32_t check;      // pixel values may fall outside [gmin, gmax] (QuantizationException)
+    int32_t second;     // the a1*v + cdStart rounding stage is not the identity
+    double ws, a0, a1;
+    uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
+};
+
+
+__device__ __forceinline__ uint32_t clamp_fields(uint32_t a) {
+    const uint32_t r = min(a >> 20, 255u), g = min((a >> 10) & 1023u, 255u), b = min(a & 1023u, 255u);
+    return (r << 20) | (g << 10) | b;
+}
+
+// Exact LUT entry of a 16-bit pixel for the linear family, branch-free:
+// v = round(a0*(x - ws)) (Java Math.round), window ends by integer compare.
+__device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, int cds8, int cde8) {
+    const double d = p.a0 * ((double)x - p.ws);
+    int v = __double2int_rz(floor(d + 0.5));          // exact in the window (d in [0, bitRes])
+    v = (d == 0x1.fffffffffffffp-2) ? 0 : v;
+    if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);   // uniform branch
+    v = x < p.lo ? cds8 : v;
+    v = x >= p.hi ? cde8 : v;
+    return (uint32_t)v & 0xFFu;
+}
+
+// Default QuantumDef (cd 0..255, bitRes 255), window start < end, and no window pixel at
+// Java's 0.49999999999999994 special case (checked on the host): round(a0*(x - ws)) clamped
+// to [0,255] equals the LUT entry for every x (below the window d < 0 -> 0, above it
+// d >= 255 -> 255), so the window compares fold into one med3.
+__device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
+    const double d = p.a0 * ((double)x - p.ws);
+    const int v = __double2int_rz(floor(d + 0.5));
+    return (uint32_t)min(max(v, 0), 255);
+}
+
+
+// A render prepared for the fused render -> JPEG path (omr_jpeg.hip): the plan is staged and
+// the contribution tables (K1) and byte LUTs built on the context stream; the fused kernel
+// quantizes + composites each pixel as K2 does (same helpers, same tables) and encodes it.
+constexpr int kFusedMaxActive = 4;
+enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4 };
+struct FusedRender {
+    K2Chan ch[kFusedMaxActive];
+    const uint32_t* contrib;     // [n_active][256] (workspace)
+    const uint8_t* ws_base;      // workspace base (kModeLut16 byte LUTs)
+    int32_t* flag;               // sticky quantization-error word
+    int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
+    int32_t pad[2];
+};
+
+// Host side (omr_render.hip).  render_fused_plan: true when the fused kernel covers these
+// settings (8/16-bit integer pixels, 1..4 active channels); *st != OMR_OK is a request error.
+// Opaque plan storage: the caller passes a FusedPlanBuf it owns.
+struct FusedPlanBuf;
+FusedPlanBuf* fused_plan_new();
+void fused_plan_free(FusedPlanBuf* fp);
+bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch, int32_t size_c,
+                       int32_t pixel_type, FusedPlanBuf* fp, omr_status* st);
+size_t render_fused_ws_bytes(const FusedPlanBuf* fp);
+// Stage the plan at ctx->ws + ws_off (the workspace must hold render_fused_ws_bytes from there),
+// build the tables on the context stream and fill `out`.
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& out);
+
+}  // namespace omr

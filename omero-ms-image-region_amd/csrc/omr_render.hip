@@ -17,6 +17,7 @@
 //    channel contributions from LDS with plain integer adds, clamps and packs ARGB, and
 //    writes it at the flipped position (the flip costs nothing).  HBM-bound.
 #include "omr_device.h"
+#include "omr_k2.h"
 
 namespace omr {
 
@@ -109,19 +110,6 @@ __global__ void __launch_bounds__(256) k_build_lut(const RenderPlan* __restrict_
 }
 
 // ------------------------------------------------------------------------------- K2
-// Per-active-channel parameters K2 reads from the kernarg segment (scalar loads, no
-// per-pixel memory traffic for settings).
-struct K2Chan {
-    int32_t index;      // plane-table column (channel index)
-    int32_t mode;       // kModeTable8 / kModeLinear16 / kModeLut16 / kModeEval
-    int32_t lo, hi;     // window thresholds for integer x: x < lo -> cdStart, x >= hi -> cdEnd
-    int32_t gmin, gmax; // LUT domain
-    int32_t check;      // pixel values may fall outside [gmin, gmax] (QuantizationException)
-    int32_t second;     // the a1*v + cdStart rounding stage is not the identity
-    double ws, a0, a1;
-    uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
-};
-
 enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3, kK2Fast16 = 4,
                     kK2Thresh = 5 /* float / 32-bit, every channel kModeThresh: no double math */ };
 
@@ -227,33 +215,6 @@ __device__ __forceinline__ double pixel_double(const Chunk<BPP, VEC>& c, int j) 
         if constexpr (BE) { const uint32_t t = bswap32(lo); lo = bswap32(hi); hi = t; }
         return __hiloint2double((int)hi, (int)lo);
     }
-}
-
-__device__ __forceinline__ uint32_t clamp_fields(uint32_t a) {
-    const uint32_t r = min(a >> 20, 255u), g = min((a >> 10) & 1023u, 255u), b = min(a & 1023u, 255u);
-    return (r << 20) | (g << 10) | b;
-}
-
-// Exact LUT entry of a 16-bit pixel for the linear family, branch-free:
-// v = round(a0*(x - ws)) (Java Math.round), window ends by integer compare.
-__device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, int cds8, int cde8) {
-    const double d = p.a0 * ((double)x - p.ws);
-    int v = __double2int_rz(floor(d + 0.5));          // exact in the window (d in [0, bitRes])
-    v = (d == 0x1.fffffffffffffp-2) ? 0 : v;
-    if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);   // uniform branch
-    v = x < p.lo ? cds8 : v;
-    v = x >= p.hi ? cde8 : v;
-    return (uint32_t)v & 0xFFu;
-}
-
-// Default QuantumDef (cd 0..255, bitRes 255), window start < end, and no window pixel at
-// Java's 0.49999999999999994 special case (checked on the host): round(a0*(x - ws)) clamped
-// to [0,255] equals the LUT entry for every x (below the window d < 0 -> 0, above it
-// d >= 255 -> 255), so the window compares fold into one med3.
-__device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
-    const double d = p.a0 * ((double)x - p.ws);
-    const int v = __double2int_rz(floor(d + 0.5));
-    return (uint32_t)min(max(v, 0), 255);
 }
 
 // General q(x) in double (float / 32-bit types): Java semantics, selects instead of branches.
@@ -1013,6 +974,86 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         }
     }
     OMR_HIP(ctx, e);
+    return OMR_OK;
+}
+
+// ---- fused render -> JPEG (omr_k2.h): the plan and K1 of a render, K2 left to the caller
+struct FusedPlanBuf {
+    PreparedPlan pp;
+    RenderLayout L;
+    int32_t pixel_type = 0;
+    int32_t mode = 0;
+};
+
+FusedPlanBuf* fused_plan_new() { return new FusedPlanBuf(); }
+void fused_plan_free(FusedPlanBuf* fp) { delete fp; }
+size_t render_fused_ws_bytes(const FusedPlanBuf* fp) { return fp->L.total; }
+
+bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch, int32_t size_c,
+                       int32_t pixel_type, FusedPlanBuf* fp, omr_status* st) {
+    *st = prepare_plan(ctx, q, ch, size_c, pixel_type, fp->pp);
+    if (*st) return false;
+    const int bpp = bytes_per_pixel(pixel_type);
+    const int na = fp->pp.plan.n_active;
+    if (bpp > 2 || na < 1 || na > kFusedMaxActive) return false;
+    fp->pixel_type = pixel_type;
+    fp->L = layout_for(fp->pp, 0);
+    bool all_linear = true, all_fast = true;
+    for (int i = 0; i < na; ++i) {
+        const ChanParam& c = fp->pp.plan.ch[i];
+        if (c.mode != kModeLinear16) all_linear = false;
+        if (!(c.mode == kModeLinear16 && fast_linear_ok(c, fp->pp.plan))) all_fast = false;
+    }
+    fp->mode = bpp == 1 ? kFusedTable8 : all_fast ? kFusedFast16 : all_linear ? kFusedLinear16 : kFusedMixed16;
+    return true;
+}
+
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& F) {
+    PreparedPlan& pp = fp->pp;
+    const RenderLayout& L = fp->L;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws) + ws_off;
+    RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
+    uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
+    const int na = pp.plan.n_active;
+    for (int a = 0; a < na; ++a) pp.plan.ch[a].lut_off += ws_off + L.lut_off;   // relative to ctx->ws
+    omr_status st = stage_h2d(ctx, d_plan, &pp.plan, pp.plan_bytes);
+    if (st) return st;
+    hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
+                       fp->pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
+    OMR_HIP(ctx, hipGetLastError());
+    if (pp.n_lut > 0) {
+        hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan,
+                           static_cast<uint8_t*>(ctx->ws));
+        OMR_HIP(ctx, hipGetLastError());
+    }
+    std::memset(&F, 0, sizeof(F));
+    double tlo, thi;
+    type_bounds(fp->pixel_type, tlo, thi);
+    for (int i = 0; i < na; ++i) {
+        const ChanParam& c = pp.plan.ch[i];
+        K2Chan& k = F.ch[i];
+        k.index = c.index;
+        k.mode = c.mode;
+        k.lo = c.lo;
+        k.hi = c.hi;
+        k.gmin = c.gmin;
+        k.gmax = c.gmax;
+        k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
+        k.second = c.second;
+        k.ws = c.ws;
+        k.a0 = c.a0;
+        k.a1 = c.a1;
+        k.lut_off = c.lut_off;
+    }
+    F.contrib = d_contrib;
+    F.ws_base = static_cast<const uint8_t*>(ctx->ws);
+    F.flag = ctx->d_flag;
+    F.n_active = na;
+    F.mode = fp->mode;
+    F.cd_start = pp.plan.cd_start;
+    F.cds8 = pp.plan.cd_start & 0xFF;
+    F.cde8 = pp.plan.cd_end & 0xFF;
+    F.is_signed = fp->pixel_type == OMR_PIXELS_INT8 || fp->pixel_type == OMR_PIXELS_INT16;
     return OMR_OK;
 }
 

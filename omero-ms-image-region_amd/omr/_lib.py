@@ -170,6 +170,10 @@ _SIGS = {
     "omr_encode_jpeg_batch_device": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
     "omr_encode_jpeg_batch": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp]),
     "omr_jpeg_quant_tables": (_i32, [_f32, _vp, _vp]),
+    "omr_render_jpeg_batch_strided_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i64, _i32, _i64, _i32, _i32,
+                                                    _i32, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
+    "omr_render_jpeg_batch_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
+                                            _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
     "omr_jpeg_quant_tables_sem": (_i32, [_f32, ctypes.c_uint32, _vp, _vp]),
     "omr_tiff_max_bytes": (_sz, [_i32, _i32]),
     "omr_encode_tiff": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),

@@ -258,6 +258,27 @@ class Context:
                                                float(quality), _ptr(d_out), d_out.numel(), _ptr(d_offsets),
                                                _ptr(d_lengths), _ptr(d_status)), self.h)
 
+    def render_jpeg_batch_strided_device(self, qdef, channels, d_base, tile_stride, channel_stride, n_tiles,
+                                         pixel_type, width, height, quality, d_out, d_offsets, d_lengths,
+                                         d_status=None, big_endian=False, flip_h=False, flip_v=False, row_stride=0,
+                                         bindings=None):
+        """Render + JPEG of a strided plane batch in one call (fused F1 kernel where it applies):
+        files packed in d_out, as encode_jpeg_batch_device."""
+        arr, keep = make_bindings(channels) if bindings is None else bindings
+        check(lib.omr_render_jpeg_batch_strided_device(
+            self.h, ctypes.byref(qdef), arr, len(channels), _ptr(d_base), tile_stride, channel_stride, n_tiles,
+            row_stride, pixel_type, int(big_endian), width, height, int(flip_h), int(flip_v), float(quality),
+            _ptr(d_out), d_out.numel(), _ptr(d_offsets), _ptr(d_lengths), _ptr(d_status)), self.h)
+
+    def render_jpeg_batch_device(self, qdef, channels, d_plane_ptrs, n_tiles, pixel_type, width, height, quality,
+                                 d_out, d_offsets, d_lengths, d_status=None, big_endian=False, flip_h=False,
+                                 flip_v=False, row_stride=0, bindings=None):
+        arr, keep = make_bindings(channels) if bindings is None else bindings
+        check(lib.omr_render_jpeg_batch_device(
+            self.h, ctypes.byref(qdef), arr, len(channels), _ptr(d_plane_ptrs), n_tiles, row_stride, pixel_type,
+            int(big_endian), width, height, int(flip_h), int(flip_v), float(quality), _ptr(d_out), d_out.numel(),
+            _ptr(d_offsets), _ptr(d_lengths), _ptr(d_status)), self.h)
+
     def encode_jpeg_batch(self, d_argb, n_tiles, width, height, quality, cap=None, tile_stride=0):
         """Batch encode device ARGB tiles -> list of JPEG byte strings (one host sync)."""
         if cap is None:

@@ -1,0 +1,152 @@
+"""Fused render -> JPEG (omr_render_jpeg_batch_*_device): render_image_region's default response
+(renderAsPackedInt + flip + compressToStream, ImageRegionRequestHandler.java:559-582) for a batch
+of HBM-resident tiles in one call.  Every file must be byte-identical to the CPU restatement's
+render + JPEG of the same tile — through the fused F1 kernel (8/16-bit, 1..4 channels, sides
+multiple of 16) and through the K2 + B1 fallback (ragged tiles, float pixels, > 4 channels)."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from omr import _lib
+from omr.context import make_qdef
+from omr.renderer import f32
+from omr.synthetic import c2_channels, tile_u16
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, chans, tiles, pt, w, h, q=0.9, model="rgb", be=False, flip=(False, False), table=False,
+         qd_kw=None):
+    """tiles: [n][c] numpy planes (file byte order already applied).  Returns (files, status)."""
+    import torch
+    n, c = len(tiles), len(tiles[0])
+    raw = np.stack([np.stack([np.ascontiguousarray(p).view(np.uint8).reshape(-1) for p in t]) for t in tiles])
+    data = torch.from_numpy(raw.copy()).to("cuda")
+    plane = raw.shape[2]
+    cap = n * (w * h * 4 + 4096)
+    d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    stat = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    qd = make_qdef(model, **(qd_kw or {}))
+    torch.cuda.synchronize()
+    if table:
+        base = data.data_ptr()
+        ptrs = torch.tensor([[base + (t * c + k) * plane for k in range(c)] for t in range(n)], dtype=torch.int64,
+                            device="cuda")
+        torch.cuda.synchronize()
+        ctx.render_jpeg_batch_device(qd, chans, ptrs, n, pt, w, h, q, d_out, offs, lens, stat, big_endian=be,
+                                     flip_h=flip[0], flip_v=flip[1])
+    else:
+        ctx.render_jpeg_batch_strided_device(qd, chans, data, c * plane, plane, n, pt, w, h, q, d_out, offs, lens,
+                                             stat, big_endian=be, flip_h=flip[0], flip_v=flip[1])
+    try:
+        ctx.synchronize()
+    except _lib.OmrError as e:
+        if e.status != _lib.QUANTIZATION:
+            raise
+    o, ln, st = offs.cpu().numpy(), lens.cpu().numpy(), stat.cpu().numpy()
+    buf = d_out.cpu().numpy()
+    return [buf[o[i]:o[i] + ln[i]].tobytes() for i in range(n)], st
+
+
+def _expect(chans, tiles, pt, w, h, q=0.9, model="rgb", be=False, flip=(False, False), qdef=None):
+    out = []
+    for t in tiles:
+        st, argb = O.render(chans, t, pt, w, h, model=model, big_endian=be, flip_h=flip[0], flip_v=flip[1],
+                            qdef=qdef)
+        assert st == 0
+        out.append(O.encode_jpeg(argb, w, h, q))
+    return out
+
+
+@pytest.mark.parametrize("table", [False, True])
+def test_c2_full_size_fused_byte_identical(ctx, table):
+    w = h = 1024
+    tiles = [[p.astype(">u2") for p in tile_u16(60 + t, 4, h, w)] for t in range(3)]
+    chans = c2_channels(4)
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, table=table)
+    assert (st == 0).all()
+    assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h, be=True)
+
+
+@pytest.mark.parametrize("flip", [(True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("be", [False, True])
+def test_flips_and_byte_order(ctx, flip, be):
+    w, h = 256, 160
+    tiles = [[(p.astype(">u2") if be else p) for p in tile_u16(70 + t, 3, h, w)] for t in range(2)]
+    chans = c2_channels(3)
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h, be=be, flip=flip, q=0.8)
+    assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h, be=be, flip=flip, q=0.8)
+
+
+@pytest.mark.parametrize("n_ch", [1, 2, 4])
+def test_u8_greyscale_and_colour(ctx, n_ch):
+    w, h = 128, 96
+    rng = np.random.default_rng(n_ch)
+    tiles = [[rng.integers(0, 256, (h, w)).astype(np.uint8) for _ in range(n_ch)] for _ in range(3)]
+    chans = [{"input_start": f32(10.5), "input_end": f32(240.0), "global_min": 0.0, "global_max": 255.0,
+              "rgba": [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255), (200, 100, 50, 128)][k]}
+             for k in range(n_ch)]
+    for model in ("greyscale", "rgb"):
+        files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT8, w, h, model=model, q=0.75)
+        assert files == _expect(chans, tiles, _lib.PIXELS_UINT8, w, h, model=model, q=0.75)
+
+
+def test_signed_reverse_lut_codomain_and_lut16(ctx):
+    """int16 with reverse + a .lut channel (Linear16 with the second rounding stage under a
+    non-default codomain), and a polynomial channel (byte-LUT gather, Mixed16)."""
+    w, h = 192, 128
+    rng = np.random.default_rng(4)
+    tiles = [[rng.integers(-2000, 2000, (h, w)).astype(np.int16) for _ in range(3)] for _ in range(2)]
+    lut = np.concatenate([np.arange(256), 255 - np.arange(256), (np.arange(256) * 3) % 256]).astype(np.uint8)
+    chans = [{"input_start": f32(-1500.5), "input_end": f32(1800.0), "global_min": -32768.0, "global_max": 32767.0,
+              "rgba": (0, 0, 255, 255), "reverse": True},
+             {"input_start": f32(-100.0), "input_end": f32(1000.0), "global_min": -32768.0, "global_max": 32767.0,
+              "lut": lut},
+             {"input_start": f32(1.0), "input_end": f32(1900.0), "global_min": -32768.0, "global_max": 32767.0,
+              "rgba": (255, 255, 0, 255), "family": _lib.FAMILY_POLYNOMIAL, "coefficient": 0.5}]
+    for qd_kw in (None, {"cd_start": 20, "cd_end": 230}):
+        files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h, qd_kw=qd_kw)
+        assert files == _expect(chans, tiles, _lib.PIXELS_INT16, w, h, qdef=make_qdef("rgb", **(qd_kw or {})))
+
+
+@pytest.mark.parametrize("shape", [(100, 60), (1024, 1000), (17, 16)])
+def test_ragged_tiles_take_the_unfused_path(ctx, shape):
+    w, h = shape
+    tiles = [[p.astype(">u2") for p in tile_u16(80 + t, 4, h, w)] for t in range(2)]
+    chans = c2_channels(4)
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, False))
+    assert (st == 0).all()
+    assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, False))
+
+
+def test_float_and_many_channels_unfused(ctx):
+    w, h = 128, 64
+    rng = np.random.default_rng(5)
+    tiles = [[rng.uniform(-5, 300, (h, w)).astype(np.float32) for _ in range(2)] for _ in range(2)]
+    chans = [{"input_start": 0.0, "input_end": 255.0, "rgba": (255, 0, 0, 255)},
+             {"input_start": 10.0, "input_end": 200.0, "rgba": (0, 255, 0, 255)}]
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_FLOAT, w, h)
+    assert files == _expect(chans, tiles, _lib.PIXELS_FLOAT, w, h)
+    tiles = [[p for p in tile_u16(90 + t, 6, h, w)] for t in range(2)]
+    chans = c2_channels(4) + c2_channels(2)
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h)
+    assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_quantization_error_flags_its_tile(ctx, fused):
+    w, h = (128, 64) if fused else (120, 64)
+    tiles = [[p.copy() for p in tile_u16(95 + t, 2, h, w)] for t in range(3)]
+    for t in tiles:
+        for p in t:
+            np.minimum(p, 60000, out=p)
+    tiles[1][1][5, 7] = 65000
+    chans = c2_channels(2)
+    for c in chans:
+        c["global_max"] = 60000.0
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h)
+    assert st.tolist() == [0, _lib.QUANTIZATION, 0]
+    exp = _expect(chans, [tiles[0], tiles[2]], _lib.PIXELS_UINT16, w, h)
+    assert files[0] == exp[0] and files[2] == exp[1]
