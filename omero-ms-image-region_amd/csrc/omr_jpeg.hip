@@ -798,7 +798,7 @@ struct FusedArgs {
     int32_t* rstat;              // [tile] OMR_QUANTIZATION when a pixel left its LUT domain
 };
 
-template <int BPP, bool BE>
+template <int BPP, bool BE, int MODE, int NA>
 struct PlaneSource {
     const FusedArgs& F;
     const uint32_t* s_contrib;   // LDS [n_active][256]
@@ -822,8 +822,7 @@ struct PlaneSource {
         const int64_t r0 = (int64_t)(F.flip_v ? H - 1 - y0 : y0) * F.row_stride + sx;
         const int64_t r1 = (int64_t)(F.flip_v ? H - 2 - y0 : y0 + 1) * F.row_stride + sx;
 #pragma unroll
-        for (int a = 0; a < kFusedMaxActive; ++a) {
-            if (a >= F.R.n_active) break;                                // uniform
+        for (int a = 0; a < NA; ++a) {
             if constexpr (BPP == 2) {
                 raw[a][0] = *reinterpret_cast<const uint32_t*>(base[a] + r0 * 2);
                 raw[a][1] = *reinterpret_cast<const uint32_t*>(base[a] + r1 * 2);
@@ -847,9 +846,9 @@ struct PlaneSource {
             const K2Chan& p = F.R.ch[a];
             if (p.check) err |= (x < p.gmin) | (x > p.gmax);
             uint32_t v;
-            if (F.R.mode == kFusedFast16) {                            // uniform branches
+            if constexpr (MODE == kFusedFast16) {
                 v = fast16(x, p);
-            } else if (F.R.mode == kFusedLinear16 || p.mode == kModeLinear16) {
+            } else if (MODE == kFusedLinear16 || p.mode == kModeLinear16) {   // uniform
                 v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
             } else {
                 const int xi = min(max(x, p.gmin), p.gmax);
@@ -862,8 +861,7 @@ struct PlaneSource {
         uint32_t acc[4] = {0, 0, 0, 0};
         const int jl = F.flip_h ? 1 : 0;        // which half of the pair is the left output pixel
 #pragma unroll
-        for (int a = 0; a < kFusedMaxActive; ++a) {
-            if (a >= F.R.n_active) break;
+        for (int a = 0; a < NA; ++a) {
             acc[0] += entry(a, raw[a][0], jl);
             acc[1] += entry(a, raw[a][0], jl ^ 1);
             acc[2] += entry(a, raw[a][1], jl);
@@ -1027,15 +1025,15 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
 
 // F1: fused render + B1 (see PlaneSource).  The contribution tables are staged once per
 // workgroup; a pixel outside its channel's LUT domain flags the tile (QuantizationException).
-template <int BPP, bool BE>
+template <int BPP, bool BE, int MODE, int NA>
 __global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F) {
     __shared__ int s[4][6 * kBS + 8];
     __shared__ uint8_t s_acsize[2][256];
     __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
     for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
-    for (int i = threadIdx.x; i < F.R.n_active * 256; i += 256) s_contrib[i] = F.R.contrib[i];
+    for (int i = threadIdx.x; i < NA * 256; i += 256) s_contrib[i] = F.R.contrib[i];
     __syncthreads();
-    PlaneSource<BPP, BE> src(F, s_contrib, blockIdx.y, A.W, A.H);
+    PlaneSource<BPP, BE, MODE, NA> src(F, s_contrib, blockIdx.y, A.W, A.H);
     b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
     if (__ballot(src.err)) {
         if ((threadIdx.x & 63) == 0) {
@@ -1485,6 +1483,31 @@ static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
     return L;
 }
 
+template <int BPP, bool BE, int MODE>
+static void launch_render_fdct_na(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f) {
+    switch (f.R.n_active) {
+    case 1: hipLaunchKernelGGL((k_jpeg_render_fdct<BPP, BE, MODE, 1>), g, dim3(256), 0, st, a1, f); break;
+    case 2: hipLaunchKernelGGL((k_jpeg_render_fdct<BPP, BE, MODE, 2>), g, dim3(256), 0, st, a1, f); break;
+    case 3: hipLaunchKernelGGL((k_jpeg_render_fdct<BPP, BE, MODE, 3>), g, dim3(256), 0, st, a1, f); break;
+    default: hipLaunchKernelGGL((k_jpeg_render_fdct<BPP, BE, MODE, 4>), g, dim3(256), 0, st, a1, f); break;
+    }
+}
+
+template <bool BE>
+static void launch_render_fdct_mode(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f) {
+    switch (f.R.mode) {
+    case kFusedFast16: launch_render_fdct_na<2, BE, kFusedFast16>(g, st, a1, f); break;
+    case kFusedLinear16: launch_render_fdct_na<2, BE, kFusedLinear16>(g, st, a1, f); break;
+    default: launch_render_fdct_na<2, BE, kFusedMixed16>(g, st, a1, f); break;
+    }
+}
+
+static void launch_render_fdct(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f, int bpp, bool be) {
+    if (bpp == 1) launch_render_fdct_na<1, false, kFusedTable8>(g, st, a1, f);
+    else if (be) launch_render_fdct_mode<true>(g, st, a1, f);
+    else launch_render_fdct_mode<false>(g, st, a1, f);
+}
+
 // Fused render -> JPEG: F1 instead of B1 (fused != nullptr; d_argb unused).
 struct FusedLaunch {
     FusedArgs args;
@@ -1540,11 +1563,8 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
         const dim3 g1((unsigned)((L.n_mcu + 4 * a1.mpw - 1) / (4 * a1.mpw)), (unsigned)n);
         if (!fused) {
             hipLaunchKernelGGL(k_jpeg_fdct_batch, g1, dim3(256), 0, ctx->stream, a1);
-        } else if (fused->bpp == 2) {
-            if (fused->be) hipLaunchKernelGGL((k_jpeg_render_fdct<2, true>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
-            else hipLaunchKernelGGL((k_jpeg_render_fdct<2, false>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
         } else {
-            hipLaunchKernelGGL((k_jpeg_render_fdct<1, false>), g1, dim3(256), 0, ctx->stream, a1, fused->args);
+            launch_render_fdct(g1, ctx->stream, a1, fused->args, fused->bpp, fused->be);
         }
     }
     hipLaunchKernelGGL(k_jpeg_block_bits, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a2);

@@ -41,10 +41,12 @@ __device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, in
 // Default QuantumDef (cd 0..255, bitRes 255), window start < end, and no window pixel at
 // Java's 0.49999999999999994 special case (checked on the host): round(a0*(x - ws)) clamped
 // to [0,255] equals the LUT entry for every x (below the window d < 0 -> 0, above it
-// d >= 255 -> 255), so the window compares fold into one med3.
+// d >= 255 -> 255), so the window compares fold into one med3.  Truncation stands in for the
+// floor: they differ only for d + 0.5 < 0, where both clamp to 0 (v_cvt_i32_f64 saturates, so
+// d + 0.5 >= 2^31 still clamps to 255).
 __device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
     const double d = p.a0 * ((double)x - p.ws);
-    const int v = __double2int_rz(floor(d + 0.5));
+    const int v = __double2int_rz(d + 0.5);
     return (uint32_t)min(max(v, 0), 255);
 }
 
