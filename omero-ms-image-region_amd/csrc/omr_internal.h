@@ -130,6 +130,13 @@ omr_status stage_h2d(Ctx* c, void* dst, const void* src, size_t bytes);
 omr_status stage_h2d2(Ctx* c, void* dst1, const void* src1, size_t n1, void* dst2, const void* src2, size_t n2);
 int bytes_per_pixel(int32_t pixel_type);
 // K3 launch over up to 32 stacks (omr_project.hip).
+struct FusedRender;
+// The fused projection glue (omr_project.hip, K3R): stacks[a] per rendered channel in plan order;
+// *done = false when it does not apply (the caller projects with K3 and renders with K2).
+omr_status enqueue_project_render(Ctx* ctx, const void* const* stacks, const FusedRender& R, int32_t pixel_type,
+                                  int32_t be_in, int32_t size_x, int32_t size_y, int32_t algorithm, int32_t start,
+                                  int32_t end, int32_t stepping, int32_t flip_h, int32_t flip_v, uint32_t* d_out,
+                                  bool* done);
 omr_status validate_projection_args(Ctx* c, int32_t pixel_type, int32_t size_x, int32_t size_y,
                                     int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
                                     int32_t stepping);

@@ -7,6 +7,7 @@
 // The flips replace ImageRegionRequestHandler.flip (:616-642) and
 // ShapeMaskRequestHandler.flip (:128-154) for callers holding an already-rendered buffer.
 #include "omr_device.h"
+#include "omr_k2.h"
 
 namespace omr {
 
@@ -275,6 +276,205 @@ __global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter)
     p32x4 q;
     __builtin_memcpy(&q, o, 16);
     ((OMR_GLOBAL p32x4*)(void*)(A.outs[s]))[c] = q;
+}
+
+// K3R: the projection glue (ImageRegionRequestHandler.java:506-559) in one kernel — every active
+// channel's stack projected and the projected pixel rendered (quantize, codomain, colour,
+// composite, flip) without the projected planes going through HBM.  A workgroup owns 64 16-byte
+// chunks (512 pixels at 16 bits) of the plane for every channel; its 4 waves take consecutive
+// quarters of the z range (exact: max is order-free, integer sums are exact), combine through
+// LDS, and each thread then narrows (PixelData.setPixelValue, as K3 stores), quantizes (K2's
+// helpers and contribution tables) and composites 2 pixels.
+struct K3RArgs {
+    const uint8_t* stacks[kFusedMaxActive];   // per active channel (plan order)
+    uint32_t* out;
+    FusedRender R;
+    int32_t start, stepping, width, height, flip_h, flip_v, mean;
+    uint32_t chunks, n_iter;
+};
+
+template <typename T, bool BEI, bool MAX, bool FAST>
+__global__ void __launch_bounds__(kBlock) k_project_render(K3RArgs A) {
+    using U = typename Raw<T>::U;
+    constexpr int V = VecPx<T>::V;                      // 8 (16-bit) or 16 (8-bit) pixels per chunk
+    using Part = typename std::conditional<MAX, T, typename Acc32<T>::type>::type;
+    __shared__ Part s_part[4][kFusedMaxActive][64 * V];
+    __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
+    const int na = A.R.n_active;
+    for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.R.contrib[i];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t c = blockIdx.x * 64 + lane;
+    const uint32_t cc = min(c, A.chunks - 1);
+    const uint64_t pchunks = (uint64_t)A.chunks * (uint64_t)A.stepping;
+    const uint32_t i0 = (uint32_t)((uint64_t)A.n_iter * wave / 4), i1 = (uint32_t)((uint64_t)A.n_iter * (wave + 1) / 4);
+#pragma unroll
+    for (int a = 0; a < kFusedMaxActive; ++a) {
+        if (a >= na) break;                                         // uniform
+        Part acc[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) acc[j] = (Part)0;
+        const OMR_GLOBAL p32x4* p = (const OMR_GLOBAL p32x4*)(const void*)(A.stacks[a]) + cc +
+                                    (uint64_t)A.start * A.chunks + (uint64_t)i0 * pchunks;
+        auto fold = [&](const p32x4 q) {
+            U u[V];
+            VecPx<T>::split(q, u);
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                const T v = px_of<T, BEI>(u[j]);
+                if constexpr (MAX) { if (v > acc[j]) acc[j] = v; }   // stackValue > projectedValue (:187)
+                else acc[j] += (Part)v;
+            }
+        };
+        uint32_t i = i0;
+        for (; i + 8 <= i1; i += 8, p += 8 * pchunks) {
+            p32x4 q[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) q[k] = __builtin_nontemporal_load(p + k * pchunks);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) fold(q[k]);
+        }
+        for (; i < i1; ++i, p += pchunks) fold(__builtin_nontemporal_load(p));
+#pragma unroll
+        for (int j = 0; j < V; ++j) s_part[wave][a][lane * V + j] = acc[j];
+    }
+    __syncthreads();
+    // thread t renders pixels 2t, 2t+1 of the workgroup's 64*V (16-bit: 512) pixels; 8-bit
+    // chunks hold 1024 pixels, so each thread takes 2 pairs
+    const uint64_t plane = (uint64_t)A.chunks * V;
+#pragma unroll
+    for (int rep = 0; rep < V / 8; ++rep) {
+        const uint32_t lp = (rep * kBlock + threadIdx.x) * 2;      // pixel pair index within the block
+        const uint64_t px = (uint64_t)blockIdx.x * 64 * V + lp;
+        if (px >= plane) break;
+        uint32_t accp[2] = {0, 0};
+        bool err = false;
+#pragma unroll
+        for (int a = 0; a < kFusedMaxActive; ++a) {
+            if (a >= na) break;
+            const K2Chan& k = A.R.ch[a];
+            const uint32_t* tab = s_contrib + a * 256;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                T t;
+                if constexpr (MAX) {
+                    Part m = s_part[0][a][lp + j];
+#pragma unroll
+                    for (int w = 1; w < 4; ++w) { const Part v = s_part[w][a][lp + j]; if (v > m) m = v; }
+                    t = m;
+                } else {
+                    Part sum = s_part[0][a][lp + j] + s_part[1][a][lp + j] + s_part[2][a][lp + j] +
+                               s_part[3][a][lp + j];
+                    double v = (double)sum;
+                    if (A.mean) v = v / (double)A.n_iter;
+                    if (v > type_max<T>()) v = type_max<T>();
+                    t = narrow<T>(v);                                // setPixelValue (Java narrowing)
+                }
+                uint32_t e;
+                if constexpr (sizeof(T) == 1) {                    // Table8: indexed by the raw byte
+                    e = tab[(uint8_t)t];
+                    err |= (e & kErrBit) != 0;
+                    e &= ~kErrBit;
+                } else {
+                    const int x = (int)t;
+                    if (k.check) err |= (x < k.gmin) | (x > k.gmax);
+                    uint32_t v;
+                    if constexpr (FAST) {
+                        v = fast16(x, k);
+                    } else if (k.mode == kModeLinear16) {
+                        v = linear16(x, k, A.R.cd_start, A.R.cds8, A.R.cde8);
+                    } else {
+                        const int xi = min(max(x, k.gmin), k.gmax);
+                        v = A.R.ws_base[k.lut_off + (uint32_t)(xi - k.gmin)];
+                    }
+                    e = tab[v];
+                }
+                accp[j] += e;
+            }
+        }
+        if (__ballot(err)) {
+            if (err) atomicOr(A.R.flag, 1);
+        }
+        uint32_t o[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t f = clamp_fields(accp[j]);
+            o[j] = 0xFF000000u | ((f >> 4) & 0xFF0000u) | ((f >> 2) & 0xFF00u) | (f & 0xFFu);
+        }
+        const uint32_t row = (uint32_t)(px / (uint64_t)A.width), col = (uint32_t)(px - (uint64_t)row * A.width);
+        const uint32_t orow = A.flip_v ? (uint32_t)A.height - 1 - row : row;
+        const uint32_t ocol = A.flip_h ? (uint32_t)A.width - 2 - col : col;
+        if (A.flip_h) { const uint32_t t2 = o[0]; o[0] = o[1]; o[1] = t2; }
+        *reinterpret_cast<uint2*>(A.out + (uint64_t)orow * A.width + ocol) = make_uint2(o[0], o[1]);
+    }
+}
+
+template <typename T, bool BEI>
+static hipError_t launch_project_render_t(const K3RArgs& a, bool max, bool fast, dim3 g, hipStream_t s) {
+    if constexpr (sizeof(T) == 1) {          // 8-bit: max only (32-bit sums of 1024 pixels per wave
+        hipLaunchKernelGGL((k_project_render<T, BEI, true, false>), g, dim3(kBlock), 0, s, a);   // exceed LDS)
+        return hipGetLastError();
+    }
+    if (max) {
+        if (fast) hipLaunchKernelGGL((k_project_render<T, BEI, true, true>), g, dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL((k_project_render<T, BEI, true, false>), g, dim3(kBlock), 0, s, a);
+    } else {
+        if (fast) hipLaunchKernelGGL((k_project_render<T, BEI, false, true>), g, dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL((k_project_render<T, BEI, false, false>), g, dim3(kBlock), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+// The fused glue when it applies (8/16-bit integer stacks, 1..4 rendered channels, 16-B aligned
+// stacks holding whole 16-B chunks per plane, even width, 8-B aligned output): *done = true.
+omr_status enqueue_project_render(Ctx* ctx, const void* const* stacks, const FusedRender& R, int32_t pixel_type,
+                                  int32_t be_in, int32_t size_x, int32_t size_y, int32_t algorithm, int32_t start,
+                                  int32_t end, int32_t stepping, int32_t flip_h, int32_t flip_v, uint32_t* d_out,
+                                  bool* done) {
+    *done = false;
+    const int bpp = bytes_per_pixel(pixel_type);
+    const int64_t plane = (int64_t)size_x * size_y;
+    if (bpp > 2 || R.n_active < 1 || R.n_active > kFusedMaxActive || plane == 0) return OMR_OK;
+    if (bpp == 1 && algorithm != OMR_PROJECTION_MAX) return OMR_OK;
+    if ((plane * bpp) % 16 || size_x % 2 || reinterpret_cast<uintptr_t>(d_out) % 8) return OMR_OK;
+    for (int a = 0; a < R.n_active; ++a)
+        if (!stacks[a] || reinterpret_cast<uintptr_t>(stacks[a]) % 16) return OMR_OK;
+    uint32_t n_iter;
+    if (algorithm == OMR_PROJECTION_MAX) n_iter = end >= start ? (uint32_t)((end - start) / stepping + 1) : 0u;
+    else n_iter = end > start ? (uint32_t)((end - start + stepping - 1) / stepping) : 0u;
+    if (n_iter > kAcc32MaxPlanes) return OMR_OK;
+    K3RArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int i = 0; i < R.n_active; ++i) a.stacks[i] = static_cast<const uint8_t*>(stacks[i]);
+    a.out = d_out;
+    a.R = R;
+    a.start = start;
+    a.stepping = stepping;
+    a.width = size_x;
+    a.height = size_y;
+    a.flip_h = flip_h ? 1 : 0;
+    a.flip_v = flip_v ? 1 : 0;
+    a.mean = algorithm == OMR_PROJECTION_MEAN ? 1 : 0;
+    a.chunks = (uint32_t)(plane * bpp / 16);
+    a.n_iter = n_iter;
+    const dim3 g((a.chunks + 63) / 64);
+    const bool mx = algorithm == OMR_PROJECTION_MAX, fast = R.mode == kFusedFast16, be = be_in != 0;
+    hipError_t e;
+    KernelTimer timer(ctx, 3);
+    switch (pixel_type) {
+    case OMR_PIXELS_INT8: e = launch_project_render_t<int8_t, false>(a, mx, false, g, ctx->stream); break;
+    case OMR_PIXELS_UINT8: e = launch_project_render_t<uint8_t, false>(a, mx, false, g, ctx->stream); break;
+    case OMR_PIXELS_INT16:
+        e = be ? launch_project_render_t<int16_t, true>(a, mx, fast, g, ctx->stream)
+               : launch_project_render_t<int16_t, false>(a, mx, fast, g, ctx->stream);
+        break;
+    default:
+        e = be ? launch_project_render_t<uint16_t, true>(a, mx, fast, g, ctx->stream)
+               : launch_project_render_t<uint16_t, false>(a, mx, fast, g, ctx->stream);
+        break;
+    }
+    OMR_HIP(ctx, e);
+    *done = true;
+    return OMR_OK;
 }
 
 template <typename T>

@@ -19,6 +19,8 @@
 #include "omr_device.h"
 #include "omr_k2.h"
 
+#include <memory>
+
 namespace omr {
 
 // ------------------------------------------------------------------------------- K1
@@ -1250,6 +1252,34 @@ extern "C" omr_status omr_render_projected_device(
     if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const int bpp = bytes_per_pixel(pixel_type);
+    if (na >= 1 && na <= kFusedMaxActive && bpp <= 2 && (size_x * (int64_t)size_y * bpp) % 16 == 0 &&
+        size_x % 2 == 0 && reinterpret_cast<uintptr_t>(d_argb_out) % 8 == 0) {
+        // K3R: project + render in one kernel (the projected planes never reach HBM)
+        std::unique_ptr<FusedPlanBuf, void (*)(FusedPlanBuf*)> fp(fused_plan_new(), fused_plan_free);
+        omr_status fst = OMR_OK;
+        if (render_fused_plan(ctx, qdef, channels, size_c, pixel_type, fp.get(), &fst)) {
+            const void* st_ptrs[kFusedMaxActive] = {};
+            bool aligned = true;
+            for (int a = 0; a < na; ++a) {
+                st_ptrs[a] = d_stacks[fp->pp.plan.ch[a].index];
+                aligned &= reinterpret_cast<uintptr_t>(st_ptrs[a]) % 16 == 0;
+            }
+            const bool dims_ok = bpp == 2 || algorithm == OMR_PROJECTION_MAX;
+            if (aligned && dims_ok) {
+                st = ensure_workspace(ctx, render_fused_ws_bytes(fp.get()));
+                if (st) return st;
+                FusedRender R;
+                st = render_fused_stage(ctx, fp.get(), 0, R);
+                if (st) return st;
+                bool done = false;
+                st = enqueue_project_render(ctx, st_ptrs, R, pixel_type, big_endian, size_x, size_y, algorithm, start,
+                                            end, stepping, flip_h, flip_v, d_argb_out, &done);
+                if (st || done) return st;    // else (> 65535 planes summed): K3 + K2 below
+            }
+        } else if (fst) {
+            return fst;
+        }
+    }
     const size_t plane_bytes = align_up((size_t)size_x * size_y * bpp, 256);
     const size_t ptr_bytes = align_up(sizeof(void*) * (size_t)(size_c > 0 ? size_c : 1), 256);
     const RenderLayout L = layout_for(pp, ptr_bytes + plane_bytes * (size_t)na);

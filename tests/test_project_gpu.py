@@ -142,3 +142,102 @@ def test_flip_errors(ctx):
         flip(ctx, src, 4, 0, True, True)                           # testFlipZeroYImage
     with pytest.raises(_lib.OmrError):
         ctx.flip_argb_device(None, src, 4, 4, True, True)
+
+
+# ---- projection glue: project every active channel + render (K3R fused, or K3 + K2) -------
+def _glue(ctx, chans, stacks, pt, w, h, z, alg, start, end, stepping=1, be=False, flip=(False, False),
+          model="rgb", qd_kw=None):
+    import torch
+    q = O.make_qdef(model, **(qd_kw or {}))
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+    devs = [dev(s) if s is not None else None for s in stacks]
+    torch.cuda.synchronize()
+    ctx.render_projected_device(q, chans, devs, pt, w, h, z, alg, start, end, out, stepping=stepping,
+                                big_endian=be, flip_h=flip[0], flip_v=flip[1])
+    ctx.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    planes = []
+    for c, s in enumerate(stacks):
+        if s is None or not chans[c].get("active", True):
+            planes.append(None)
+            continue
+        st, p = O.project(s, pt, w, h, z, alg, start, end, stepping, be_in=be, be_out=be)
+        assert st == 0
+        planes.append(p)
+    planes = [p if p is not None else np.zeros(w * h * np.dtype(stacks[0].dtype).itemsize, np.uint8) for p in planes]
+    st, exp = O.render(chans, planes, pt, w, h, big_endian=be, flip_h=flip[0], flip_v=flip[1], qdef=q)
+    assert st == 0
+    np.testing.assert_array_equal(got, exp)
+
+
+GLUE_TYPES = [(_lib.PIXELS_UINT16, np.uint16, (0.0, 65535.0)), (_lib.PIXELS_INT16, np.int16, (-32768.0, 32767.0)),
+              (_lib.PIXELS_UINT8, np.uint8, (0.0, 255.0)), (_lib.PIXELS_INT8, np.int8, (-128.0, 127.0))]
+
+
+@pytest.mark.parametrize("pt,dtype,rng_", GLUE_TYPES)
+@pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM])
+@pytest.mark.parametrize("be", [False, True])
+def test_projection_glue_types_and_algorithms(ctx, pt, dtype, rng_, alg, be):
+    z, h, w = 13, 48, 64
+    stacks = [rand_stack(dtype, z, h, w, 300 + c) for c in range(3)]
+    if be:
+        stacks = [s.astype(s.dtype.newbyteorder(">")) for s in stacks]
+    lo, hi = rng_
+    span = hi - lo
+    chans = [{"input_start": lo + span * f0, "input_end": lo + span * f1, "global_min": lo, "global_max": hi,
+              "rgba": col} for (f0, f1), col in zip([(0.0, 1.0), (0.1, 0.7), (0.3, 0.4)],
+                                                    [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255)])]
+    _glue(ctx, chans, stacks, pt, w, h, z, alg, 1, z - 2, be=be, flip=(True, False))
+
+
+@pytest.mark.parametrize("n_ch", [1, 2, 4])
+@pytest.mark.parametrize("flip", [(False, False), (False, True), (True, True)])
+def test_projection_glue_channels_flips_modes(ctx, n_ch, flip):
+    z, h, w = 64, 64, 128
+    rng = np.random.default_rng(n_ch)
+    stacks = [np.clip(microscopy_u16(h, w, rng).astype(np.int64) + rng.integers(-300, 300, (z, h, w)), 0,
+                      65535).astype(np.uint16) for _ in range(n_ch)]
+    chans = c2_channels(4)[:n_ch]
+    lut = np.concatenate([np.arange(256), 255 - np.arange(256), np.arange(256) // 2]).astype(np.uint8)
+    variants = [{}, {"reverse": True}, {"lut": lut}, {"family": _lib.FAMILY_LOGARITHMIC}]
+    for c in range(n_ch):
+        chans[c].update(variants[c])
+    for alg, stepping in ((_lib.PROJECTION_MAX, 1), (_lib.PROJECTION_MEAN, 2), (_lib.PROJECTION_SUM, 3)):
+        _glue(ctx, chans, stacks, _lib.PIXELS_UINT16, w, h, z, alg, 2, z - 1, stepping=stepping, flip=flip)
+    _glue(ctx, chans, stacks, _lib.PIXELS_UINT16, w, h, z, _lib.PROJECTION_MEAN, 0, z - 1,
+          qd_kw={"cd_start": 30, "cd_end": 220})
+
+
+def test_projection_glue_unfused_cases(ctx):
+    """Odd width, five channels, 8-bit mean, float: the K3 + K2 path, same results."""
+    rng = np.random.default_rng(9)
+    z = 9
+    s16 = [rng.integers(0, 65536, (z, 8, 33)).astype(np.uint16) for _ in range(5)]
+    chans = c2_channels(4) + c2_channels(1)
+    _glue(ctx, chans[:2], s16[:2], _lib.PIXELS_UINT16, 33, 8, z, _lib.PROJECTION_MEAN, 0, z - 1)
+    s16 = [rng.integers(0, 65536, (z, 8, 32)).astype(np.uint16) for _ in range(5)]
+    _glue(ctx, chans, s16, _lib.PIXELS_UINT16, 32, 8, z, _lib.PROJECTION_MAX, 0, z - 1)
+    s8 = [rng.integers(0, 256, (z, 16, 32)).astype(np.uint8) for _ in range(2)]
+    c8 = [{"input_start": 0.0, "input_end": 255.0, "global_min": 0.0, "global_max": 255.0, "rgba": (255, 9, 0, 255)},
+          {"input_start": 20.0, "input_end": 90.0, "global_min": 0.0, "global_max": 255.0, "rgba": (0, 99, 255, 255)}]
+    _glue(ctx, c8, s8, _lib.PIXELS_UINT8, 32, 16, z, _lib.PROJECTION_MEAN, 0, z - 1)
+    sf = [rng.uniform(-10, 300, (z, 16, 32)).astype(np.float32) for _ in range(2)]
+    cf = [{"input_start": 0.0, "input_end": 255.0, "rgba": (255, 0, 0, 255)},
+          {"input_start": 5.0, "input_end": 200.0, "rgba": (0, 0, 255, 255)}]
+    _glue(ctx, cf, sf, _lib.PIXELS_FLOAT, 32, 16, z, _lib.PROJECTION_MAX, 0, z - 1)
+
+
+def test_projection_glue_quantization_error(ctx):
+    import torch
+    z, h, w = 4, 16, 32
+    stacks = [np.full((z, h, w), 100, np.uint16) for _ in range(2)]
+    stacks[1][2, 3, 4] = 65000
+    chans = c2_channels(2)
+    for c in chans:
+        c["global_max"] = 60000.0
+    out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+    ctx.render_projected_device(O.make_qdef("rgb"), chans, [dev(s) for s in stacks], _lib.PIXELS_UINT16, w, h, z,
+                                _lib.PROJECTION_MAX, 0, z - 1, out)
+    with pytest.raises(_lib.OmrError) as e:
+        ctx.synchronize()
+    assert e.value.status == _lib.QUANTIZATION
