@@ -90,7 +90,10 @@ struct Ctx {
     int pin_slot = 0;
     int cu_count = 256;
     bool k2_nt_store = true;
-    uint32_t sem = 0;            // OMR_SEM_* (omr_ctx_set_semantics)     // env OMR_K2_NT_STORE=0: plain ARGB stores (measurement switch)
+    uint32_t sem = 0;            // OMR_SEM_* (omr_ctx_set_semantics)
+    // projection glue through the fused K3R kernel (env OMR_K3R=1; measured slower than K3 + K2
+    // on C3, DESIGN.md §K3R, so off by default)
+    bool k3r = false;     // env OMR_K2_NT_STORE=0: plain ARGB stores (measurement switch)
     // kernel timing (omr_ctx_enable_kernel_timing)
     bool timing = false;
     struct Timed { hipEvent_t start, stop; int kind; };

@@ -51,6 +51,39 @@ __device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
 }
 
 
+__device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey, uint32_t sem) {
+    const int vv = p.reverse ? ((cde - v + cds) & 0xFF) : v;
+    if (grey && !(p.has_lut && (sem & OMR_SEM_GREYSCALE_LUT)))
+        return ((uint32_t)vv << 20) | ((uint32_t)vv << 10) | (uint32_t)vv;
+    uint32_t r, g, b;
+    if (p.has_lut) {
+        r = p.lut_rgb[vv]; g = p.lut_rgb[256 + vv]; b = p.lut_rgb[512 + vv];
+    } else if (sem & OMR_SEM_ALPHA_SEPARATE) {
+        r = (uint32_t)(int)((float)(int)(p.cratio[0] * (float)vv) * p.alpha);
+        g = (uint32_t)(int)((float)(int)(p.cratio[1] * (float)vv) * p.alpha);
+        b = (uint32_t)(int)((float)(int)(p.cratio[2] * (float)vv) * p.alpha);
+    } else {
+        r = (uint32_t)(int)(p.ratio[0] * (float)vv);
+        g = (uint32_t)(int)(p.ratio[1] * (float)vv);
+        b = (uint32_t)(int)(p.ratio[2] * (float)vv);
+    }
+    return (r << 20) | (g << 10) | b;
+}
+
+// Contribution-table entry t of active channel a (K1, and K2's in-LDS build for small launches).
+// Table8 channels are indexed by the raw byte.
+__device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__ plan, int a, int t, int is_signed8) {
+    const ChanParam& p = plan->ch[a];
+    const int cds = plan->cd_start, cde = plan->cd_end;
+    if (p.mode == kModeTable8) {
+        const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
+        if (value < p.gmin || value > p.gmax) return kErrBit;
+        const int v = quantize_eval((double)value, p, cds, cde);
+        return pack_contrib(p, v, cds, cde, plan->greyscale, plan->sem);
+    }
+    return pack_contrib(p, t, cds, cde, plan->greyscale, plan->sem);
+}
+
 // A render prepared for the fused render -> JPEG path (omr_jpeg.hip): the plan is staged and
 // the contribution tables (K1) and byte LUTs built on the context stream; the fused kernel
 // quantizes + composites each pixel as K2 does (same helpers, same tables) and encodes it.
@@ -58,7 +91,8 @@ constexpr int kFusedMaxActive = 4;
 enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4 };
 struct FusedRender {
     K2Chan ch[kFusedMaxActive];
-    const uint32_t* contrib;     // [n_active][256] (workspace)
+    const uint32_t* contrib;     // [n_active][256] (workspace; built by K1 unless the kernel builds it)
+    const RenderPlan* plan;      // the staged plan (kernels that build the tables themselves)
     const uint8_t* ws_base;      // workspace base (kModeLut16 byte LUTs)
     int32_t* flag;               // sticky quantization-error word
     int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
@@ -76,6 +110,7 @@ bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_bin
 size_t render_fused_ws_bytes(const FusedPlanBuf* fp);
 // Stage the plan at ctx->ws + ws_off (the workspace must hold render_fused_ws_bytes from there),
 // build the tables on the context stream and fill `out`.
-omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& out);
+// build_contrib false: the fused kernel builds the tables from `plan` (contrib_entry) itself.
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& out, bool build_contrib = true);
 
 }  // namespace omr

@@ -291,22 +291,30 @@ struct K3RArgs {
     FusedRender R;
     int32_t start, stepping, width, height, flip_h, flip_v, mean;
     uint32_t chunks, n_iter;
+    FastDiv ndiv;         // n_iter (mean: exact integer quotient, see below)
 };
+
+constexpr int kK3RChunks = 32;   // 16-B chunks per workgroup (256 pixels at 16 bits)
+constexpr int kK3RParts = 8;     // z parts per workgroup: 4 waves x 2 half-waves
 
 template <typename T, bool BEI, bool MAX, bool FAST>
 __global__ void __launch_bounds__(kBlock) k_project_render(K3RArgs A) {
     using U = typename Raw<T>::U;
     constexpr int V = VecPx<T>::V;                      // 8 (16-bit) or 16 (8-bit) pixels per chunk
+    constexpr int NPX = kK3RChunks * V;                 // pixels per workgroup
     using Part = typename std::conditional<MAX, T, typename Acc32<T>::type>::type;
-    __shared__ Part s_part[4][kFusedMaxActive][64 * V];
+    __shared__ Part s_part[kK3RParts][kFusedMaxActive][NPX];
     __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
     const int na = A.R.n_active;
-    for (int i = threadIdx.x; i < na * 256; i += kBlock) s_contrib[i] = A.R.contrib[i];
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t c = blockIdx.x * 64 + lane;
+    for (int i = threadIdx.x; i < na * 256; i += kBlock)     // K1's tables, built here (no K1 launch)
+        s_contrib[i] = contrib_entry(A.R.plan, i >> 8, i & 255, std::is_same<T, int8_t>::value ? 1 : 0);
+    // lane l of wave w: chunk (l & 31) of the workgroup's 32, z part 2w + (l >> 5) of 8
+    const uint32_t lane = threadIdx.x & 63u, part = (threadIdx.x >> 6) * 2 + (lane >> 5), ch = lane & 31u;
+    const uint32_t c = blockIdx.x * kK3RChunks + ch;
     const uint32_t cc = min(c, A.chunks - 1);
     const uint64_t pchunks = (uint64_t)A.chunks * (uint64_t)A.stepping;
-    const uint32_t i0 = (uint32_t)((uint64_t)A.n_iter * wave / 4), i1 = (uint32_t)((uint64_t)A.n_iter * (wave + 1) / 4);
+    const uint32_t i0 = (uint32_t)((uint64_t)A.n_iter * part / kK3RParts);
+    const uint32_t i1 = (uint32_t)((uint64_t)A.n_iter * (part + 1) / kK3RParts);
 #pragma unroll
     for (int a = 0; a < kFusedMaxActive; ++a) {
         if (a >= na) break;                                         // uniform
@@ -335,83 +343,84 @@ __global__ void __launch_bounds__(kBlock) k_project_render(K3RArgs A) {
         }
         for (; i < i1; ++i, p += pchunks) fold(__builtin_nontemporal_load(p));
 #pragma unroll
-        for (int j = 0; j < V; ++j) s_part[wave][a][lane * V + j] = acc[j];
+        for (int j = 0; j < V; ++j) s_part[part][a][ch * V + j] = acc[j];
     }
     __syncthreads();
-    // thread t renders pixels 2t, 2t+1 of the workgroup's 64*V (16-bit: 512) pixels; 8-bit
-    // chunks hold 1024 pixels, so each thread takes 2 pairs
+    // thread t renders pixel t (16-bit: 256 per workgroup; 8-bit: 512, two per thread)
     const uint64_t plane = (uint64_t)A.chunks * V;
 #pragma unroll
-    for (int rep = 0; rep < V / 8; ++rep) {
-        const uint32_t lp = (rep * kBlock + threadIdx.x) * 2;      // pixel pair index within the block
-        const uint64_t px = (uint64_t)blockIdx.x * 64 * V + lp;
+    for (int rep = 0; rep < NPX / kBlock; ++rep) {
+        const uint32_t lp = rep * kBlock + threadIdx.x;
+        const uint64_t px = (uint64_t)blockIdx.x * NPX + lp;
         if (px >= plane) break;
-        uint32_t accp[2] = {0, 0};
+        uint32_t accp = 0;
         bool err = false;
 #pragma unroll
         for (int a = 0; a < kFusedMaxActive; ++a) {
             if (a >= na) break;
             const K2Chan& k = A.R.ch[a];
-            const uint32_t* tab = s_contrib + a * 256;
+            T t;
+            if constexpr (MAX) {
+                Part m = s_part[0][a][lp];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                T t;
-                if constexpr (MAX) {
-                    Part m = s_part[0][a][lp + j];
+                for (int w = 1; w < kK3RParts; ++w) { const Part v = s_part[w][a][lp]; if (v > m) m = v; }
+                t = m;
+            } else {
+                // sum as double, mean = sum / count, clamp at the type max, (int) narrowing
+                // (ProjectionService.java:268-288): with |sum| < 2^31 and count <= 32767 the
+                // double quotient never rounds up across an integer (the gap to the next one is
+                // >= 1/count >> its ulp), so the truncated quotient is the integer quotient
+                // toward zero; sums below the 16-bit minimum wrap in the short cast as in Java.
+                Part sum = s_part[0][a][lp];
 #pragma unroll
-                    for (int w = 1; w < 4; ++w) { const Part v = s_part[w][a][lp + j]; if (v > m) m = v; }
-                    t = m;
-                } else {
-                    Part sum = s_part[0][a][lp + j] + s_part[1][a][lp + j] + s_part[2][a][lp + j] +
-                               s_part[3][a][lp + j];
-                    double v = (double)sum;
-                    if (A.mean) v = v / (double)A.n_iter;
-                    if (v > type_max<T>()) v = type_max<T>();
-                    t = narrow<T>(v);                                // setPixelValue (Java narrowing)
+                for (int w = 1; w < kK3RParts; ++w) sum += s_part[w][a][lp];
+                int32_t v = (int32_t)sum;
+                if (A.mean) {
+                    const uint32_t m = (uint32_t)(v < 0 ? -v : v);
+                    const int32_t q = (int32_t)fdiv(m, A.ndiv);
+                    v = v < 0 ? -q : q;
                 }
-                uint32_t e;
-                if constexpr (sizeof(T) == 1) {                    // Table8: indexed by the raw byte
-                    e = tab[(uint8_t)t];
-                    err |= (e & kErrBit) != 0;
-                    e &= ~kErrBit;
-                } else {
-                    const int x = (int)t;
-                    if (k.check) err |= (x < k.gmin) | (x > k.gmax);
-                    uint32_t v;
-                    if constexpr (FAST) {
-                        v = fast16(x, k);
-                    } else if (k.mode == kModeLinear16) {
-                        v = linear16(x, k, A.R.cd_start, A.R.cds8, A.R.cde8);
-                    } else {
-                        const int xi = min(max(x, k.gmin), k.gmax);
-                        v = A.R.ws_base[k.lut_off + (uint32_t)(xi - k.gmin)];
-                    }
-                    e = tab[v];
-                }
-                accp[j] += e;
+                v = min(v, (int32_t)type_max<T>());
+                t = (T)v;                                            // setPixelValue (Java narrowing)
             }
+            uint32_t e;
+            const uint32_t* tab = s_contrib + a * 256;
+            if constexpr (sizeof(T) == 1) {                         // Table8: indexed by the raw byte
+                e = tab[(uint8_t)t];
+                err |= (e & kErrBit) != 0;
+                e &= ~kErrBit;
+            } else {
+                const int x = (int)t;
+                if (k.check) err |= (x < k.gmin) | (x > k.gmax);
+                uint32_t v;
+                if constexpr (FAST) {
+                    v = fast16(x, k);
+                } else if (k.mode == kModeLinear16) {
+                    v = linear16(x, k, A.R.cd_start, A.R.cds8, A.R.cde8);
+                } else {
+                    const int xi = min(max(x, k.gmin), k.gmax);
+                    v = A.R.ws_base[k.lut_off + (uint32_t)(xi - k.gmin)];
+                }
+                e = tab[v];
+            }
+            accp += e;
         }
         if (__ballot(err)) {
             if (err) atomicOr(A.R.flag, 1);
         }
-        uint32_t o[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t f = clamp_fields(accp[j]);
-            o[j] = 0xFF000000u | ((f >> 4) & 0xFF0000u) | ((f >> 2) & 0xFF00u) | (f & 0xFFu);
-        }
+        const uint32_t f = clamp_fields(accp);
+        const uint32_t o = 0xFF000000u | ((f >> 4) & 0xFF0000u) | ((f >> 2) & 0xFF00u) | (f & 0xFFu);
         const uint32_t row = (uint32_t)(px / (uint64_t)A.width), col = (uint32_t)(px - (uint64_t)row * A.width);
         const uint32_t orow = A.flip_v ? (uint32_t)A.height - 1 - row : row;
-        const uint32_t ocol = A.flip_h ? (uint32_t)A.width - 2 - col : col;
-        if (A.flip_h) { const uint32_t t2 = o[0]; o[0] = o[1]; o[1] = t2; }
-        *reinterpret_cast<uint2*>(A.out + (uint64_t)orow * A.width + ocol) = make_uint2(o[0], o[1]);
+        const uint32_t ocol = A.flip_h ? (uint32_t)A.width - 1 - col : col;
+        A.out[(uint64_t)orow * A.width + ocol] = o;
     }
 }
 
 template <typename T, bool BEI>
 static hipError_t launch_project_render_t(const K3RArgs& a, bool max, bool fast, dim3 g, hipStream_t s) {
-    if constexpr (sizeof(T) == 1) {          // 8-bit: max only (32-bit sums of 1024 pixels per wave
-        hipLaunchKernelGGL((k_project_render<T, BEI, true, false>), g, dim3(kBlock), 0, s, a);   // exceed LDS)
+    if constexpr (sizeof(T) == 1) {          // 8-bit: max only (their 32-bit partial sums exceed LDS)
+        hipLaunchKernelGGL((k_project_render<T, BEI, true, false>), g, dim3(kBlock), 0, s, a);
         return hipGetLastError();
     }
     if (max) {
@@ -435,13 +444,13 @@ omr_status enqueue_project_render(Ctx* ctx, const void* const* stacks, const Fus
     const int64_t plane = (int64_t)size_x * size_y;
     if (bpp > 2 || R.n_active < 1 || R.n_active > kFusedMaxActive || plane == 0) return OMR_OK;
     if (bpp == 1 && algorithm != OMR_PROJECTION_MAX) return OMR_OK;
-    if ((plane * bpp) % 16 || size_x % 2 || reinterpret_cast<uintptr_t>(d_out) % 8) return OMR_OK;
+    if ((plane * bpp) % 16 || reinterpret_cast<uintptr_t>(d_out) % 4) return OMR_OK;
     for (int a = 0; a < R.n_active; ++a)
         if (!stacks[a] || reinterpret_cast<uintptr_t>(stacks[a]) % 16) return OMR_OK;
     uint32_t n_iter;
     if (algorithm == OMR_PROJECTION_MAX) n_iter = end >= start ? (uint32_t)((end - start) / stepping + 1) : 0u;
     else n_iter = end > start ? (uint32_t)((end - start + stepping - 1) / stepping) : 0u;
-    if (n_iter > kAcc32MaxPlanes) return OMR_OK;
+    if (n_iter > 32767 || (algorithm != OMR_PROJECTION_MAX && n_iter == 0)) return OMR_OK;   // |sum| < 2^31
     K3RArgs a;
     std::memset(&a, 0, sizeof(a));
     for (int i = 0; i < R.n_active; ++i) a.stacks[i] = static_cast<const uint8_t*>(stacks[i]);
@@ -456,7 +465,8 @@ omr_status enqueue_project_render(Ctx* ctx, const void* const* stacks, const Fus
     a.mean = algorithm == OMR_PROJECTION_MEAN ? 1 : 0;
     a.chunks = (uint32_t)(plane * bpp / 16);
     a.n_iter = n_iter;
-    const dim3 g((a.chunks + 63) / 64);
+    a.ndiv = make_fastdiv(n_iter ? n_iter : 1);
+    const dim3 g((a.chunks + kK3RChunks - 1) / kK3RChunks);
     const bool mx = algorithm == OMR_PROJECTION_MAX, fast = R.mode == kFusedFast16, be = be_in != 0;
     hipError_t e;
     KernelTimer timer(ctx, 3);

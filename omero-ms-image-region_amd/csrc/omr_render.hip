@@ -24,25 +24,6 @@
 namespace omr {
 
 // ------------------------------------------------------------------------------- K1
-__device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey, uint32_t sem) {
-    const int vv = p.reverse ? ((cde - v + cds) & 0xFF) : v;
-    if (grey && !(p.has_lut && (sem & OMR_SEM_GREYSCALE_LUT)))
-        return ((uint32_t)vv << 20) | ((uint32_t)vv << 10) | (uint32_t)vv;
-    uint32_t r, g, b;
-    if (p.has_lut) {
-        r = p.lut_rgb[vv]; g = p.lut_rgb[256 + vv]; b = p.lut_rgb[512 + vv];
-    } else if (sem & OMR_SEM_ALPHA_SEPARATE) {
-        r = (uint32_t)(int)((float)(int)(p.cratio[0] * (float)vv) * p.alpha);
-        g = (uint32_t)(int)((float)(int)(p.cratio[1] * (float)vv) * p.alpha);
-        b = (uint32_t)(int)((float)(int)(p.cratio[2] * (float)vv) * p.alpha);
-    } else {
-        r = (uint32_t)(int)(p.ratio[0] * (float)vv);
-        g = (uint32_t)(int)(p.ratio[1] * (float)vv);
-        b = (uint32_t)(int)(p.ratio[2] * (float)vv);
-    }
-    return (r << 20) | (g << 10) | b;
-}
-
 // Parameter blocks (plans, pointer tables, headers: a few KiB) from pinned host memory;
 // blockIdx.y selects one of two (dst, src, bytes) segments.
 __global__ void __launch_bounds__(256) k_h2d_small(uint8_t* __restrict__ dst1, const uint8_t* __restrict__ src1,
@@ -79,20 +60,6 @@ hipError_t launch_h2d_small(hipStream_t s, void* dst1, const void* pinned_src1, 
                        static_cast<const uint8_t*>(pinned_src1), (uint64_t)n1, static_cast<uint8_t*>(dst2),
                        static_cast<const uint8_t*>(pinned_src2), (uint64_t)n2);
     return hipGetLastError();
-}
-
-// Contribution-table entry t of active channel a (K1, and K2's in-LDS build for small launches).
-// Table8 channels are indexed by the raw byte.
-__device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__ plan, int a, int t, int is_signed8) {
-    const ChanParam& p = plan->ch[a];
-    const int cds = plan->cd_start, cde = plan->cd_end;
-    if (p.mode == kModeTable8) {
-        const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
-        if (value < p.gmin || value > p.gmax) return kErrBit;
-        const int v = quantize_eval((double)value, p, cds, cde);
-        return pack_contrib(p, v, cds, cde, plan->greyscale, plan->sem);
-    }
-    return pack_contrib(p, t, cds, cde, plan->greyscale, plan->sem);
 }
 
 // grid: n_active blocks x 256 threads.
@@ -991,10 +958,7 @@ FusedPlanBuf* fused_plan_new() { return new FusedPlanBuf(); }
 void fused_plan_free(FusedPlanBuf* fp) { delete fp; }
 size_t render_fused_ws_bytes(const FusedPlanBuf* fp) { return fp->L.total; }
 
-bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch, int32_t size_c,
-                       int32_t pixel_type, FusedPlanBuf* fp, omr_status* st) {
-    *st = prepare_plan(ctx, q, ch, size_c, pixel_type, fp->pp);
-    if (*st) return false;
+static bool fused_from_prepared(FusedPlanBuf* fp, int32_t pixel_type) {
     const int bpp = bytes_per_pixel(pixel_type);
     const int na = fp->pp.plan.n_active;
     if (bpp > 2 || na < 1 || na > kFusedMaxActive) return false;
@@ -1010,7 +974,14 @@ bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_bin
     return true;
 }
 
-omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& F) {
+bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch, int32_t size_c,
+                       int32_t pixel_type, FusedPlanBuf* fp, omr_status* st) {
+    *st = prepare_plan(ctx, q, ch, size_c, pixel_type, fp->pp);
+    if (*st) return false;
+    return fused_from_prepared(fp, pixel_type);
+}
+
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& F, bool build_contrib) {
     PreparedPlan& pp = fp->pp;
     const RenderLayout& L = fp->L;
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws) + ws_off;
@@ -1020,9 +991,11 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
     for (int a = 0; a < na; ++a) pp.plan.ch[a].lut_off += ws_off + L.lut_off;   // relative to ctx->ws
     omr_status st = stage_h2d(ctx, d_plan, &pp.plan, pp.plan_bytes);
     if (st) return st;
-    hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
-                       fp->pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
-    OMR_HIP(ctx, hipGetLastError());
+    if (build_contrib) {
+        hipLaunchKernelGGL(k_build_contrib, dim3(na), dim3(256), 0, ctx->stream, d_plan, d_contrib,
+                           fp->pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
+        OMR_HIP(ctx, hipGetLastError());
+    }
     if (pp.n_lut > 0) {
         hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan,
                            static_cast<uint8_t*>(ctx->ws));
@@ -1048,6 +1021,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.lut_off = c.lut_off;
     }
     F.contrib = d_contrib;
+    F.plan = d_plan;
     F.ws_base = static_cast<const uint8_t*>(ctx->ws);
     F.flag = ctx->d_flag;
     F.n_active = na;
@@ -1252,32 +1226,30 @@ extern "C" omr_status omr_render_projected_device(
     if (!d_argb_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null output");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const int bpp = bytes_per_pixel(pixel_type);
-    if (na >= 1 && na <= kFusedMaxActive && bpp <= 2 && (size_x * (int64_t)size_y * bpp) % 16 == 0 &&
-        size_x % 2 == 0 && reinterpret_cast<uintptr_t>(d_argb_out) % 8 == 0) {
-        // K3R: project + render in one kernel (the projected planes never reach HBM)
-        std::unique_ptr<FusedPlanBuf, void (*)(FusedPlanBuf*)> fp(fused_plan_new(), fused_plan_free);
-        omr_status fst = OMR_OK;
-        if (render_fused_plan(ctx, qdef, channels, size_c, pixel_type, fp.get(), &fst)) {
+    if (ctx->k3r && na >= 1 && na <= kFusedMaxActive && bpp <= 2 && (size_x * (int64_t)size_y * bpp) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(d_argb_out) % 4 == 0) {
+        // K3R: project + render in one kernel (the projected planes never reach HBM); the
+        // contribution tables are built by K3R itself from the staged plan (no K1 launch)
+        FusedPlanBuf fp;
+        fp.pp = pp;
+        if (fused_from_prepared(&fp, pixel_type)) {
             const void* st_ptrs[kFusedMaxActive] = {};
             bool aligned = true;
             for (int a = 0; a < na; ++a) {
-                st_ptrs[a] = d_stacks[fp->pp.plan.ch[a].index];
+                st_ptrs[a] = d_stacks[fp.pp.plan.ch[a].index];
                 aligned &= reinterpret_cast<uintptr_t>(st_ptrs[a]) % 16 == 0;
             }
-            const bool dims_ok = bpp == 2 || algorithm == OMR_PROJECTION_MAX;
-            if (aligned && dims_ok) {
-                st = ensure_workspace(ctx, render_fused_ws_bytes(fp.get()));
+            if (aligned && (bpp == 2 || algorithm == OMR_PROJECTION_MAX)) {
+                st = ensure_workspace(ctx, render_fused_ws_bytes(&fp));
                 if (st) return st;
                 FusedRender R;
-                st = render_fused_stage(ctx, fp.get(), 0, R);
+                st = render_fused_stage(ctx, &fp, 0, R, /*build_contrib=*/false);
                 if (st) return st;
                 bool done = false;
                 st = enqueue_project_render(ctx, st_ptrs, R, pixel_type, big_endian, size_x, size_y, algorithm, start,
                                             end, stepping, flip_h, flip_v, d_argb_out, &done);
-                if (st || done) return st;    // else (> 65535 planes summed): K3 + K2 below
+                if (st || done) return st;    // else (too many planes summed): K3 + K2 below
             }
-        } else if (fst) {
-            return fst;
         }
     }
     const size_t plane_bytes = align_up((size_t)size_x * size_y * bpp, 256);

@@ -144,7 +144,25 @@ def test_flip_errors(ctx):
         ctx.flip_argb_device(None, src, 4, 4, True, True)
 
 
-# ---- projection glue: project every active channel + render (K3R fused, or K3 + K2) -------
+# ---- projection glue: project every active channel + render (K3 + K2, or the fused K3R) ----
+@pytest.fixture(scope="module")
+def k3r_ctx():
+    import os
+    import omr
+    os.environ["OMR_K3R"] = "1"                 # read at context creation
+    try:
+        c = omr.Context(0)
+    finally:
+        del os.environ["OMR_K3R"]
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["k3_k2", "k3r"])
+def glue_ctx(request, ctx, k3r_ctx):
+    return ctx if request.param == "k3_k2" else k3r_ctx
+
+
 def _glue(ctx, chans, stacks, pt, w, h, z, alg, start, end, stepping=1, be=False, flip=(False, False),
           model="rgb", qd_kw=None):
     import torch
@@ -177,7 +195,8 @@ GLUE_TYPES = [(_lib.PIXELS_UINT16, np.uint16, (0.0, 65535.0)), (_lib.PIXELS_INT1
 @pytest.mark.parametrize("pt,dtype,rng_", GLUE_TYPES)
 @pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM])
 @pytest.mark.parametrize("be", [False, True])
-def test_projection_glue_types_and_algorithms(ctx, pt, dtype, rng_, alg, be):
+def test_projection_glue_types_and_algorithms(glue_ctx, pt, dtype, rng_, alg, be):
+    ctx = glue_ctx
     z, h, w = 13, 48, 64
     stacks = [rand_stack(dtype, z, h, w, 300 + c) for c in range(3)]
     if be:
@@ -192,7 +211,8 @@ def test_projection_glue_types_and_algorithms(ctx, pt, dtype, rng_, alg, be):
 
 @pytest.mark.parametrize("n_ch", [1, 2, 4])
 @pytest.mark.parametrize("flip", [(False, False), (False, True), (True, True)])
-def test_projection_glue_channels_flips_modes(ctx, n_ch, flip):
+def test_projection_glue_channels_flips_modes(glue_ctx, n_ch, flip):
+    ctx = glue_ctx
     z, h, w = 64, 64, 128
     rng = np.random.default_rng(n_ch)
     stacks = [np.clip(microscopy_u16(h, w, rng).astype(np.int64) + rng.integers(-300, 300, (z, h, w)), 0,
@@ -208,7 +228,8 @@ def test_projection_glue_channels_flips_modes(ctx, n_ch, flip):
           qd_kw={"cd_start": 30, "cd_end": 220})
 
 
-def test_projection_glue_unfused_cases(ctx):
+def test_projection_glue_unfused_cases(glue_ctx):
+    ctx = glue_ctx
     """Odd width, five channels, 8-bit mean, float: the K3 + K2 path, same results."""
     rng = np.random.default_rng(9)
     z = 9
@@ -227,7 +248,8 @@ def test_projection_glue_unfused_cases(ctx):
     _glue(ctx, cf, sf, _lib.PIXELS_FLOAT, 32, 16, z, _lib.PROJECTION_MAX, 0, z - 1)
 
 
-def test_projection_glue_quantization_error(ctx):
+def test_projection_glue_quantization_error(glue_ctx):
+    ctx = glue_ctx
     import torch
     z, h, w = 4, 16, 32
     stacks = [np.full((z, h, w), 100, np.uint16) for _ in range(2)]
