@@ -264,7 +264,9 @@ omr_status omr_render_packed_int_device(omr_ctx* ctx, const omr_quantum_def* qde
 /*
  * Batch of n_tiles same-settings tile requests (one viewer's tiles; the request-level
  * parallelism of ImageRegionMicroserviceVerticle.java:149-165 coalesced into one launch).
- * d_plane_ptrs: DEVICE array of n_tiles*size_c device pointers ([tile][channel]).
+ * d_plane_ptrs: DEVICE array of n_tiles*size_c device pointers ([tile][channel]); each plane
+ * must start 16-byte aligned when width and row_stride are multiples of 16 bytes' worth of pixels
+ * (the vector path: 16-B loads), which the library cannot check on the host.
  * d_argb_out: device [n_tiles][height][width].  d_status (optional, device int32[n_tiles]):
  * per-tile OMR_OK / OMR_QUANTIZATION.  Asynchronous on the context stream.
  */

@@ -150,6 +150,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     c->stream = c->own_stream;
     if (const char* v = std::getenv("OMR_K2_NT_STORE")) c->k2_nt_store = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_K3R")) c->k3r = std::atoi(v) != 0;
+    if (const char* v = std::getenv("OMR_K2_EVAL_CPT")) c->k2_eval_cpt = std::atoi(v) == 4 ? 4 : 2;
     *out = c;
     return OMR_OK;
 }

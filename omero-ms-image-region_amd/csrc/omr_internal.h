@@ -89,11 +89,14 @@ struct Ctx {
     hipEvent_t pin_ev[kPinSlots] = {};
     int pin_slot = 0;
     int cu_count = 256;
-    bool k2_nt_store = true;
+    bool k2_nt_store = false;   // env OMR_K2_NT_STORE=1: non-temporal ARGB stores (measurement switch)
     uint32_t sem = 0;            // OMR_SEM_* (omr_ctx_set_semantics)
     // projection glue through the fused K3R kernel (env OMR_K3R=1; measured slower than K3 + K2
     // on C3, DESIGN.md §K3R, so off by default)
-    bool k3r = false;     // env OMR_K2_NT_STORE=0: plain ARGB stores (measurement switch)
+    bool k3r = false;
+    // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
+    // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
+    int k2_eval_cpt = 2;
     // kernel timing (omr_ctx_enable_kernel_timing)
     bool timing = false;
     struct Timed { hipEvent_t start, stop; int kind; };

@@ -711,8 +711,21 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
 }
 
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
-static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s) {
+static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s, int cpt = kCPT) {
     const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
+    if constexpr (BPP == 4 && VEC > 1 && (MODE == kK2Thresh || MODE == kK2Eval)) {
+        // grid-stride float / 32-bit modes, OMR_K2_EVAL_CPT=4: 4 chunks per lane (12 loads in
+        // flight at 3 channels; measured slower than kCPT on C5)
+        if (cpt == 4) {
+            switch (na) {
+            case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            default: break;
+            }
+        }
+    }
     if constexpr (BPP <= 2 && kCPT > 1) {   // grid-stride eval modes size their own grid
         if (small) {
             switch (na) {
@@ -735,7 +748,8 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small
 }
 
 template <int BPP, int VEC, bool BE>
-static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, int grid, bool small, hipStream_t s) {
+static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, int grid, bool small, hipStream_t s,
+                                   int cpt) {
     if constexpr (BPP == 1) {
         return pt == OMR_PIXELS_INT8 ? launch_render_na<1, VEC, BE, true, OMR_PIXELS_INT8, kK2Table8>(a, na, grid, small, s)
                                      : launch_render_na<1, VEC, BE, false, OMR_PIXELS_UINT8, kK2Table8>(a, na, grid, small, s);
@@ -750,13 +764,13 @@ static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, 
                                      : launch_render_na<2, VEC, BE, false, OMR_PIXELS_UINT16, kK2Mixed16>(a, na, grid, small, s);
     } else if constexpr (BPP == 4) {
         if (mode16 == kK2Thresh) {
-            if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Thresh>(a, na, grid, small, s);
-            if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Thresh>(a, na, grid, small, s);
-            return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Thresh>(a, na, grid, small, s);
+            if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Thresh>(a, na, grid, small, s, cpt);
+            if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Thresh>(a, na, grid, small, s, cpt);
+            return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Thresh>(a, na, grid, small, s, cpt);
         }
-        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, small, s);
-        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, small, s);
-        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, small, s);
+        if (pt == OMR_PIXELS_FLOAT) return launch_render_na<4, VEC, BE, false, OMR_PIXELS_FLOAT, kK2Eval>(a, na, grid, small, s, cpt);
+        if (pt == OMR_PIXELS_INT32) return launch_render_na<4, VEC, BE, true, OMR_PIXELS_INT32, kK2Eval>(a, na, grid, small, s, cpt);
+        return launch_render_na<4, VEC, BE, false, OMR_PIXELS_UINT32, kK2Eval>(a, na, grid, small, s, cpt);
     } else {
         return launch_render_na<8, VEC, BE, false, OMR_PIXELS_DOUBLE, kK2Eval>(a, na, grid, small, s);
     }
@@ -764,9 +778,9 @@ static hipError_t launch_render_pt(const K2Args& a, int pt, int na, int mode16, 
 
 template <int BPP, int VEC>
 static hipError_t launch_render_be(const K2Args& a, int pt, bool be, int na, int mode16, int grid, bool small,
-                                   hipStream_t s) {
-    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, mode16, grid, small, s)
-              : launch_render_pt<BPP, VEC, false>(a, pt, na, mode16, grid, small, s);
+                                   hipStream_t s, int cpt) {
+    return be ? launch_render_pt<BPP, VEC, true>(a, pt, na, mode16, grid, small, s, cpt)
+              : launch_render_pt<BPP, VEC, false>(a, pt, na, mode16, grid, small, s, cpt);
 }
 
 // kK2Fast16 preconditions (see fast16): default codomain, increasing window, finite slope,
@@ -889,7 +903,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cd_end = pp.plan.cd_end;
     a.cds8 = pp.plan.cd_start & 0xFF;
     a.cde8 = pp.plan.cd_end & 0xFF;
-    const int cpt_thread = (na >= 1 && na <= 4 && !small) ? kCPT : 1;
+    // chunks per lane: kCPT (the float / 32-bit vector path: the context's k2_eval_cpt), 1 for
+    // small launches and the runtime-channel-count kernels
+    const int cpt_thread = (na >= 1 && na <= 4 && !small) ? (bpp == 4 && aligned ? ctx->k2_eval_cpt : kCPT) : 1;
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.nt_store = ctx->k2_nt_store ? 1 : 0;
     a.total = (uint32_t)total;
@@ -929,17 +945,17 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     KernelTimer timer(ctx, 2);
     if (aligned) {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
         }
     } else {
         switch (bpp) {
-        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
-        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream); break;
+        case 1: e = launch_render_be<1, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        case 2: e = launch_render_be<2, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        case 4: e = launch_render_be<4, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        default: e = launch_render_be<8, 1>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
         }
     }
     OMR_HIP(ctx, e);
@@ -1076,9 +1092,11 @@ omr_status omr_render_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
     if (st) return st;
     if (d_status) OMR_HIP(ctx, hipMemsetAsync(d_status, 0, sizeof(int32_t) * (size_t)n_tiles, ctx->stream));
     const int bpp = bytes_per_pixel(pixel_type);
+    // the plane pointers live on the device: 16-B alignment is the caller's contract (omr.h); the
+    // output is checked here (its 16-B vector stores fall back to scalar ones when misaligned)
+    const bool aligned = vec_aligned(bpp, width, row_stride) && reinterpret_cast<uintptr_t>(d_argb_out) % 16 == 0;
     return enqueue_render(ctx, pp, pixel_type, big_endian, d_plane_ptrs, size_c, n_tiles, row_stride,
-                          width, height, flip_h, flip_v, d_argb_out, d_status,
-                          vec_aligned(bpp, width, row_stride), L);
+                          width, height, flip_h, flip_v, d_argb_out, d_status, aligned, L);
 }
 
 omr_status omr_render_batch_strided_device(omr_ctx* ctx, const omr_quantum_def* qdef,

@@ -13,7 +13,7 @@ for s in $STEPS; do
       (grep -m1 "model name" /proc/cpuinfo; nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null;
        grep -m1 -o -w avx512f /proc/cpuinfo; rocm-smi --showclocks 2>/dev/null | head -30) > $OUT/info.txt 2>&1 ;;
     series)
-      timeout -k 10 180 python -u tools/k2_series.py > $OUT/k2_series_nt1.json 2> $OUT/k2_series_nt1.err || exit $?
+      OMR_K2_NT_STORE=1 timeout -k 10 180 python -u tools/k2_series.py > $OUT/k2_series_nt1.json 2> $OUT/k2_series_nt1.err || exit $?
       OMR_K2_NT_STORE=0 timeout -k 10 180 python -u tools/k2_series.py > $OUT/k2_series_nt0.json 2> $OUT/k2_series_nt0.err || exit $? ;;
     bench)
       timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || exit $? ;;

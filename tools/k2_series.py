@@ -49,7 +49,7 @@ def main():
         s = sorted(v)
         return {"n": len(v), "min": s[0], "med": s[len(s) // 2], "max": s[-1], "mean": round(sum(v) / len(v), 4),
                 "series": v[:40]}
-    res = {"batch": B, "nt_store": os.environ.get("OMR_K2_NT_STORE", "1")}
+    res = {"batch": B, "nt_store": os.environ.get("OMR_K2_NT_STORE", "0")}
     for _ in range(5):
         step()
     ctx.synchronize()
