@@ -47,6 +47,24 @@ __device__ __forceinline__ int quantize_eval(double x, const ChanParam& p, int c
 __device__ __forceinline__ uint32_t bswap16x2(uint32_t d) { return __builtin_amdgcn_perm(d, d, 0x02030001u); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t d) { return __builtin_amdgcn_perm(d, d, 0x00010203u); }
 
+// Packed 2 x u16 minimum / maximum (v_pk_min_u16 / v_pk_max_u16).
+typedef uint16_t omr_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(omr_u16x2, a), __builtin_bit_cast(omr_u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(omr_u16x2, a), __builtin_bit_cast(omr_u16x2, b)));
+}
+
+// Load through an explicit global (addrspace 1) pointer.  A pointer the compiler cannot prove
+// global (read from a device table, or selected between such a pointer and a kernarg one)
+// otherwise becomes a flat load, which also counts against lgkmcnt: every later LDS wait
+// (s_waitcnt lgkmcnt(0)) then waits for that HBM load too, serialising a prefetch.
+template <typename T>
+__device__ __forceinline__ T ld_global(const void* p) {
+    return *(const __attribute__((address_space(1))) T*)p;
+}
+
 // 32-bit magic-number division (n < 2^31, d >= 1).
 struct FastDiv {
     uint32_t d, mul, shift;

@@ -809,6 +809,8 @@ struct PlaneSource {
     __device__ PlaneSource(const FusedArgs& f, const uint32_t* sc, int tile, int w, int h)
         : F(f), s_contrib(sc), W(w), H(h) {
 #pragma unroll
+        for (int a = 0; a < NA; ++a) { mn[a] = 0xFFFFFFFFu; mx[a] = 0u; }
+#pragma unroll
         for (int a = 0; a < kFusedMaxActive; ++a) {
             const int c = F.R.ch[a].index;
             base[a] = F.strided ? F.sbase + (int64_t)tile * F.tile_stride + (int64_t)c * F.chan_stride
@@ -823,16 +825,22 @@ struct PlaneSource {
         const int64_t r1 = (int64_t)(F.flip_v ? H - 2 - y0 : y0 + 1) * F.row_stride + sx;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            if constexpr (BPP == 2) {
-                raw[a][0] = *reinterpret_cast<const uint32_t*>(base[a] + r0 * 2);
-                raw[a][1] = *reinterpret_cast<const uint32_t*>(base[a] + r1 * 2);
+            if constexpr (BPP == 2) {   // global, not flat, loads: see ld_global
+                raw[a][0] = ld_global<uint32_t>(base[a] + r0 * 2);
+                raw[a][1] = ld_global<uint32_t>(base[a] + r1 * 2);
             } else {
-                raw[a][0] = *reinterpret_cast<const uint16_t*>(base[a] + r0);
-                raw[a][1] = *reinterpret_cast<const uint16_t*>(base[a] + r1);
+                raw[a][0] = ld_global<uint16_t>(base[a] + r0);
+                raw[a][1] = ld_global<uint16_t>(base[a] + r1);
             }
         }
     }
+    // 16-bit LUT-domain check (QuantizationException): per channel, the packed 2 x 16-bit
+    // minimum and maximum of the lane's pixels (sign-biased for signed types, so one unsigned
+    // v_pk_min/max_u16 covers two pixels) are kept and compared with [gmin, gmax] once in
+    // finish(), instead of two compares and a select per pixel.
+    uint32_t mn[NA], mx[NA];
     // contribution-table entry of pixel j (0: lower address, 1: upper) of raw word w, channel a
+    // (16-bit types: w already in native byte order)
     __device__ __forceinline__ uint32_t entry(int a, uint32_t w, int j) {
         const uint32_t* tab = s_contrib + a * 256;
         if constexpr (BPP == 1) {
@@ -840,11 +848,9 @@ struct PlaneSource {
             err |= (e & kErrBit) != 0;
             return e & ~kErrBit;
         } else {
-            if constexpr (BE) w = bswap16x2(w);
             const uint32_t h = j ? (w >> 16) : (w & 0xFFFF);
             const int x = F.R.is_signed ? (int)(int16_t)h : (int)h;
             const K2Chan& p = F.R.ch[a];
-            if (p.check) err |= (x < p.gmin) | (x > p.gmax);
             uint32_t v;
             if constexpr (MODE == kFusedFast16) {
                 v = fast16(x, p);
@@ -862,10 +868,20 @@ struct PlaneSource {
         const int jl = F.flip_h ? 1 : 0;        // which half of the pair is the left output pixel
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            acc[0] += entry(a, raw[a][0], jl);
-            acc[1] += entry(a, raw[a][0], jl ^ 1);
-            acc[2] += entry(a, raw[a][1], jl);
-            acc[3] += entry(a, raw[a][1], jl ^ 1);
+            uint32_t w0 = raw[a][0], w1 = raw[a][1];
+            if constexpr (BPP == 2) {
+                if constexpr (BE) { w0 = bswap16x2(w0); w1 = bswap16x2(w1); }
+                if (F.R.any_check) {              // wave-uniform
+                    const uint32_t sg = F.R.is_signed ? 0x80008000u : 0u;
+                    const uint32_t b0 = w0 ^ sg, b1 = w1 ^ sg;
+                    mn[a] = pk_min_u16(mn[a], pk_min_u16(b0, b1));
+                    mx[a] = pk_max_u16(mx[a], pk_max_u16(b0, b1));
+                }
+            }
+            acc[0] += entry(a, w0, jl);
+            acc[1] += entry(a, w0, jl ^ 1);
+            acc[2] += entry(a, w1, jl);
+            acc[3] += entry(a, w1, jl ^ 1);
         }
         uint32_t px[4];
 #pragma unroll
@@ -876,6 +892,23 @@ struct PlaneSource {
         p00 = px[0]; p01 = px[1]; p10 = px[2]; p11 = px[3];
     }
     __device__ __forceinline__ uint32_t at(int, int) const { return 0; }   // never: H % 16 == 0
+    // after the last MCU: fold the 16-bit domain extremes into err
+    __device__ __forceinline__ void finish() {
+        if constexpr (BPP == 2) {
+            if (!F.R.any_check) return;
+            const uint32_t sg = F.R.is_signed ? 0x8000u : 0u;
+#pragma unroll
+            for (int a = 0; a < NA; ++a) {
+                const K2Chan& p = F.R.ch[a];
+                if (!p.check) continue;
+                const uint32_t lo = min(mn[a] & 0xFFFFu, mn[a] >> 16) ^ sg;
+                const uint32_t hi = max(mx[a] & 0xFFFFu, mx[a] >> 16) ^ sg;
+                const int xl = F.R.is_signed ? (int)(int16_t)lo : (int)lo;
+                const int xh = F.R.is_signed ? (int)(int16_t)hi : (int)hi;
+                err |= (xl < p.gmin) | (xh > p.gmax);
+            }
+        }
+    }
 };
 
 // The B1 body for one pixel source (see k_jpeg_fdct_batch below).
@@ -1035,6 +1068,7 @@ __global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F)
     __syncthreads();
     PlaneSource<BPP, BE, MODE, NA> src(F, s_contrib, blockIdx.y, A.W, A.H);
     b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
+    src.finish();
     if (__ballot(src.err)) {
         if ((threadIdx.x & 63) == 0) {
             atomicOr(F.R.flag, 1);

@@ -96,7 +96,8 @@ struct FusedRender {
     const uint8_t* ws_base;      // workspace base (kModeLut16 byte LUTs)
     int32_t* flag;               // sticky quantization-error word
     int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
-    int32_t pad[2];
+    int32_t any_check;           // some channel's LUT domain is narrower than its pixel type
+    int32_t pad;
 };
 
 // Host side (omr_render.hip).  render_fused_plan: true when the fused kernel covers these

@@ -1030,6 +1030,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.gmin = c.gmin;
         k.gmax = c.gmax;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
+        F.any_check |= k.check;
         k.second = c.second;
         k.ws = c.ws;
         k.a0 = c.a0;

@@ -150,3 +150,22 @@ def test_quantization_error_flags_its_tile(ctx, fused):
     assert st.tolist() == [0, _lib.QUANTIZATION, 0]
     exp = _expect(chans, [tiles[0], tiles[2]], _lib.PIXELS_UINT16, w, h)
     assert files[0] == exp[0] and files[2] == exp[1]
+
+
+def test_quantization_error_signed_lower_and_upper_bounds(ctx):
+    """Fused 16-bit domain check (packed per-lane min/max, folded once per lane): int16 planes,
+    a pixel exactly at globalMin / globalMax is inside, one below / above flags only its tile."""
+    w, h = 128, 64
+    rng = np.random.default_rng(11)
+    tiles = [[rng.integers(-900, 900, (h, w)).astype(np.int16) for _ in range(2)] for _ in range(4)]
+    tiles[0][0][0, 0], tiles[0][1][63, 127] = -1000, 1000       # on the bounds: fine
+    tiles[1][0][17, 33] = -1001                                 # below globalMin
+    tiles[3][1][40, 2] = 1001                                   # above globalMax
+    chans = [{"input_start": f32(-800.0), "input_end": f32(700.0), "global_min": -1000.0, "global_max": 1000.0,
+              "rgba": (255, 0, 0, 255)},
+             {"input_start": f32(-50.0), "input_end": f32(900.0), "global_min": -1000.0, "global_max": 1000.0,
+              "rgba": (0, 255, 255, 255)}]
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h)
+    assert st.tolist() == [0, _lib.QUANTIZATION, 0, _lib.QUANTIZATION]
+    exp = _expect(chans, [tiles[0], tiles[2]], _lib.PIXELS_INT16, w, h)
+    assert files[0] == exp[0] and files[2] == exp[1]

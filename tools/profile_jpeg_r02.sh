@@ -7,7 +7,7 @@ R=$PWD
 O=$R/gpurun_out/${1:-jpeg_pmc_r02}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-for case in c2 c1; do
+for case in ${JPEG_CASES:-c2 c1}; do
   i=0
   for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU_FP64 SQ_INSTS_SMEM" \
              "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_BUSY_CYCLES" \
