@@ -1094,6 +1094,7 @@ __device__ __forceinline__ uint32_t dc_bits(const int16_t* dcs, int b, const Huf
 }
 
 constexpr int kTileThreads = 1024;
+constexpr int kB3LdsWords = 4096;   // B3: a group's stream staged in LDS up to 512 bits per block
 constexpr int kGrp = 256;   // blocks per B3 workgroup = chunks per B4a/B6 group
 
 __device__ __forceinline__ uint32_t block_reduce_sum(uint32_t v, uint32_t* s_wave) {
@@ -1138,7 +1139,7 @@ struct GroupScanArgs {
     uint32_t* gsum;              // [tile][stride] -> exclusive offsets
     const uint32_t* n_groups;    // [tile] (nullptr: fixed_groups)
     uint32_t* total;             // [tile]
-    uint32_t* zero_words;        // B2b: [tile][slot_words] zero-filled up to the total (or nullptr)
+    uint32_t* zero_words;        // B2b: [tile][slot_words] words B3 ORs into, zeroed (or nullptr)
     const uint32_t* base_add;    // B4b: total += base_add-derived byte count (or nullptr)
     int64_t stride, slot_words;
     int32_t fixed_groups;
@@ -1147,10 +1148,12 @@ struct GroupScanArgs {
 __global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs A) {
     __shared__ uint32_t sw[16];
     __shared__ uint32_t carry;
+    __shared__ int s_unstaged;
     const int tile = blockIdx.x;
     uint32_t* g = A.gsum + (int64_t)tile * A.stride;
     const uint32_t ng = A.n_groups ? A.n_groups[tile] : (uint32_t)A.fixed_groups;
-    if (threadIdx.x == 0) carry = 0;
+    uint32_t* zw = A.zero_words ? A.zero_words + (int64_t)tile * A.slot_words : nullptr;
+    if (threadIdx.x == 0) { carry = 0; s_unstaged = 0; }
     __syncthreads();
     for (uint32_t base = 0; base < ng; base += kTileThreads) {
         const uint32_t i = base + threadIdx.x;
@@ -1159,6 +1162,14 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs 
         const uint32_t ex = block_exclusive_scan(v, sw, tot);
         const uint32_t c = carry;
         if (i < ng) g[i] = c + ex;
+        // B2b: B3 builds a group's words in LDS and ORs only its first and last word into HBM
+        // (shared with the neighbouring groups), so only those need zeroing; a group too long
+        // for B3's LDS (ORs at every block boundary) makes the whole tile zeroed below
+        if (zw && i < ng && v) {
+            const uint32_t w0 = (c + ex) >> 5, w1 = (c + ex + v - 1) >> 5;
+            if (w1 - w0 + 1 <= (uint32_t)kB3LdsWords) { zw[w0] = 0; zw[w1] = 0; }
+            else s_unstaged = 1;
+        }
         __syncthreads();
         if (threadIdx.x == 0) carry = c + tot;
         __syncthreads();
@@ -1166,9 +1177,9 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs 
     uint32_t total = carry;
     if (A.base_add) total += (A.base_add[tile] + 7) / 8;   // B4b: stuffed bytes = bytes + 0xFF count
     if (threadIdx.x == 0) A.total[tile] = total;
-    if (A.zero_words) {                                    // B2b: the tile's bit stream words
+    if (zw && s_unstaged) {                                // every word of the tile's bit stream
         const uint32_t nw = (total + 31) / 32 + 1;
-        uint4* w4 = reinterpret_cast<uint4*>(A.zero_words + (int64_t)tile * A.slot_words);
+        uint4* w4 = reinterpret_cast<uint4*>(zw);
         for (uint32_t i = threadIdx.x; i < (nw + 3) / 4; i += kTileThreads) w4[i] = make_uint4(0, 0, 0, 0);
     }
 }
@@ -1189,7 +1200,6 @@ struct B3Args {
 // a static register), the codes come from the LDS Huffman tables and accumulate in a 64-bit
 // register; whole 32-bit words are stored directly, the two words a block may share with its
 // neighbours are ORed in.
-constexpr int kB3LdsWords = 4096;   // a group's stream staged in LDS up to 512 bits per block
 
 __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     __shared__ HuffLds h;
@@ -1479,8 +1489,23 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
         __syncthreads();
         const uint32_t gbytes = min(nbytes - g * kGrp * kStuffBytes, (uint32_t)(kGrp * kStuffBytes)) + gtot;
         const uint64_t base = (uint64_t)g * kGrp * kStuffBytes + A.coff[(int64_t)tile * A.slot_groups + g];
+        // copy out: 16-byte stores from the first 16-byte aligned output byte on (the group's
+        // bytes start anywhere), each assembled from five LDS words by a funnel shift; the
+        // unaligned head and the tail go byte by byte
         const uint8_t* sbytes = reinterpret_cast<const uint8_t*>(swords);
-        for (uint32_t i = threadIdx.x; i < gbytes; i += kGrp) out[base + i] = sbytes[i];
+        uint8_t* dst = out + base;
+        const uint32_t head = min((16u - (uint32_t)((uintptr_t)dst & 15u)) & 15u, gbytes);
+        const uint32_t nv = (gbytes - head) / 16, tail0 = head + nv * 16;
+        if (threadIdx.x < head) dst[threadIdx.x] = sbytes[threadIdx.x];
+        const uint32_t sh = 8 * (head & 3u);
+        for (uint32_t j = threadIdx.x; j < nv; j += kGrp) {
+            const uint32_t* sw4 = swords + (head >> 2) + 4 * j;
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = sh ? (sw4[k] >> sh) | (sw4[k + 1] << (32 - sh)) : sw4[k];
+            *reinterpret_cast<uint4*>(dst + head + 16 * j) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        for (uint32_t i = tail0 + threadIdx.x; i < gbytes; i += kGrp) dst[i] = sbytes[i];
         __syncthreads();
     }
 }

@@ -18,7 +18,8 @@ def main():
     from omr.context import make_bindings, make_qdef
     from omr.renderer import f32
     from omr.synthetic import C2_COLORS
-    T, B, uniq = 1024, 32, 4
+    T, uniq = 1024, 4
+    B = int(os.environ.get("C5_TILES", "32"))
     rng = np.random.default_rng(20261015 + 5)
     host = np.stack([np.stack([rng.lognormal(5, 1.5, (T, T)).astype(np.float32),
                                rng.normal(0, 300, (T, T)).astype(np.float32),
