@@ -44,6 +44,19 @@ omr_status ensure_workspace(Ctx* c, size_t bytes) {
     return OMR_OK;
 }
 
+omr_status ensure_host_out(Ctx* c, size_t bytes) {
+    if (bytes <= c->h_out_cap) return OMR_OK;
+    if (c->h_out) {
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        OMR_HIP(c, hipHostFree(c->h_out));
+        c->h_out = nullptr;
+        c->h_out_cap = 0;
+    }
+    OMR_HIP(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_out), bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    c->h_out_cap = bytes;
+    return OMR_OK;
+}
+
 omr_status ensure_aux(Ctx* c, size_t bytes) {
     if (bytes <= c->aux_cap) return OMR_OK;
     if (c->aux) {
@@ -150,6 +163,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     c->stream = c->own_stream;
     if (const char* v = std::getenv("OMR_K2_NT_STORE")) c->k2_nt_store = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_K3R")) c->k3r = std::atoi(v) != 0;
+    if (const char* v = std::getenv("OMR_PNG_DEVICE_D3")) c->png_device_d3 = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_K2_EVAL_CPT")) c->k2_eval_cpt = std::atoi(v) == 4 ? 4 : 2;
     *out = c;
     return OMR_OK;

@@ -94,6 +94,9 @@ struct Ctx {
     // projection glue through the fused K3R kernel (env OMR_K3R=1; measured slower than K3 + K2
     // on C3, DESIGN.md §K3R, so off by default)
     bool k3r = false;
+    // PNG D3 (Huffman tables) on the device (env OMR_PNG_DEVICE_D3=1): no mid-encode host round
+    // trip, but the single-workgroup build measured slower than the host's
+    bool png_device_d3 = false;
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
     int k2_eval_cpt = 2;
@@ -123,6 +126,8 @@ omr_status hip_fail(Ctx* c, hipError_t e, const char* what);
 omr_status ensure_workspace(Ctx* c, size_t bytes);
 // Ensure ctx->aux holds at least `bytes` (contents not preserved across growth).
 omr_status ensure_aux(Ctx* c, size_t bytes);
+// Fine-grained pinned landing buffer (ctx->h_out) of at least `bytes` (grow-only).
+omr_status ensure_host_out(Ctx* c, size_t bytes);
 // Copy `bytes` from host `src` to device `dst` through the pinned ring (async on ctx stream).
 // Move the sticky device status word to fine-grained host memory and clear it, on `s`
 // (omr_render.hip): omr_ctx_synchronize then needs one stream sync and no copy round trip.

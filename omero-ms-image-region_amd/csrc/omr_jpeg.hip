@@ -1696,17 +1696,8 @@ static omr_status encode_jpeg_single_batched(Ctx* ctx, const uint32_t* d_argb, i
     if (st) return st;
     // the file lands in the context's pinned buffer straight from the device (one sync, no
     // length round trip before the copy)
-    if (ctx->h_out_cap < jcap + 16) {
-        if (ctx->h_out) {
-            OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            OMR_HIP(ctx, hipHostFree(ctx->h_out));
-            ctx->h_out = nullptr;
-            ctx->h_out_cap = 0;
-        }
-        OMR_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_out), jcap + 16,
-                                   hipHostMallocCoherent | hipHostMallocMapped));
-        ctx->h_out_cap = jcap + 16;
-    }
+    st = ensure_host_out(ctx, jcap + 16);
+    if (st) return st;
     hipLaunchKernelGGL(k_file_to_host, dim3((unsigned)((jcap + 16 * 256 - 1) / (16 * 256))), dim3(256), 0,
                        ctx->stream, ws + o_out, d_lens, ctx->h_out);
     OMR_HIP(ctx, hipGetLastError());

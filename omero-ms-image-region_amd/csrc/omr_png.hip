@@ -6,10 +6,13 @@
 // (:165-221): MSB-first bit mask -> (flip) -> 2-entry palette PNG (index 0 transparent,
 // index 1 = fill colour; 1-bit rows when width % 8 == 0, else 8-bit, :174-198).
 //
-// PNG is compared decoded (pixels), so the zlib stream uses stored deflate blocks: every
-// output byte is a pure function of its index, written by one lane; Adler-32 is a parallel
-// 64-bit reduction; CRC-32 is per-segment CRCs combined with x^(8n) mod P multiplications
-// (XOR-reduction), so the whole IDAT chunk is built on the device.
+// PNG is compared decoded (pixels), so the filter choice and the deflate parse are ours: the
+// zlib stream is one dynamic-Huffman block built on the device (D1-D6 below), or stored blocks
+// when that is shorter (noise; every output byte then a pure function of its index).  Adler-32
+// is a parallel 64-bit reduction; CRC-32 is per-segment CRCs combined with x^(8n) mod P
+// multiplications (XOR-reduction).  The whole IDAT chunk is built on the device, stored vs
+// dynamic is decided there, and the chunk lands in pinned host memory: one stream sync per
+// encode.
 #include "omr_device.h"
 
 namespace omr {
@@ -98,8 +101,13 @@ struct PngArgs {
     int64_t rowlen;          // 1 + row bytes
     int64_t raw;             // rowlen * H
     int64_t nblk;            // stored blocks
-    int64_t zlen;            // zlib stream length (2 + 5*nblk + raw + 4)
+    int64_t zlen;            // zlib stream length of the stored encoding (2 + 5*nblk + raw + 4)
+    // [0] zlib stream length chosen on the device (stored or dynamic), [1] 1 = stored blocks,
+    // [2] IDAT chunk bytes (8 + zlen + 4); written by k_png_select
+    int64_t* meta;
 };
+
+__device__ __forceinline__ int64_t png_zlen(const PngArgs& A) { return A.meta[0]; }
 
 __device__ __forceinline__ uint32_t mask_bit(const PngArgs& A, int x, int y) {
     const int sx = A.flip_h ? A.W - 1 - x : x, sy = A.flip_v ? A.H - 1 - y : y;
@@ -124,6 +132,7 @@ __device__ __forceinline__ uint32_t raw_byte(const PngArgs& A, int64_t i) {
 
 // One lane per zlib-stream byte (header, stored-block headers, payload) + Adler partials.
 __global__ void __launch_bounds__(256) k_png_layout(PngArgs A) {
+    if (A.meta[1] == 0) return;                     // the dynamic stream was chosen
     unsigned long long s1 = 0, s2 = 0;
     uint8_t* z = A.chunk + 8;
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < A.zlen - 4; j += (int64_t)gridDim.x * 256) {
@@ -165,10 +174,11 @@ __global__ void __launch_bounds__(256) k_png_layout(PngArgs A) {
 __global__ void k_png_adler(PngArgs A) {
     const uint64_t a = (1 + A.sums[0]) % 65521, b = ((uint64_t)A.raw % 65521 + A.sums[1] % 65521) % 65521;
     const uint32_t adler = (uint32_t)((b << 16) | a);
-    uint8_t* t = A.chunk + 8 + A.zlen - 4;
+    const int64_t zlen = png_zlen(A);
+    uint8_t* t = A.chunk + 8 + zlen - 4;
     t[0] = adler >> 24; t[1] = adler >> 16; t[2] = adler >> 8; t[3] = adler;
     // chunk length and type now: the type is the first 4 bytes the CRC covers
-    const uint32_t len = (uint32_t)A.zlen;
+    const uint32_t len = (uint32_t)zlen;
     A.chunk[0] = len >> 24; A.chunk[1] = len >> 16; A.chunk[2] = len >> 8; A.chunk[3] = len;
     A.chunk[4] = 'I'; A.chunk[5] = 'D'; A.chunk[6] = 'A'; A.chunk[7] = 'T';
 }
@@ -202,7 +212,7 @@ __global__ void __launch_bounds__(256) k_png_crc(PngArgs A) {
     __shared__ uint32_t s_x[4];
     for (int i = threadIdx.x; i < 8 * 256; i += 256) t[i >> 8][i & 255] = c_crc8.t[i >> 8][i & 255];
     __syncthreads();
-    const int64_t n = 4 + A.zlen;
+    const int64_t n = 4 + png_zlen(A);
     const uint8_t* d = A.chunk + 4;                 // 4-byte aligned (chunk is 256-aligned)
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t b0 = s * kCrcSeg;
@@ -231,7 +241,7 @@ __global__ void __launch_bounds__(256) k_png_crc(PngArgs A) {
 
 __global__ void k_png_finish(PngArgs A) {
     const uint32_t crc = *A.crc_out;
-    uint8_t* c = A.chunk + 8 + A.zlen;
+    uint8_t* c = A.chunk + 8 + png_zlen(A);
     c[0] = crc >> 24; c[1] = crc >> 16; c[2] = crc >> 8; c[3] = crc;
 }
 
@@ -242,12 +252,12 @@ __global__ void k_png_finish(PngArgs A) {
 //   D1 k_png_filter     one workgroup per row: the five PNG filters, pick the minimum sum of
 //                       |signed residual| (libpng's heuristic), write filter byte + row; Adler
 //                       partials
-//   D2 k_png_lz_parse   one lane per 256-byte segment (staged in LDS with one row of look-back):
+//   D2 k_png_lz_parse   one lane per 32-byte segment (staged in LDS with one row of look-back):
 //                       greedy LZ77 over
 //                       the distances image rows repeat at (1, bpp, 2*bpp, one row up; matches
 //                       may reach back into earlier segments, never past the segment end);
 //                       tokens + symbol histograms
-//   D3 (host)           length-limited (15-bit) Huffman codes for literal/length and distance
+//   D3 k_png_tables     length-limited (15-bit) Huffman codes for literal/length and distance
 //                       symbols from the two histograms, the run-length coded code-length
 //                       header (7-bit code) — one dynamic block for the whole image
 //   D4 k_png_lz_bits    bits per segment -> exclusive scan -> bit offsets
@@ -435,8 +445,9 @@ __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
     }
 }
 
-// Sum of the per-row Adler partials into A.sums (one workgroup).
+// Sum of the per-row Adler partials into A.sums (one workgroup; dynamic stream only).
 __global__ void __launch_bounds__(256) k_png_adler_rows(DflArgs D) {
+    if (D.P.meta[1]) return;
     __shared__ unsigned long long s_ad[2][4];
     unsigned long long s1 = 0, s2 = 0;
     for (int y = threadIdx.x; y < D.P.H; y += 256) { s1 += D.row_sums[2 * y]; s2 += D.row_sums[2 * y + 1]; }
@@ -514,10 +525,275 @@ __global__ void __launch_bounds__(kParseLanes) k_png_lz_parse(DflArgs D, int32_t
     if (threadIdx.x < 30 && dh[threadIdx.x]) atomicAdd(&D.dhist[threadIdx.x], dh[threadIdx.x]);
 }
 
-// ---- D3 on the host: the code is a function of two small histograms (286 + 30 counts), so it is
-// built on the CPU between two launches (one 1.3 KB read back, one 1 KB upload) instead of by a
-// single GPU lane.
+// ---- D3 on the device: the code is a function of two small histograms (286 + 30 counts); one
+// workgroup builds it between D2 and D4, so an encode needs no host round trip mid-pipeline.
+// The parallel steps (ranking, depths, length assignment, canonical codes) use every lane; the
+// two-queue merge, the Kraft repair and the run-length header are short serial loops on lane 0.
 
+// The table block D4/D5 read: codes, lengths and the block header bits.
+struct DflTables {
+    uint16_t lcode[286];
+    uint16_t dcode[30];
+    uint8_t llen[286];
+    uint8_t dlen[30];
+    uint32_t hdr[96];        // header bits LSB-first; hdr[95] = bit count
+};
+
+constexpr int kHuffMaxSym = 288;
+constexpr int kHuffThreads = 320;       // one symbol per thread (286 + 30 + 19 symbols: <= 286)
+struct HuffWork {                       // LDS scratch of one tree
+    alignas(16) uint32_t f[kHuffMaxSym];   // symbol frequencies
+    uint32_t wt[2 * kHuffMaxSym];       // leaf weights (sorted), then merged nodes
+    int16_t ord[kHuffMaxSym];           // used symbols by (frequency, symbol)
+    int16_t parent[2 * kHuffMaxSym];
+    uint8_t len[kHuffMaxSym];
+    int bl[17];                         // leaves per code length
+    int next[17];
+    int wcnt[kHuffThreads / 64][16];    // per wave: symbols of each code length
+    int m;
+};
+
+// Code lengths (<= maxbits) of the n symbols in W.f -> W.len, by the two-queue Huffman
+// construction (leaves sorted by (freq, symbol)), then miniz's tdefl_huffman_enforce_max_code_size:
+// clamp, then drop one max-length code and split the longest shorter code until the Kraft sum is
+// exactly 2^maxbits; the longest codes go to the least frequent symbols.  Fewer than two used
+// symbols get two 1-bit codes (RFC 1951 3.2.7 allows the unused one).  Every thread calls it.
+__device__ void huff_lengths_dev(HuffWork& W, int n, int maxbits) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) W.m = 0;
+    if (tid < 17) W.bl[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += nt) {
+        const uint32_t fi = W.f[i];
+        W.len[i] = 0;
+        if (fi) {                                   // rank among the used symbols (stable order)
+            int r = 0;
+            const int n4 = n & ~3;
+            const uint4* f4 = reinterpret_cast<const uint4*>(W.f);
+#pragma unroll 4
+            for (int j = 0; j < n4; j += 4) {       // four broadcast reads per LDS access
+                const uint4 v = f4[j >> 2];
+                r += (v.x != 0u && (v.x < fi || (v.x == fi && j < i))) ? 1 : 0;
+                r += (v.y != 0u && (v.y < fi || (v.y == fi && j + 1 < i))) ? 1 : 0;
+                r += (v.z != 0u && (v.z < fi || (v.z == fi && j + 2 < i))) ? 1 : 0;
+                r += (v.w != 0u && (v.w < fi || (v.w == fi && j + 3 < i))) ? 1 : 0;
+            }
+            for (int j = n4; j < n; ++j) {
+                const uint32_t fj = W.f[j];
+                r += (fj != 0u && (fj < fi || (fj == fi && j < i))) ? 1 : 0;
+            }
+            W.ord[r] = (int16_t)i;
+            atomicAdd(&W.m, 1);
+        }
+    }
+    __syncthreads();
+    const int m = W.m;
+    if (m < 2) {
+        if (tid == 0) {
+            const int a = m == 1 ? W.ord[0] : 0;
+            W.len[a] = 1;
+            W.len[a == 0 ? 1 : 0] = 1;
+        }
+        __syncthreads();
+        return;
+    }
+    for (int k = tid; k < m; k += nt) W.wt[k] = W.f[W.ord[k]];
+    __syncthreads();
+    if (tid == 0) {                                 // two queues: sorted leaves, merged nodes
+        // the two heads of each queue are read together (one LDS round trip per merge); a leaf
+        // wins ties, as wt[li] <= wt[qi] does
+        constexpr uint32_t kInf = 0xFFFFFFFFu;       // weights stay below it (< 2^31 bytes)
+        int li = 0, qi = m, qn = m;
+        for (int c = 0; c < m - 1; ++c) {
+            const uint32_t a = li < m ? W.wt[li] : kInf, b = li + 1 < m ? W.wt[li + 1] : kInf;
+            const uint32_t q0 = qi < qn ? W.wt[qi] : kInf, q1 = qi + 1 < qn ? W.wt[qi + 1] : kInf;
+            int p0, p1;
+            uint32_t w0, w1;
+            if (a <= q0) {                          // first: leaf li; second: leaf li+1 or node qi
+                p0 = li; w0 = a;
+                if (b <= q0) { p1 = li + 1; w1 = b; li += 2; }
+                else { p1 = qi; w1 = q0; li += 1; qi += 1; }
+            } else {                                // first: node qi; second: leaf li or node qi+1
+                p0 = qi; w0 = q0;
+                if (a <= q1) { p1 = li; w1 = a; li += 1; qi += 1; }
+                else { p1 = qi + 1; w1 = q1; qi += 2; }
+            }
+            W.wt[qn] = w0 + w1;
+            W.parent[p0] = W.parent[p1] = (int16_t)qn;
+            ++qn;
+        }
+    }
+    __syncthreads();
+    const int root = 2 * m - 2;
+    for (int k = tid; k < m; k += nt) {             // leaf depth: walk up to the root
+        int d = 0;
+        for (int x = k; x != root; x = W.parent[x]) ++d;
+        atomicAdd(&W.bl[min(d, maxbits)], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {                                 // Kraft repair after the clamp (in registers)
+        int bl[16];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) bl[b] = W.bl[b];
+        uint32_t total = 0;
+#pragma unroll
+        for (int b = 1; b < 16; ++b)
+            if (b <= maxbits) total += (uint32_t)bl[b] << (maxbits - b);
+        while (total != (1u << maxbits)) {
+#pragma unroll
+            for (int b = 1; b < 16; ++b)
+                if (b == maxbits) bl[b]--;
+            bool done = false;
+#pragma unroll
+            for (int b = 14; b > 0; --b)
+                if (!done && b < maxbits && bl[b]) { bl[b]--; bl[b + 1] += 2; done = true; }
+            --total;
+        }
+#pragma unroll
+        for (int b = 0; b < 16; ++b) W.bl[b] = bl[b];
+    }
+    __syncthreads();
+    for (int k = tid; k < m; k += nt) {             // rank k -> length (least frequent longest)
+        int cum = 0, b = maxbits;
+        for (; b > 1; --b) {
+            cum += W.bl[b];
+            if (k < cum) break;
+        }
+        W.len[W.ord[k]] = (uint8_t)b;
+    }
+    __syncthreads();
+}
+
+// Canonical codes of W.len (RFC 1951 3.2.2), bit-reversed for LSB-first packing; every thread
+// (kHuffThreads, one symbol each).  A symbol's rank among the symbols of its length: ballots
+// per length inside its wave, plus the counts of the waves before it.
+__device__ void huff_canon_dev(HuffWork& W, int n, uint16_t* code) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int l = tid < n ? W.len[tid] : 0;
+    const uint64_t lt = (1ull << lane) - 1;
+    int rk = 0;
+#pragma unroll
+    for (int b = 1; b < 16; ++b) {
+        const uint64_t mk = __ballot(l == b);
+        if (lane == 0) W.wcnt[wv][b] = __popcll(mk);
+        if (l == b) rk = __popcll(mk & lt);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int c = 0, prev = 0;
+        for (int b = 1; b < 16; ++b) {
+            c = (c + prev) << 1;
+            W.next[b] = c;
+            prev = 0;
+            for (int w = 0; w < kHuffThreads / 64; ++w) prev += W.wcnt[w][b];
+        }
+    }
+    __syncthreads();
+    if (tid < n) {
+        if (!l) {
+            code[tid] = 0;
+        } else {
+            for (int w = 0; w < wv; ++w) rk += W.wcnt[w][l];
+            const uint32_t v = (uint32_t)(W.next[l] + rk);
+            code[tid] = (uint16_t)(__brev(v) >> (32 - l));
+        }
+    }
+    __syncthreads();
+}
+
+// D3: one workgroup.  hist = [286 literal/length][30 distance] counts from D2.
+__global__ void __launch_bounds__(kHuffThreads) k_png_tables(const uint32_t* __restrict__ hist, DflTables* __restrict__ T) {
+    __shared__ HuffWork W;
+    __shared__ DflTables t;
+    __shared__ uint8_t seq[286 + 30];
+    __shared__ uint8_t rs[286 + 30], rx[286 + 30];   // run-length symbols and their extra bits
+    __shared__ int s_nr, s_hlit, s_hdist;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 286; i += kHuffThreads) W.f[i] = hist[i] + (i == 256 ? 1u : 0u);   // + EOB
+    huff_lengths_dev(W, 286, kMaxBits);
+    for (int i = tid; i < 286; i += kHuffThreads) t.llen[i] = W.len[i];
+    huff_canon_dev(W, 286, t.lcode);
+    if (tid < 30) W.f[tid] = hist[286 + tid];
+    huff_lengths_dev(W, 30, kMaxBits);
+    if (tid < 30) t.dlen[tid] = W.len[tid];
+    huff_canon_dev(W, 30, t.dcode);
+    if (tid == 0) {                                 // zlib trees.c scan_tree over the lengths
+        int hlit = 286, hdist = 30;
+        while (hlit > 257 && t.llen[hlit - 1] == 0) --hlit;
+        while (hdist > 1 && t.dlen[hdist - 1] == 0) --hdist;
+        for (int i = 0; i < hlit; ++i) seq[i] = t.llen[i];
+        for (int i = 0; i < hdist; ++i) seq[hlit + i] = t.dlen[i];
+        const int ns = hlit + hdist;
+        int nr = 0;
+        for (int i = 0; i < ns;) {
+            const int v = seq[i];
+            int r = 1;
+            while (i + r < ns && seq[i + r] == v) ++r;
+            if (v == 0 && r >= 3) {
+                const int k = min(r, 138);
+                rs[nr] = k >= 11 ? 18 : 17;
+                rx[nr++] = (uint8_t)(k >= 11 ? k - 11 : k - 3);
+                i += k;
+            } else if (v != 0 && r >= 4) {
+                const int k = min(r - 1, 6);
+                rs[nr] = (uint8_t)v; rx[nr++] = 0;
+                rs[nr] = 16; rx[nr++] = (uint8_t)(k - 3);
+                i += 1 + k;
+            } else {
+                rs[nr] = (uint8_t)v; rx[nr++] = 0;
+                ++i;
+            }
+        }
+        s_nr = nr; s_hlit = hlit; s_hdist = hdist;
+    }
+    if (tid < 19) W.f[tid] = 0;
+    __syncthreads();
+    const int nr = s_nr;
+    for (int i = tid; i < nr; i += kHuffThreads) atomicAdd(&W.f[rs[i]], 1u);
+    huff_lengths_dev(W, 19, 7);
+    __shared__ uint16_t ccode[19];
+    huff_canon_dev(W, 19, ccode);
+    for (int i = tid; i < 96; i += kHuffThreads) t.hdr[i] = 0;
+    // each run-length entry's code + extra bits (LSB-first: the code, then the extra), in parallel
+    __shared__ uint16_t ev[286 + 30];
+    __shared__ uint8_t en[286 + 30];
+    for (int i = tid; i < nr; i += kHuffThreads) {
+        const int sym = rs[i];
+        const int xb = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
+        ev[i] = (uint16_t)(ccode[sym] | ((uint32_t)rx[i] << W.len[sym]));
+        en[i] = (uint8_t)(W.len[sym] + xb);
+    }
+    __syncthreads();
+    if (tid == 0) {                                 // block header, LSB-first
+        static constexpr uint8_t kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+        int hclen = 19;
+        while (hclen > 4 && W.len[kOrd[hclen - 1]] == 0) --hclen;
+        uint32_t nb = 0;
+        uint64_t acc = 0;                           // pending bits, LSB-first; whole words out
+        auto put = [&](uint32_t v, int n) {
+            acc |= (uint64_t)(v & ((1u << n) - 1u)) << (nb & 31);   // n <= 14
+            nb += n;
+            if ((nb >> 5) != ((nb - n) >> 5)) { t.hdr[(nb - n) >> 5] = (uint32_t)acc; acc >>= 32; }
+        };
+        put(1, 1);                                  // BFINAL
+        put(2, 2);                                  // BTYPE = 10 (dynamic)
+        put((uint32_t)(s_hlit - 257), 5);
+        put((uint32_t)(s_hdist - 1), 5);
+        put((uint32_t)(hclen - 4), 4);
+        for (int i = 0; i < hclen; ++i) put(W.len[kOrd[i]], 3);
+        for (int i = 0; i < nr; ++i) put(ev[i], en[i]);
+        if (nb & 31) t.hdr[nb >> 5] = (uint32_t)acc;
+        t.hdr[95] = nb;
+    }
+    __syncthreads();
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&t);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(T);
+    for (int i = tid; i < (int)(sizeof(DflTables) / 4); i += kHuffThreads) dst[i] = src[i];
+}
+
+// ---- D3 on the host (the default): the same construction in C++ between D2 and D4 (one
+// 1.3 KB histogram read back, one 1 KB table upload).  Measured faster per encode than the
+// single-workgroup device build above, which ctx->png_device_d3 selects.
 // Code lengths (<= maxbits) by the two-queue Huffman construction (leaves sorted by (freq,
 // symbol)), then miniz's tdefl_huffman_enforce_max_code_size: clamp, then drop one max-length
 // code and split the longest shorter code until the Kraft sum is exactly 2^maxbits; the longest
@@ -581,15 +857,6 @@ static void canon_host(const uint8_t* len, int n, uint16_t* code) {
         code[i] = (uint16_t)r;
     }
 }
-
-// The table block D4/D5 read: codes, lengths and the block header bits.
-struct DflTables {
-    uint16_t lcode[286];
-    uint16_t dcode[30];
-    uint8_t llen[286];
-    uint8_t dlen[30];
-    uint32_t hdr[96];        // header bits LSB-first; hdr[95] = bit count
-};
 
 static void build_dynamic_block(const uint32_t* lhist, const uint32_t* dhist, DflTables& T) {
     uint32_t lf[286], df[30];
@@ -734,12 +1001,40 @@ __global__ void __launch_bounds__(256) k_png_lz_write(DflArgs D) {
     if (nacc > 0) atomicOr(&D.words[wpos], (uint32_t)acc);
 }
 
-// Deflate bytes -> IDAT chunk: [len][IDAT][78 01][deflate ...][adler][crc].
-__global__ void __launch_bounds__(256) k_png_zcopy(DflArgs D, int64_t nbytes) {
+// Stored or dynamic: the zlib stream length of each, the shorter wins (noise: stored).
+__global__ void k_png_select(DflArgs D) {
+    const int64_t zdyn = 2 + (int64_t)D.tot[1] + 4;
+    const bool stored = zdyn >= D.P.zlen;
+    const int64_t zlen = stored ? D.P.zlen : zdyn;
+    D.P.meta[0] = zlen;
+    D.P.meta[1] = stored ? 1 : 0;
+    D.P.meta[2] = 8 + zlen + 4;
+}
+
+// Deflate bytes -> IDAT chunk: [len][IDAT][78 01][deflate ...][adler][crc] (dynamic stream only).
+__global__ void __launch_bounds__(256) k_png_zcopy(DflArgs D) {
+    if (D.P.meta[1]) return;
+    const int64_t nbytes = D.tot[1];
     uint8_t* z = D.P.chunk + 8;
     const uint8_t* src = reinterpret_cast<const uint8_t*>(D.words);
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nbytes + 2; i += (int64_t)gridDim.x * 256)
         z[i] = i == 0 ? 0x78 : i == 1 ? 0x01 : src[i - 2];
+}
+
+// The IDAT chunk length, and with `copy` the chunk, land in the context's fine-grained pinned
+// buffer: [len u64][pad 8][chunk].
+constexpr int64_t kPngLandBytes = 256 * 1024;
+__global__ void __launch_bounds__(256) k_png_chunk_to_host(PngArgs A, uint8_t* __restrict__ host, int copy) {
+    const int64_t len = A.meta[2];
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i == 0) *reinterpret_cast<int64_t*>(host) = len;
+    if (!copy || i >= len) return;
+    uint8_t* dst = host + 16;
+    if (i + 16 <= len) {
+        *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(A.chunk + i);
+    } else {
+        for (int64_t j = i; j < len; ++j) dst[j] = A.chunk[j];
+    }
 }
 
 static void put32(std::vector<uint8_t>& v, uint32_t x) {
@@ -772,7 +1067,7 @@ static PngPlan png_plan(int kind, int W, int H) {
 
 // Scratch layout of one PNG encode (ws + off): deflate working buffers after the chunk.
 struct PngLayout {
-    size_t sums, crc, chunk, flt, tokens, ntok, lhist, dhist, tab, segb, tot, words, rows, scan,
+    size_t sums, crc, meta, chunk, flt, tokens, ntok, lhist, dhist, tab, segb, tot, words, rows, scan,
         total;
     int64_t nseg, out_words;
 };
@@ -786,6 +1081,7 @@ static PngLayout png_layout(int kind, int W, int H) {
     auto take = [&](size_t b) { const size_t r = o; o = align_up(o + b, 256); return r; };
     L.sums = take(16);
     L.crc = take(4);
+    L.meta = take(32);
     L.chunk = take((size_t)P.chunk_bytes);
     L.flt = take((size_t)P.raw);
     L.tokens = take((size_t)P.raw * 4);
@@ -857,12 +1153,15 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     D.nseg = L.nseg;
     D.out_words = L.out_words;
     D.bpp = kind == kRgb ? 3 : 1;
+    A.meta = reinterpret_cast<int64_t*>(ws + L.meta);
+    D.P = A;
     OMR_HIP(ctx, hipMemsetAsync(ws + L.sums, 0, 256, ctx->stream));
     OMR_HIP(ctx, hipMemsetAsync(ws + L.crc, 0, 4, ctx->stream));
     OMR_HIP(ctx, hipMemsetAsync(ws + L.lhist, 0, L.dhist + 30 * 4 - L.lhist, ctx->stream));
     const unsigned gseg = (unsigned)((L.nseg + 255) / 256);
     const size_t rows_lds = align_up(2 * (size_t)(P.rowlen - 1), 16);
     if (rows_lds > (size_t)150 * 1024) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG row too wide");
+    if (P.chunk_bytes >= ((int64_t)1 << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG image too large");
     if (rows_lds > (size_t)60 * 1024)
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_png_filter),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds + 1024));
@@ -870,15 +1169,21 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     const int32_t back = (int32_t)align_up((size_t)std::min<int64_t>(std::max<int64_t>(P.rowlen, 2 * D.bpp), kMaxBack), 16);
     hipLaunchKernelGGL(k_png_lz_parse, dim3((unsigned)((L.nseg + kParseLanes - 1) / kParseLanes)), dim3(kParseLanes),
                        (size_t)back + (size_t)kParseLanes * kSeg, ctx->stream, D, back);
-    OMR_HIP(ctx, hipGetLastError());
-    // D3: the two histograms to the host, the code back (pinned ring, async-safe)
-    uint32_t hist[286 + 30];
-    OMR_HIP(ctx, hipMemcpyAsync(hist, ws + L.lhist, sizeof(hist), hipMemcpyDeviceToHost, ctx->stream));
-    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    DflTables T;
-    build_dynamic_block(hist, hist + 286, T);
-    omr_status sst = stage_h2d(ctx, ws + L.tab, &T, sizeof(T));
-    if (sst) return sst;
+    if (ctx->png_device_d3) {
+        // D3 on the device: the code from the two histograms, no host round trip
+        hipLaunchKernelGGL(k_png_tables, dim3(1), dim3(kHuffThreads), 0, ctx->stream, D.lhist,
+                           reinterpret_cast<DflTables*>(ws + L.tab));
+        OMR_HIP(ctx, hipGetLastError());
+    } else {
+        // D3 on the host: the two histograms to the host, the code back (pinned ring)
+        uint32_t hist[286 + 30];
+        OMR_HIP(ctx, hipMemcpyAsync(hist, ws + L.lhist, sizeof(hist), hipMemcpyDeviceToHost, ctx->stream));
+        OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        DflTables T;
+        build_dynamic_block(hist, hist + 286, T);
+        omr_status sst = stage_h2d(ctx, ws + L.tab, &T, sizeof(T));
+        if (sst) return sst;
+    }
     hipLaunchKernelGGL(k_png_lz_bits, dim3(gseg), dim3(256), 0, ctx->stream, D);
     OMR_HIP(ctx, hipGetLastError());
     omr_status st = device_exclusive_scan(ctx, D.seg_bits, D.seg_bits, L.nseg, D.tot,
@@ -887,36 +1192,39 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     hipLaunchKernelGGL(k_png_zero_words, dim3((unsigned)std::min<int64_t>((L.out_words + 255) / 256, 4096)), dim3(256),
                        0, ctx->stream, D);
     hipLaunchKernelGGL(k_png_lz_write, dim3(gseg), dim3(256), 0, ctx->stream, D);
-    OMR_HIP(ctx, hipGetLastError());
-    uint32_t tot[2] = {0, 0};
-    OMR_HIP(ctx, hipMemcpyAsync(tot, D.tot, 8, hipMemcpyDeviceToHost, ctx->stream));
-    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    const int64_t zdeflate = 2 + (int64_t)tot[1] + 4;
-    const bool stored = zdeflate >= P.zlen;          // incompressible: stored blocks are shorter
-    A.zlen = stored ? P.zlen : zdeflate;
-    D.P = A;
-    const int64_t chunk_bytes = 8 + A.zlen + 4;
-    const size_t total = pre.size() + (size_t)chunk_bytes + sizeof(iend);
-    if (out_len) *out_len = total;
-    if (!out || cap < total) return fail(ctx, OMR_BUFFER_TOO_SMALL, "PNG output buffer too small");
-    if (stored) {
-        OMR_HIP(ctx, hipMemsetAsync(ws + L.sums, 0, 16, ctx->stream));
-        const int64_t need = (P.zlen + 255) / 256;
-        const unsigned g = (unsigned)std::min<int64_t>(need, (int64_t)ctx->cu_count * 8);
-        hipLaunchKernelGGL(k_png_layout, dim3(g), dim3(256), 0, ctx->stream, A);
-    } else {
-        const unsigned g = (unsigned)std::min<int64_t>((tot[1] + 2 + 255) / 256, (int64_t)ctx->cu_count * 8);
-        hipLaunchKernelGGL(k_png_zcopy, dim3(std::max(g, 1u)), dim3(256), 0, ctx->stream, D, (int64_t)tot[1]);
-        hipLaunchKernelGGL(k_png_adler_rows, dim3(1), dim3(256), 0, ctx->stream, D);
-    }
+    // stored vs dynamic decided on the device; both paths are queued, the unchosen one exits
+    hipLaunchKernelGGL(k_png_select, dim3(1), dim3(1), 0, ctx->stream, D);
+    const unsigned gl = (unsigned)std::min<int64_t>((P.zlen + 255) / 256, (int64_t)ctx->cu_count * 8);
+    hipLaunchKernelGGL(k_png_layout, dim3(gl), dim3(256), 0, ctx->stream, A);
+    hipLaunchKernelGGL(k_png_zcopy, dim3(gl), dim3(256), 0, ctx->stream, D);
+    hipLaunchKernelGGL(k_png_adler_rows, dim3(1), dim3(256), 0, ctx->stream, D);
     hipLaunchKernelGGL(k_png_adler, dim3(1), dim3(1), 0, ctx->stream, A);
-    const int64_t segs = (4 + A.zlen + kCrcSeg - 1) / kCrcSeg;
+    const int64_t segs = (4 + P.zlen + kCrcSeg - 1) / kCrcSeg;   // stored length: the longest
     hipLaunchKernelGGL(k_png_crc, dim3((unsigned)((segs + 255) / 256)), dim3(256), 0, ctx->stream, A);
     hipLaunchKernelGGL(k_png_finish, dim3(1), dim3(1), 0, ctx->stream, A);
     OMR_HIP(ctx, hipGetLastError());
-    std::memcpy(out, pre.data(), pre.size());
-    OMR_HIP(ctx, hipMemcpyAsync(out + pre.size(), A.chunk, (size_t)chunk_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    // Small chunks (masks) land with their length in pinned host memory: one stream sync.  Big
+    // ones (rendered RGB tiles): the length lands first, then one DMA copy of exactly the chunk
+    // (a kernel writing MBs over PCIe into host memory plus a host memcpy was slower).
+    const bool land = P.chunk_bytes <= kPngLandBytes;
+    st = ensure_host_out(ctx, land ? (size_t)P.chunk_bytes + 16 : 16);
+    if (st) return st;
+    const int64_t land_bytes = land ? P.chunk_bytes : 0;
+    hipLaunchKernelGGL(k_png_chunk_to_host, dim3((unsigned)((land_bytes + 16 * 256 - 1) / (16 * 256) + 1)), dim3(256),
+                       0, ctx->stream, A, ctx->h_out, land ? 1 : 0);
+    OMR_HIP(ctx, hipGetLastError());
     OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t chunk_bytes = *reinterpret_cast<volatile int64_t*>(ctx->h_out);
+    const size_t total = pre.size() + (size_t)chunk_bytes + sizeof(iend);
+    if (out_len) *out_len = total;
+    if (!out || cap < total) return fail(ctx, OMR_BUFFER_TOO_SMALL, "PNG output buffer too small");
+    std::memcpy(out, pre.data(), pre.size());
+    if (land) {
+        std::memcpy(out + pre.size(), ctx->h_out + 16, (size_t)chunk_bytes);
+    } else {
+        OMR_HIP(ctx, hipMemcpyAsync(out + pre.size(), A.chunk, (size_t)chunk_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     std::memcpy(out + pre.size() + chunk_bytes, iend, sizeof(iend));
     return OMR_OK;
 }

@@ -238,3 +238,26 @@ def test_png_wide_rows(ctx):
     png = ctx.encode_png(argb, w, h)
     exp = np.stack([(argb >> 16) & 0xFF, (argb >> 8) & 0xFF, argb & 0xFF], -1).astype(np.uint8)
     np.testing.assert_array_equal(np.asarray(decode(png)), exp)
+
+
+def test_png_device_huffman_tables_match_host(monkeypatch):
+    """D3 on the device (OMR_PNG_DEVICE_D3=1: one workgroup builds the length-limited codes and
+    the run-length header) restates the host construction: every file byte-identical to the
+    host-D3 encode, for images and masks, including noise (stored blocks) and a skewed
+    (geometric) pixel distribution."""
+    import omr
+    rng = np.random.default_rng(77)
+    imgs = dict(_png_images())
+    imgs["noise_96"] = rng.integers(0, 2**32, (96, 96), dtype=np.uint32) | 0xFF000000
+    v = np.concatenate([np.full(2 ** k, k, np.uint32) for k in range(18)])      # geometric counts
+    imgs["skewed"] = (rng.permutation(v)[:128 * 1024].reshape(256, 512) * 0x010101) | 0xFF000000
+    masks = [(w, h, np.packbits(rng.integers(0, 2, w * h)).tobytes()) for w, h in [(64, 48), (333, 77)]]
+    with omr.Context(0) as host:
+        want = {k: host.encode_png(a, a.shape[1], a.shape[0]) for k, a in imgs.items()}
+        mwant = [host.render_shape_mask_png(b, w, h, (9, 8, 7, 6)) for w, h, b in masks]
+    monkeypatch.setenv("OMR_PNG_DEVICE_D3", "1")
+    with omr.Context(0) as dev:
+        for k, a in imgs.items():
+            assert dev.encode_png(a, a.shape[1], a.shape[0]) == want[k], k
+        for (w, h, b), exp in zip(masks, mwant):
+            assert dev.render_shape_mask_png(b, w, h, (9, 8, 7, 6)) == exp
