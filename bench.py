@@ -200,7 +200,7 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
     lens = torch.empty(B, dtype=torch.int32, device=dev)
     stat = torch.empty(B, dtype=torch.int32, device=dev)
     import omr
-    ctx2 = omr.Context(ctx.device)
+    ctx2 = omr.Context(ctx.device, torch_order=False)
     for name, (qd, chans, src, pt, tstride, cstride, be) in cases.items():
         binds = make_bindings(chans)
 
@@ -395,7 +395,7 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
     out = torch.empty((S, S), dtype=torch.int32, device=dev)
     binds = make_bindings(chans)   # marshalled once, as a Java caller would hold its Renderer state
     import omr
-    ctx2 = omr.Context(ctx.device)
+    ctx2 = omr.Context(ctx.device, torch_order=False)
     res = {}
     for name, alg, end in (("max", _lib.PROJECTION_MAX, Z - 1), ("mean", _lib.PROJECTION_MEAN, Z - 1)):
         def step():
@@ -815,7 +815,7 @@ def main():
     from omr.context import make_bindings, make_qdef
     from omr.synthetic import c2_channels
 
-    ctx = omr.Context(dev_index)
+    ctx = omr.Context(dev_index, torch_order=False)
     qdef = make_qdef("rgb")
     chans = c2_channels(CHANNELS)
     bindings = make_bindings(chans)

@@ -4,6 +4,7 @@ Host arrays are numpy; device buffers are torch tensors on the context's GPU (to
 only used as the device-memory allocator — all compute runs in libomr.so kernels).
 """
 import ctypes
+import functools
 
 import numpy as np
 
@@ -62,18 +63,26 @@ def make_qdef(model, cd_start=0, cd_end=255, bit_resolution=255):
 
 
 class Context:
-    """One omr_ctx.  Its launches run on the context's own non-blocking HIP stream, which does
-    not order with torch's streams: call order_after_torch() before a call that reads tensors
-    torch has just written (or a caller-side synchronize), and keep tensors alive (or
-    record_stream them) until synchronize() when torch might reuse their memory."""
+    """One omr_ctx.  Its launches run on the context's own non-blocking HIP stream.
 
-    def __init__(self, device=0):
+    torch_order (default True): every *_device call is stream-ordered with torch's current
+    stream at the API boundary, without a host sync: the context stream first waits for the
+    work torch has queued (the inputs), and torch's stream then waits for the call's kernels
+    (the outputs), so a following tensor op (.cpu(), a kernel, a free) sees the result.  Keep
+    tensors alive until the call's work is done when torch might reuse their memory (the
+    caching allocator reuses on torch's stream, which the second wait orders).  With
+    torch_order=False (the bench: explicit synchronize around timed regions) nothing is added
+    to a call; order_after_torch() / order_torch_after() do the same by hand."""
+
+    def __init__(self, device=0, torch_order=True):
         h = ctypes.c_void_p()
         st = lib.omr_ctx_create(int(device), ctypes.byref(h))
         if st != _lib.OK:
             raise _lib.OmrError(st, f"omr_ctx_create(device={device}) failed")
         self.h = h
         self.device = device
+        self.torch_order = bool(torch_order)
+        self._ext = None
 
     def close(self):
         if self.h:
@@ -102,13 +111,25 @@ class Context:
     def synchronize(self):
         check(lib.omr_ctx_synchronize(self.h), self.h)
 
+    def _ext_stream(self):
+        import torch
+        if self._ext is None or self._ext[0] != self.stream:
+            self._ext = (self.stream, torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device)))
+        return self._ext[1]
+
     def order_after_torch(self):
         """The context's stream waits for the work queued so far on torch's current stream."""
         import torch
-        dev = torch.device("cuda", self.device)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        torch.cuda.ExternalStream(self.stream, device=dev).wait_event(ev)
+        ev.record(torch.cuda.current_stream(torch.device("cuda", self.device)))
+        self._ext_stream().wait_event(ev)
+
+    def order_torch_after(self):
+        """torch's current stream waits for the work queued so far on the context's stream."""
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(self._ext_stream())
+        torch.cuda.current_stream(torch.device("cuda", self.device)).wait_event(ev)
 
     def set_semantics(self, flags):
         """OMR_SEM_* switches (omr._lib.SEM_*) for later calls on this context."""
@@ -320,3 +341,21 @@ class Context:
                                             int(flip_v), out.ctypes.data, cap, ctypes.byref(n)),
               self.h)
         return out[:n.value].tobytes()
+
+
+def _torch_ordered(fn):
+    """Wrap a *_device method: inputs after torch's queued work, torch after the outputs."""
+    @functools.wraps(fn)
+    def call(self, *a, **k):
+        if self.torch_order:
+            self.order_after_torch()
+        try:
+            return fn(self, *a, **k)
+        finally:
+            if self.torch_order and self.h:
+                self.order_torch_after()
+    return call
+
+
+for _name in [n for n in vars(Context) if n.endswith("_device") or n == "encode_jpeg_batch"]:
+    setattr(Context, _name, _torch_ordered(getattr(Context, _name)))
