@@ -248,8 +248,6 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
         fb = d_out.cpu().numpy()
         assert all(fb[fo[i]:fo[i] + fl[i]].tobytes() == ref_files[ref_offs[i]:ref_offs[i] + ln[i]].tobytes()
                    for i in range(B)), "fused render->JPEG differs from render + JPEG"
-        # B1 / F1 are VALU-bound: instructions per MCU from the SQ counters (profiles/r02), the
-        # rate 1 wave-instruction per 4 cycles per SIMD (wave64 on SIMD16)
         mcus = B * (TILE // 16) ** 2
         px = TILE * TILE
         nblk = (TILE // 16) ** 2 * 6
@@ -274,6 +272,9 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
             "J1_ns_per_mcu": round(avg.get(5, float("nan")) * 1e6 / mcus, 4),
             "F1_ns_per_mcu": round(avg_f.get(5, float("nan")) * 1e6 / mcus, 4),
         }
+        vr = jpeg_valu_roofline(name, mcus, avg.get(5), avg_f.get(5), avg.get(6))
+        if vr:
+            res[name]["valu_roofline"] = vr
         if with_cpu:
             try:
                 res[name]["cpu_baseline"] = jpeg_cpu_baseline(torch, name, src, chans, pt, be, q,
@@ -282,6 +283,35 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
                 log(f"jpeg cpu baseline failed: {e}")
     ctx2.close()
     return res
+
+
+VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02", "jpeg_valu_pmc.json")
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2   # 1,024 SIMD-32s, a wave64 VALU op per 2 cycles
+
+
+def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
+    """B1 / F1 / B3 are VALU-issue-bound: achieved = VALU wave-instructions per
+    launch (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r02.sh) x MCUs
+    / the kernel's measured average duration; peak = every SIMD issuing one wave64 VALU
+    instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, v_fma_f32 wave64 throughput)."""
+    case = "c1" if name.startswith("c1") else "c2"
+    try:
+        with open(VALU_PMC) as fh:
+            pmc = json.load(fh).get(case, {})
+    except (OSError, ValueError):
+        return None
+    out = {"bound": "valu", "unit": "wave-instr/s", "peak": VALU_PEAK_WAVE_INSTR_PER_S,
+           "source": os.path.relpath(VALU_PMC, os.path.dirname(os.path.abspath(__file__))) + f" [{case}]"}
+    for label, key, ms in (("B1_fdct", "k_jpeg_fdct_batch", j1_ms), ("F1_render_fdct", "k_jpeg_render_fdct", f1_ms),
+                           ("B3_huffman", "k_jpeg_huff_thread", j3_ms)):
+        k = next((k for k in pmc if key in k), None)
+        if k is None or not ms:
+            continue
+        ipm = pmc[k]["SQ_INSTS_VALU_per_mcu"]
+        ach = ipm * mcus / (ms * 1e-3)
+        out[label] = {"valu_instr_per_mcu": round(ipm, 1), "achieved": round(ach, 1),
+                      "frac": round(ach / VALU_PEAK_WAVE_INSTR_PER_S, 4), "avg_launch_ms": round(ms, 5)}
+    return out
 
 
 def jpeg_cpu_baseline(torch, name, src, chans, pt, be, q, seconds, threads):
