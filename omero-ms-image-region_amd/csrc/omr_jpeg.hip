@@ -835,9 +835,9 @@ struct PlaneSource {
         }
     }
     // 16-bit LUT-domain check (QuantizationException): per channel, the packed 2 x 16-bit
-    // minimum and maximum of the lane's pixels (sign-biased for signed types, so one unsigned
-    // v_pk_min/max_u16 covers two pixels) are kept and compared with [gmin, gmax] once in
-    // finish(), instead of two compares and a select per pixel.
+    // minimum and maximum of the lane's (biased) pixels (one v_pk_min/max_u16 covers two pixels)
+    // are kept and compared with [gmin, gmax] once in finish(), instead of two compares and a
+    // select per pixel.
     uint32_t mn[NA], mx[NA];
     // contribution-table entry of pixel j (0: lower address, 1: upper) of raw word w, channel a
     // (16-bit types: w already in native byte order)
@@ -848,8 +848,7 @@ struct PlaneSource {
             err |= (e & kErrBit) != 0;
             return e & ~kErrBit;
         } else {
-            const uint32_t h = j ? (w >> 16) : (w & 0xFFFF);
-            const int x = F.R.is_signed ? (int)(int16_t)h : (int)h;
+            const int x = (int)(j ? (w >> 16) : (w & 0xFFFF));   // int16: biased to unsigned (take())
             const K2Chan& p = F.R.ch[a];
             uint32_t v;
             if constexpr (MODE == kFusedFast16) {
@@ -871,11 +870,14 @@ struct PlaneSource {
             uint32_t w0 = raw[a][0], w1 = raw[a][1];
             if constexpr (BPP == 2) {
                 if constexpr (BE) { w0 = bswap16x2(w0); w1 = bswap16x2(w1); }
+                // int16 pixels biased to unsigned (x + 32768, one XOR per pixel pair); the host
+                // moved the channel's window, LUT domain and thresholds by the same amount
+                const uint32_t sg = F.R.is_signed ? 0x80008000u : 0u;
+                w0 ^= sg;
+                w1 ^= sg;
                 if (F.R.any_check) {              // wave-uniform
-                    const uint32_t sg = F.R.is_signed ? 0x80008000u : 0u;
-                    const uint32_t b0 = w0 ^ sg, b1 = w1 ^ sg;
-                    mn[a] = pk_min_u16(mn[a], pk_min_u16(b0, b1));
-                    mx[a] = pk_max_u16(mx[a], pk_max_u16(b0, b1));
+                    mn[a] = pk_min_u16(mn[a], pk_min_u16(w0, w1));
+                    mx[a] = pk_max_u16(mx[a], pk_max_u16(w0, w1));
                 }
             }
             acc[0] += entry(a, w0, jl);
@@ -896,15 +898,12 @@ struct PlaneSource {
     __device__ __forceinline__ void finish() {
         if constexpr (BPP == 2) {
             if (!F.R.any_check) return;
-            const uint32_t sg = F.R.is_signed ? 0x8000u : 0u;
 #pragma unroll
             for (int a = 0; a < NA; ++a) {
                 const K2Chan& p = F.R.ch[a];
                 if (!p.check) continue;
-                const uint32_t lo = min(mn[a] & 0xFFFFu, mn[a] >> 16) ^ sg;
-                const uint32_t hi = max(mx[a] & 0xFFFFu, mx[a] >> 16) ^ sg;
-                const int xl = F.R.is_signed ? (int)(int16_t)lo : (int)lo;
-                const int xh = F.R.is_signed ? (int)(int16_t)hi : (int)hi;
+                const int xl = (int)min(mn[a] & 0xFFFFu, mn[a] >> 16);    // biased, as gmin / gmax
+                const int xh = (int)max(mx[a] & 0xFFFFu, mx[a] >> 16);
                 err |= (xl < p.gmin) | (xh > p.gmax);
             }
         }
@@ -1753,7 +1752,7 @@ static omr_status render_jpeg_batch(Ctx* ctx, const omr_quantum_def* qdef, const
         if (st) return st;
         FusedLaunch fl;
         std::memset(&fl, 0, sizeof(fl));
-        st = render_fused_stage(ctx, fp.get(), 0, fl.args.R);
+        st = render_fused_stage(ctx, fp.get(), 0, fl.args.R, /*build_contrib=*/true, /*bias_int16=*/true);
         if (st) return st;
         fl.args.sbase = static_cast<const uint8_t*>(d_base);
         fl.args.planes = d_ptrs;

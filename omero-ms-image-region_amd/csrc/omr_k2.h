@@ -112,6 +112,9 @@ size_t render_fused_ws_bytes(const FusedPlanBuf* fp);
 // Stage the plan at ctx->ws + ws_off (the workspace must hold render_fused_ws_bytes from there),
 // build the tables on the context stream and fill `out`.
 // build_contrib false: the fused kernel builds the tables from `plan` (contrib_entry) itself.
-omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& out, bool build_contrib = true);
+// bias_int16: int16 pixel-domain parameters (ws, lo, hi, gmin, gmax) + 32768, for a kernel that
+// reads int16 pixels biased to unsigned (the fused JPEG kernel; plans from render_fused_plan).
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& out, bool build_contrib = true,
+                              bool bias_int16 = false);
 
 }  // namespace omr

@@ -994,10 +994,17 @@ bool render_fused_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_bin
                        int32_t pixel_type, FusedPlanBuf* fp, omr_status* st) {
     *st = prepare_plan(ctx, q, ch, size_c, pixel_type, fp->pp);
     if (*st) return false;
+    // int16: the fused JPEG kernel reads pixels biased to unsigned (x + 32768) and takes
+    // ws + 32768, which must be exact so that (x + 32768) - (ws + 32768) rounds like x - ws
+    for (int i = 0; i < fp->pp.plan.n_active; ++i) {
+        const double ws = fp->pp.plan.ch[i].ws;
+        if (pixel_type == OMR_PIXELS_INT16 && (ws + 32768.0) - 32768.0 != ws) return false;
+    }
     return fused_from_prepared(fp, pixel_type);
 }
 
-omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& F, bool build_contrib) {
+omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRender& F, bool build_contrib,
+                              bool bias_int16) {
     PreparedPlan& pp = fp->pp;
     const RenderLayout& L = fp->L;
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws) + ws_off;
@@ -1020,19 +1027,23 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
     std::memset(&F, 0, sizeof(F));
     double tlo, thi;
     type_bounds(fp->pixel_type, tlo, thi);
+    // int16 with bias_int16 (the fused JPEG kernel): pixels are read biased to unsigned, so every
+    // pixel-domain parameter moves by 32768 with them (x - ws, x - gmin and the compares are
+    // unchanged; render_fused_plan checked that ws + 32768 is exact)
+    const int bias = bias_int16 && fp->pixel_type == OMR_PIXELS_INT16 ? 32768 : 0;
     for (int i = 0; i < na; ++i) {
         const ChanParam& c = pp.plan.ch[i];
         K2Chan& k = F.ch[i];
         k.index = c.index;
         k.mode = c.mode;
-        k.lo = c.lo;
-        k.hi = c.hi;
-        k.gmin = c.gmin;
-        k.gmax = c.gmax;
+        k.lo = c.lo + bias;
+        k.hi = c.hi + bias;
+        k.gmin = c.gmin + bias;
+        k.gmax = c.gmax + bias;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
         F.any_check |= k.check;
         k.second = c.second;
-        k.ws = c.ws;
+        k.ws = c.ws + (double)bias;
         k.a0 = c.a0;
         k.a1 = c.a1;
         k.lut_off = c.lut_off;

@@ -169,3 +169,20 @@ def test_quantization_error_signed_lower_and_upper_bounds(ctx):
     assert st.tolist() == [0, _lib.QUANTIZATION, 0, _lib.QUANTIZATION]
     exp = _expect(chans, [tiles[0], tiles[2]], _lib.PIXELS_INT16, w, h)
     assert files[0] == exp[0] and files[2] == exp[1]
+
+
+def test_int16_window_start_inexact_after_bias_falls_back(ctx):
+    """The fused kernel reads int16 pixels biased by 32768 and moves the window start with them;
+    a window start for which ws + 32768 is not exact (1e-30) takes the K2 + B1 path instead.
+    Both must give the oracle's files (a fused int16 case alongside for contrast)."""
+    w, h = 64, 48
+    rng = np.random.default_rng(19)
+    tiles = [[rng.integers(-2000, 2000, (h, w)).astype(np.int16) for _ in range(2)] for _ in range(2)]
+    for ws in (1e-30, -1000.25):
+        chans = [{"input_start": f32(ws), "input_end": f32(1500.0), "global_min": -32768.0, "global_max": 32767.0,
+                  "rgba": (255, 128, 0, 255)},
+                 {"input_start": f32(-1500.0), "input_end": f32(20.0), "global_min": -32768.0,
+                  "global_max": 32767.0, "rgba": (0, 64, 255, 255), "reverse": True}]
+        files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h)
+        assert st.tolist() == [0, 0]
+        assert files == _expect(chans, tiles, _lib.PIXELS_INT16, w, h), ws
