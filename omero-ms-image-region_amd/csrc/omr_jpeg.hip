@@ -135,6 +135,19 @@ __device__ __forceinline__ void ycc(uint32_t p, int& y, int& cb, int& cr) {
     cr = (32768 * r - 27439 * g - 5329 * b + (128 << 16) + 32767) >> 16;
 }
 
+// The same on separate components (B1/F1 pixel sources hand over r, g, b).
+struct Rgb {
+    int r, g, b;
+};
+__device__ __forceinline__ void ycc(const Rgb& p, int& y, int& cb, int& cr) {
+    y = (19595 * p.r + 38470 * p.g + 7471 * p.b + 32768) >> 16;
+    cb = (-11059 * p.r - 21709 * p.g + 32768 * p.b + (128 << 16) + 32767) >> 16;
+    cr = (32768 * p.r - 27439 * p.g - 5329 * p.b + (128 << 16) + 32767) >> 16;
+}
+__device__ __forceinline__ Rgb rgb_of(uint32_t p) {
+    return Rgb{(int)((p >> 16) & 0xFF), (int)((p >> 8) & 0xFF), (int)(p & 0xFF)};
+}
+
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 #define M24(a, c) __mul24((a), (c))
 
@@ -779,8 +792,9 @@ struct ArgbSource {
             nclamp = false;
         }
     }
-    __device__ __forceinline__ void take(uint32_t& p00, uint32_t& p01, uint32_t& p10, uint32_t& p11) {
-        p00 = nclamp ? na.y : na.x; p01 = na.y; p10 = nclamp ? nb.y : nb.x; p11 = nb.y;
+    __device__ __forceinline__ void take(Rgb (&px)[4]) {
+        px[0] = rgb_of(nclamp ? na.y : na.x); px[1] = rgb_of(na.y);
+        px[2] = rgb_of(nclamp ? nb.y : nb.x); px[3] = rgb_of(nb.y);
     }
     __device__ __forceinline__ uint32_t at(int x, int y) const { return img[(int64_t)y * W + x]; }
 };
@@ -862,7 +876,7 @@ struct PlaneSource {
             return tab[v];
         }
     }
-    __device__ __forceinline__ void take(uint32_t& p00, uint32_t& p01, uint32_t& p10, uint32_t& p11) {
+    __device__ __forceinline__ void take(Rgb (&px)[4]) {
         uint32_t acc[4] = {0, 0, 0, 0};
         const int jl = F.flip_h ? 1 : 0;        // which half of the pair is the left output pixel
 #pragma unroll
@@ -885,13 +899,10 @@ struct PlaneSource {
             acc[2] += entry(a, w1, jl);
             acc[3] += entry(a, w1, jl ^ 1);
         }
-        uint32_t px[4];
+        // components straight from the 10-bit sums (no ARGB pack for ycc() to unpack)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t c = clamp_fields(acc[j]);
-            px[j] = 0xFF000000u | ((c >> 4) & 0xFF0000u) | ((c >> 2) & 0xFF00u) | (c & 0xFFu);
-        }
-        p00 = px[0]; p01 = px[1]; p10 = px[2]; p11 = px[3];
+        for (int j = 0; j < 4; ++j)
+            px[j] = Rgb{(int)min(acc[j] >> 20, 255u), (int)min((acc[j] >> 10) & 1023u, 255u), (int)min(acc[j] & 1023u, 255u)};
     }
     __device__ __forceinline__ uint32_t at(int, int) const { return 0; }   // never: H % 16 == 0
     // after the last MCU: fold the 16-bit domain extremes into err
@@ -943,32 +954,31 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         bool grey;
         {
             const int x0 = mx * 16 + 2 * cx;
-            uint32_t p00, p01, p10, p11;
-            src.take(p00, p01, p10, p11);
+            Rgb px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
+            src.take(px);
             if (m + 1 < m1) fetch(m + 1);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
-            auto isg = [](uint32_t p) { return (p & 0xFFFFu) == ((p >> 8) & 0xFFFFu); };
-            grey = __ballot(!(isg(p00) && isg(p01) && isg(p10) && isg(p11)) || cyg >= chv) == 0;
+            auto isg = [](const Rgb& p) { return p.r == p.g && p.g == p.b; };
+            grey = __ballot(!(isg(px[0]) && isg(px[1]) && isg(px[2]) && isg(px[3])) || cyg >= chv) == 0;
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
             const int o = ((2 * cy) & 7) * 8 + ((2 * cx) & 7);
             if (grey) {
-                S[blk * kBS + o] = (int)(p00 & 0xFFu) - 128;
-                S[blk * kBS + o + 1] = (int)(p01 & 0xFFu) - 128;
-                S[blk * kBS + o + 8] = (int)(p10 & 0xFFu) - 128;
-                S[blk * kBS + o + 9] = (int)(p11 & 0xFFu) - 128;
+                S[blk * kBS + o] = px[0].b - 128;
+                S[blk * kBS + o + 1] = px[1].b - 128;
+                S[blk * kBS + o + 8] = px[2].b - 128;
+                S[blk * kBS + o + 9] = px[3].b - 128;
             } else {
-            ycc(p00, y, cb0, cr0); S[blk * kBS + o] = y - 128;
-            ycc(p01, y, cb1, cr1); S[blk * kBS + o + 1] = y - 128;
-            ycc(p10, y, cb2, cr2); S[blk * kBS + o + 8] = y - 128;
-            ycc(p11, y, cb3, cr3); S[blk * kBS + o + 9] = y - 128;
+            ycc(px[0], y, cb0, cr0); S[blk * kBS + o] = y - 128;
+            ycc(px[1], y, cb1, cr1); S[blk * kBS + o + 1] = y - 128;
+            ycc(px[2], y, cb2, cr2); S[blk * kBS + o + 8] = y - 128;
+            ycc(px[3], y, cb3, cr3); S[blk * kBS + o + 9] = y - 128;
             if (cyg >= chv) {
                 const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
                 const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
-                p00 = src.at(xa, r0); p01 = src.at(xb, r0);
-                p10 = src.at(xa, r1); p11 = src.at(xb, r1);
-                ycc(p00, y, cb0, cr0); ycc(p01, y, cb1, cr1); ycc(p10, y, cb2, cr2); ycc(p11, y, cb3, cr3);
+                ycc(src.at(xa, r0), y, cb0, cr0); ycc(src.at(xb, r0), y, cb1, cr1);
+                ycc(src.at(xa, r1), y, cb2, cr2); ycc(src.at(xb, r1), y, cb3, cr3);
             }
             const int bias = (cx & 1) ? 2 : 1;
             S[4 * kBS + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
