@@ -877,8 +877,7 @@ struct PlaneSource {
         }
     }
     __device__ __forceinline__ void take(Rgb (&px)[4]) {
-        uint32_t acc[4] = {0, 0, 0, 0};
-        const int jl = F.flip_h ? 1 : 0;        // which half of the pair is the left output pixel
+        uint32_t acc[4] = {0, 0, 0, 0};         // source order: (lo, hi) of row 0, then row 1
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             uint32_t w0 = raw[a][0], w1 = raw[a][1];
@@ -894,10 +893,14 @@ struct PlaneSource {
                     mx[a] = pk_max_u16(mx[a], pk_max_u16(w0, w1));
                 }
             }
-            acc[0] += entry(a, w0, jl);
-            acc[1] += entry(a, w0, jl ^ 1);
-            acc[2] += entry(a, w1, jl);
-            acc[3] += entry(a, w1, jl ^ 1);
+            acc[0] += entry(a, w0, 0);
+            acc[1] += entry(a, w0, 1);
+            acc[2] += entry(a, w1, 0);
+            acc[3] += entry(a, w1, 1);
+        }
+        if (F.flip_h) {                         // the upper half of each pair is the left output pixel
+            const uint32_t t0 = acc[0], t2 = acc[2];
+            acc[0] = acc[1]; acc[1] = t0; acc[2] = acc[3]; acc[3] = t2;
         }
         // components straight from the 10-bit sums (no ARGB pack for ycc() to unpack)
 #pragma unroll
