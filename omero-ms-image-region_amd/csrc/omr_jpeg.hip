@@ -867,6 +867,8 @@ struct PlaneSource {
             uint32_t v;
             if constexpr (MODE == kFusedFast16) {
                 v = fast16(x, p);
+            } else if constexpr (MODE == kFusedFast16I) {
+                v = fast16i(x, p);
             } else if (MODE == kFusedLinear16 || p.mode == kModeLinear16) {   // uniform
                 v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
             } else {
@@ -1567,7 +1569,10 @@ static void launch_render_fdct_na(dim3 g, hipStream_t st, const B1Args& a1, cons
 template <bool BE>
 static void launch_render_fdct_mode(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f) {
     switch (f.R.mode) {
-    case kFusedFast16: launch_render_fdct_na<2, BE, kFusedFast16>(g, st, a1, f); break;
+    case kFusedFast16:
+        if (f.R.ws_int) launch_render_fdct_na<2, BE, kFusedFast16I>(g, st, a1, f);
+        else launch_render_fdct_na<2, BE, kFusedFast16>(g, st, a1, f);
+        break;
     case kFusedLinear16: launch_render_fdct_na<2, BE, kFusedLinear16>(g, st, a1, f); break;
     default: launch_render_fdct_na<2, BE, kFusedMixed16>(g, st, a1, f); break;
     }

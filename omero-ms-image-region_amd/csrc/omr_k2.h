@@ -33,8 +33,8 @@ __device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, in
     int v = __double2int_rz(floor(d + 0.5));          // exact in the window (d in [0, bitRes])
     v = (d == 0x1.fffffffffffffp-2) ? 0 : v;
     if (p.second) v = (int)java_round_d(p.a1 * (double)v + (double)cds);   // uniform branch
-    v = x < p.lo ? cds8 : v;
     v = x >= p.hi ? cde8 : v;
+    v = x < p.lo ? cds8 : v;                          // checked first upstream: wins for ws > we
     return (uint32_t)v & 0xFFu;
 }
 
@@ -46,6 +46,14 @@ __device__ __forceinline__ uint32_t linear16(int x, const K2Chan& p, int cds, in
 // d + 0.5 >= 2^31 still clamps to 255).
 __device__ __forceinline__ uint32_t fast16(int x, const K2Chan& p) {
     const double d = p.a0 * ((double)x - p.ws);
+    const int v = __double2int_rz(d + 0.5);
+    return (uint32_t)min(max(v, 0), 255);
+}
+
+// fast16 for an integral window start: (double)(x - ws) is the same double as (double)x - ws
+// (both exact), with the subtraction in int32 instead of f64 (one f64 operation fewer).
+__device__ __forceinline__ uint32_t fast16i(int x, const K2Chan& p) {
+    const double d = p.a0 * (double)(x - (int)p.ws);
     const int v = __double2int_rz(d + 0.5);
     return (uint32_t)min(max(v, 0), 255);
 }
@@ -88,7 +96,8 @@ __device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__
 // the contribution tables (K1) and byte LUTs built on the context stream; the fused kernel
 // quantizes + composites each pixel as K2 does (same helpers, same tables) and encodes it.
 constexpr int kFusedMaxActive = 4;
-enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4 };
+enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4,
+                           kFusedFast16I = 5 /* launch-only: Fast16 with integral window starts */ };
 struct FusedRender {
     K2Chan ch[kFusedMaxActive];
     const uint32_t* contrib;     // [n_active][256] (workspace; built by K1 unless the kernel builds it)
@@ -97,7 +106,7 @@ struct FusedRender {
     int32_t* flag;               // sticky quantization-error word
     int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
     int32_t any_check;           // some channel's LUT domain is narrower than its pixel type
-    int32_t pad;
+    int32_t ws_int;              // every window start is an integer (|ws| < 2^30): x - ws in int32
 };
 
 // Host side (omr_render.hip).  render_fused_plan: true when the fused kernel covers these

@@ -1042,6 +1042,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.gmax = c.gmax + bias;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
         F.any_check |= k.check;
+        F.ws_int = (i == 0 ? 1 : F.ws_int) & ((c.ws == std::floor(c.ws) && std::fabs(c.ws) < 1073741824.0) ? 1 : 0);
         k.second = c.second;
         k.ws = c.ws + (double)bias;
         k.a0 = c.a0;

@@ -495,3 +495,30 @@ def test_small_and_full_launch_boundary(ctx, pt, na, n):
         st, exp = O.render(chans, [np.ascontiguousarray(host[t, c]) for c in range(na)], pt, w, h, flip_h=True)
         assert st == 0
         np.testing.assert_array_equal(got[t], exp, err_msg=f"tile {t}")
+
+
+@pytest.mark.parametrize("pt,dtype,lo,hi", [(_lib.PIXELS_UINT8, np.uint8, 0, 256),
+                                            (_lib.PIXELS_UINT16, np.uint16, 0, 65536),
+                                            (_lib.PIXELS_INT16, np.int16, -32768, 32768),
+                                            (_lib.PIXELS_FLOAT, np.float32, -100, 70000)])
+def test_inverted_and_empty_windows(ctx, pt, dtype, lo, hi):
+    """inputStart > inputEnd and inputStart == inputEnd: the lower end is tested first upstream,
+    so below the start is cdStart even past the end, and the rest is cdEnd (a step at the start).
+    Mixed with an ordinary window so every K2 mode path meets them (linear16 used to let the
+    upper end win)."""
+    w, h = 96, 40
+    rng = np.random.default_rng(int(hi) & 0xFFFF)
+    planes = [rng.integers(lo, hi, (h, w)).astype(dtype) for _ in range(3)]
+    span = hi - lo
+    for ws, we in [(lo + 0.8 * span, lo + 0.2 * span), (lo + 0.5 * span, lo + 0.5 * span),
+                   (lo + 0.6 * span + 0.5, lo + 0.3 * span)]:
+        chans = [{"input_start": f32(ws), "input_end": f32(we), "rgba": (255, 0, 0, 255)},
+                 {"input_start": f32(lo + 0.1 * span), "input_end": f32(lo + 0.9 * span), "rgba": (0, 255, 0, 255)},
+                 {"input_start": f32(we), "input_end": f32(ws), "rgba": (0, 0, 255, 255), "reverse": True}]
+        if pt != _lib.PIXELS_FLOAT:
+            for c in chans:
+                c["global_min"], c["global_max"] = float(lo), float(hi - 1)
+        got = host_render(ctx, chans, planes, pt, w, h)
+        st, exp = O.render(chans, planes, pt, w, h)
+        assert st == 0
+        np.testing.assert_array_equal(got, exp, err_msg=f"window {ws}:{we}")

@@ -186,3 +186,17 @@ def test_int16_window_start_inexact_after_bias_falls_back(ctx):
         files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h)
         assert st.tolist() == [0, 0]
         assert files == _expect(chans, tiles, _lib.PIXELS_INT16, w, h), ws
+
+
+@pytest.mark.parametrize("starts", [(100.0, 0.0, 2000.0), (100.5, 0.0, 2000.25), (-3.0, 7.0, 65000.0)])
+def test_fast16_integral_and_fractional_window_starts(ctx, starts):
+    """Default-codomain linear u16 channels take F1's Fast16 mode; with every window start an
+    integer the kernel subtracts in int32 (Fast16I), otherwise in f64: both byte-identical."""
+    w, h = 128, 64
+    tiles = [[p.astype(">u2") for p in tile_u16(120 + t, 3, h, w)] for t in range(2)]
+    ends = (3000.0, 65535.0, 9000.75)
+    chans = [{"input_start": f32(s), "input_end": f32(e), "global_min": 0.0, "global_max": 65535.0,
+              "rgba": c} for s, e, c in zip(starts, ends, [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255)])]
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, True))
+    assert st.tolist() == [0, 0]
+    assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, True))
