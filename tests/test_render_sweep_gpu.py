@@ -1,0 +1,157 @@
+"""Randomised parity sweep of renderAsPackedInt (K1 + K2 through the C ABI) against the CPU
+restatement: pixel types, channel counts, active flags, windows (ordinary, inverted, empty,
+beyond the type range, fractional, NaN / infinite ends), families and coefficients, reverse,
+noise reduction, codomains and bit resolutions, greyscale and rgb, colours and .lut tables,
+flips, and pixels at the type extremes (float: NaN, +-inf, -0).  Fixed seeds.
+
+Bar (north_star): bit-exact for the linear family; log / polynomial / exponential may differ by
+one code where the device log/pow and glibc's differ in the last ulp (+-2 per component when two
+channels share it, and nearly every pixel exact)."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from omr import _lib
+from omr.context import make_qdef
+from omr.renderer import f32
+
+pytestmark = pytest.mark.gpu
+
+TYPES = [(_lib.PIXELS_UINT8, np.uint8), (_lib.PIXELS_INT8, np.int8), (_lib.PIXELS_UINT16, np.uint16),
+         (_lib.PIXELS_INT16, np.int16), (_lib.PIXELS_UINT32, np.uint32), (_lib.PIXELS_INT32, np.int32),
+         (_lib.PIXELS_FLOAT, np.float32)]
+
+
+def _range(dtype):
+    if dtype == np.float32:
+        return -5000.0, 70000.0
+    i = np.iinfo(dtype)
+    return float(i.min), float(i.max)
+
+
+def _planes(rng, dtype, n, h, w):
+    lo, hi = _range(dtype)
+    out = []
+    for _ in range(n):
+        if dtype == np.float32:
+            p = rng.normal(20000, 20000, (h, w)).astype(np.float32)
+            p.flat[rng.integers(0, h * w, 6)] = [np.nan, np.inf, -np.inf, -0.0, 0.0, 1e30]
+        else:
+            p = rng.integers(int(lo), int(hi) + 1, (h, w), dtype=np.int64).astype(dtype)
+            p.flat[rng.integers(0, h * w, 2)] = [lo, hi]
+        out.append(p)
+    return out
+
+
+def _window(rng, dtype):
+    lo, hi = _range(dtype)
+    span = hi - lo
+    kind = rng.integers(0, 8)
+    a, b = sorted(rng.uniform(lo, hi, 2))
+    if kind == 0:
+        return b, a                                   # inverted
+    if kind == 1:
+        return a, a                                   # empty
+    if kind == 2:
+        return lo - 0.3 * span, hi + 0.3 * span       # beyond the type range
+    if kind == 3:
+        return float(np.floor(a)) + 0.25, float(np.floor(a)) + 0.75 + rng.integers(0, 9)
+    if kind == 4 and dtype == np.float32:
+        return (float("nan"), b) if rng.integers(0, 2) else (a, float("inf"))
+    return a, b
+
+
+def _config(seed):
+    rng = np.random.default_rng(seed)
+    pt, dtype = TYPES[seed % len(TYPES)]
+    n = int(rng.integers(1, 5))
+    chans = []
+    for c in range(n):
+        ws, we = _window(rng, dtype)
+        d = {"active": bool(rng.integers(0, 5) > 0), "input_start": f32(ws), "input_end": f32(we),
+             "rgba": tuple(int(v) for v in rng.integers(0, 256, 4)),
+             "reverse": bool(rng.integers(0, 4) == 0), "noise_reduction": bool(rng.integers(0, 5) == 0)}
+        fam = int(rng.choice([_lib.FAMILY_LINEAR] * 5 + [_lib.FAMILY_POLYNOMIAL, _lib.FAMILY_LOGARITHMIC,
+                                                          _lib.FAMILY_EXPONENTIAL]))
+        if fam != _lib.FAMILY_LINEAR:
+            d["family"] = fam
+            d["coefficient"] = float(rng.choice([0.5, 1.0, 1.5, 2.0, 0.3]))
+        if rng.integers(0, 5) == 0:
+            d["lut"] = rng.integers(0, 256, 768).astype(np.uint8)
+        if dtype != np.float32:
+            lo, hi = _range(dtype)
+            d["global_min"], d["global_max"] = lo, hi
+        chans.append(d)
+    cds = int(rng.choice([0, 0, 0, 10, 40]))
+    cde = int(rng.choice([255, 255, 200, 128])) if cds < 100 else 255
+    q = make_qdef("greyscale" if rng.integers(0, 4) == 0 else "rgb", cd_start=cds, cd_end=cde,
+                  bit_resolution=int(rng.choice([255, 255, 127, 63])))
+    flips = (bool(rng.integers(0, 2)), bool(rng.integers(0, 2)))
+    return pt, dtype, chans, q, flips, rng
+
+
+@pytest.mark.parametrize("seed", list(range(int(__import__("os").environ.get("OMR_SWEEP_SEEDS", "56")))))
+def test_render_sweep(ctx, seed):
+    pt, dtype, chans, q, (fh, fv), rng = _config(seed)
+    h, w = 24, 40
+    planes = _planes(rng, dtype, len(chans), h, w)
+    st, exp = O.render(chans, planes, pt, w, h, qdef=q, flip_h=fh, flip_v=fv)
+    try:
+        got = ctx.render_packed_int(q, chans, planes, pt, w, h, flip_h=fh, flip_v=fv)
+        gst = 0
+    except _lib.OmrError as e:
+        gst = e.status
+    assert gst == st, f"status {gst} vs restatement {st}"
+    if st:
+        return
+    linear = all(c.get("family", _lib.FAMILY_LINEAR) == _lib.FAMILY_LINEAR for c in chans if c["active"])
+    if linear:
+        np.testing.assert_array_equal(got, exp)
+    else:
+        g, e = got.view(np.uint8).astype(int), exp.view(np.uint8).astype(int)
+        assert np.abs(g - e).max() <= 2 and np.mean(got == exp) > 0.98
+
+
+@pytest.mark.parametrize("seed", list(range(int(__import__("os").environ.get("OMR_SWEEP_SEEDS", "56")) // 2)))
+def test_render_jpeg_sweep(ctx, seed):
+    """The same random settings through the fused render -> JPEG batch (F1 for 8/16-bit types
+    with 1-4 active channels, else K2 + B1): every file byte-identical to the restatement's
+    render + JPEG (a QuantizationException flags the tile)."""
+    import torch
+    pt, dtype, chans, q, (fh, fv), rng = _config(1000 + seed)
+    if dtype not in (np.uint8, np.int8, np.uint16, np.int16):
+        pt, dtype = (_lib.PIXELS_UINT16, np.uint16) if seed % 2 else (_lib.PIXELS_INT8, np.int8)
+        lo, hi = _range(dtype)
+        for c in chans:
+            c["global_min"], c["global_max"] = lo, hi
+            ws, we = _window(rng, dtype)
+            c["input_start"], c["input_end"] = f32(ws), f32(we)
+    h, w, n = 32, 48, 2
+    tiles = [_planes(rng, dtype, len(chans), h, w) for _ in range(n)]
+    raw = np.stack([np.stack([np.ascontiguousarray(p).view(np.uint8).reshape(-1) for p in t]) for t in tiles])
+    data = torch.from_numpy(raw.copy()).to("cuda")
+    plane = raw.shape[2]
+    d_out = torch.empty(n * (w * h * 4 + 4096), dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n, dtype=torch.int64, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    stat = torch.full((n,), -7, dtype=torch.int32, device="cuda")
+    qual = float(rng.choice([0.5, 0.9, 1.0]))
+    ctx.render_jpeg_batch_strided_device(q, chans, data, len(chans) * plane, plane, n, pt, w, h, qual, d_out, offs,
+                                         lens, stat, flip_h=fh, flip_v=fv)
+    try:
+        ctx.synchronize()
+    except _lib.OmrError as e:
+        assert e.status == _lib.QUANTIZATION
+    o, ln, st = offs.cpu().numpy(), lens.cpu().numpy(), stat.cpu().numpy()
+    buf = d_out.cpu().numpy()
+    for i in range(n):
+        rst, argb = O.render(chans, tiles[i], pt, w, h, qdef=q, flip_h=fh, flip_v=fv)
+        if rst:
+            assert st[i] == _lib.QUANTIZATION
+            continue
+        assert st[i] == 0
+        exp = O.encode_jpeg(argb, w, h, qual)
+        got = buf[o[i]:o[i] + ln[i]].tobytes()
+        linear = all(c.get("family", _lib.FAMILY_LINEAR) == _lib.FAMILY_LINEAR for c in chans if c["active"])
+        if linear:
+            assert got == exp, f"tile {i}"
