@@ -4,6 +4,8 @@ Projection: ProjectionService.java:46-317 (bit-exact for every pixel type: integ
 exact, float sums keep the reference's z order in double).  Flips: the reference's index-oracle
 tests (ImageRegionRequestHandlerTest.java:69-200, ShapeMaskRequestHandlerTest.java:84-215).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -263,3 +265,38 @@ def test_projection_glue_quantization_error(glue_ctx):
     with pytest.raises(_lib.OmrError) as e:
         ctx.synchronize()
     assert e.value.status == _lib.QUANTIZATION
+
+
+@pytest.mark.parametrize("seed", list(range(int(os.environ.get("OMR_SWEEP_SEEDS", "40")))))
+def test_projection_glue_sweep(glue_ctx, seed):
+    """Random projection requests through the glue (K3 + K2, and K3R): type, byte order, active
+    channels, windows (inverted / empty / fractional), reverse, .lut, codomain, algorithm,
+    z range and stepping, flips — against the restatement's project + render."""
+    rng = np.random.default_rng(7000 + seed)
+    pt, dtype, (lo, hi) = GLUE_TYPES[seed % len(GLUE_TYPES)]
+    n = int(rng.integers(1, 5))
+    z, h, w = int(rng.integers(2, 20)), 16, 32 * int(rng.integers(1, 3))
+    stacks = [rand_stack(dtype, z, h, w, 9000 + 10 * seed + c) for c in range(n)]
+    be = bool(rng.integers(0, 2))
+    if be:
+        stacks = [s.astype(s.dtype.newbyteorder(">")) for s in stacks]
+    chans = []
+    for c in range(n):
+        a, b = sorted(rng.uniform(lo, hi, 2))
+        kind = rng.integers(0, 5)
+        ws, we = (b, a) if kind == 0 else (a, a) if kind == 1 else (a + 0.5, b) if kind == 2 else (a, b)
+        d = {"input_start": float(ws), "input_end": float(we), "global_min": lo, "global_max": hi,
+             "rgba": tuple(int(v) for v in rng.integers(0, 256, 4)), "reverse": bool(rng.integers(0, 3) == 0)}
+        if rng.integers(0, 5) == 0:
+            d["lut"] = rng.integers(0, 256, 768).astype(np.uint8)
+        chans.append(d)
+    alg = int(rng.choice([_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM]))
+    start = int(rng.integers(0, z))
+    end = int(rng.integers(start, z))
+    if alg != _lib.PROJECTION_MAX and end == start:
+        end = min(z - 1, start + 1)
+        if end == start:
+            start = max(0, start - 1)
+    qd_kw = {"cd_start": 20, "cd_end": 230} if rng.integers(0, 4) == 0 else None
+    _glue(glue_ctx, chans, stacks, pt, w, h, z, alg, start, end, stepping=int(rng.integers(1, 4)), be=be,
+          flip=(bool(rng.integers(0, 2)), bool(rng.integers(0, 2))), qd_kw=qd_kw)
