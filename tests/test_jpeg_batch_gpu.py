@@ -128,3 +128,22 @@ def test_batch_errors(ctx):
     with pytest.raises(_lib.OmrError) as e:
         ctx.encode_jpeg_batch(d, 1, 8, 8, 0.9, cap=100)   # a 8x8 file is > 100 bytes
     assert e.value.status == _lib.BUFFER_TOO_SMALL
+
+
+@pytest.mark.parametrize("seed", list(range(int(os.environ.get("OMR_SWEEP_SEEDS", "24")))))
+def test_jpeg_sweep_sizes_qualities(ctx, seed):
+    """Random tile sizes (1..300 per side, any remainder mod 16), qualities in (0, 1] and content
+    kinds through the batched encoder and the single-tile entry point: byte-identical to the
+    restatement."""
+    import torch
+    rng = np.random.default_rng(500 + seed)
+    w, h = int(rng.integers(1, 301)), int(rng.integers(1, 301))
+    q = float(rng.choice([0.01, 0.3, 0.75, 0.9, 1.0, float(rng.uniform(0.02, 1.0))]))
+    kinds = ["noise", "sparse", "flat", "smooth", "grey"]
+    tiles = [content(kinds[int(rng.integers(0, 5))], h, w, 40 * seed + i) for i in range(3)]
+    got = run_batch(ctx, tiles, w, h, q)
+    for i, t in enumerate(tiles):
+        exp = O.encode_jpeg(t, w, h, q)
+        assert got[i] == exp, f"batch tile {i} {w}x{h} q={q}"
+    d = torch.from_numpy(tiles[0].reshape(-1).view(np.int32).copy()).to("cuda")
+    assert ctx.encode_jpeg_device(d, w, h, q) == O.encode_jpeg(tiles[0], w, h, q), f"single {w}x{h} q={q}"
