@@ -101,7 +101,16 @@ __constant__ ZzInv c_zzinv = make_zzinv();
 
 struct QTabs {
     uint16_t q[2][64];  // natural order
+    uint32_t m[2][64];  // ceil(2^32 / (8 q)): B1's reciprocal quantiser (set_recips)
 };
+
+static void set_recips(QTabs& t) {
+    for (int c = 0; c < 2; ++c)
+        for (int i = 0; i < 64; ++i) {
+            const uint64_t d = (uint64_t)t.q[c][i] << 3;
+            t.m[c][i] = (uint32_t)((0x100000000ull + d - 1) / d);
+        }
+}
 
 // JPEGQTable.getScaledInstance(scale, forceBaseline=true): (int)(q*scale + 0.5f) in [1, 255].
 static int scale_entry(int q, float scale) {
@@ -936,8 +945,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
     const int ywib = (W + 7) / 8, yhib = (H + 7) / 8;
     const int nat = c_zigzag[lane];                 // this lane owns zig-zag position `lane`
     const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
-    const uint32_t my_ = (uint32_t)((0x100000000ull + (uint64_t)(qy << 3) - 1) / (uint64_t)(qy << 3));
-    const uint32_t mc_ = (uint32_t)((0x100000000ull + (uint64_t)(qc << 3) - 1) / (uint64_t)(qc << 3));
+    const uint32_t my_ = A.qt.m[0][nat], mc_ = A.qt.m[1][nat];   // host-computed (no 64-bit divide)
     const int hy = qy << 2, hc = qc << 2;
     const uint64_t lt_mask = (1ull << lane) - 1;
     // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
@@ -1616,6 +1624,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     // 4 MCUs per wave once that still gives >= 4 waves per SIMD (16 per CU)
     a1.mpw = (int64_t)n * L.n_mcu >= (int64_t)kB1McuPerWave * 16 * ctx->cu_count ? kB1McuPerWave : 1;
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
+    set_recips(a1.qt);
     uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
     B2aArgs a2{a1.aclen, a1.dcs, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
     GroupScanArgs a2b{u32(L.gsum), nullptr, u32(L.tbits), u32(L.words), nullptr, L.ngb, L.slot_words, (int32_t)L.ngb};
