@@ -754,7 +754,7 @@ struct B1Args {
     QTabs qt;
 };
 
-constexpr int kB1McuPerWave = 4;   // big batches; a few tiles use 1 so the grid still fills the chip
+constexpr int kB1McuPerWave = 8;   // big batches; a few tiles use 1 so the grid still fills the chip
 
 // Pixels (x, y) and (x+1, y) of one row (clamped to the image), as one 8-byte load when both
 // are inside the row.
