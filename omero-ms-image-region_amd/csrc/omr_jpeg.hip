@@ -1225,12 +1225,16 @@ struct B3Args {
 
 __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     __shared__ HuffLds h;
-    __shared__ uint32_t s_ac[2][256];   // AC tables packed as size << 16 | code
+    // AC tables packed as size << 16 | code, with the size-0 entries (run, 0) — EOB and ZRL are
+    // taken from c_huff directly — zeroed: a zero coefficient then codes as zero bits with no
+    // select in the coefficient loop
+    __shared__ uint32_t s_ac[2][256];
     __shared__ uint32_t s_words[kB3LdsWords];
     __shared__ uint32_t sw[16];
     load_huff_lds(h);
     for (int i = threadIdx.x; i < 512; i += blockDim.x)
-        s_ac[i >> 8][i & 255] = ((uint32_t)c_huff[1 + 2 * (i >> 8)].size[i & 255] << 16) | c_huff[1 + 2 * (i >> 8)].code[i & 255];
+        s_ac[i >> 8][i & 255] = (i & 15) == 0 ? 0u
+            : ((uint32_t)c_huff[1 + 2 * (i >> 8)].size[i & 255] << 16) | c_huff[1 + 2 * (i >> 8)].code[i & 255];
     const int tile = blockIdx.y;
     const int b = blockIdx.x * kGrp + threadIdx.x;
     const int64_t gb = (int64_t)tile * A.nb + b;
@@ -1288,7 +1292,8 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
             const int nbits = d ? 32 - __clz(d) : 0;
             put(((uint32_t)h.code[td][nbits] << nbits) | ((uint32_t)d2 & ((1u << nbits) - 1)), h.size[td][nbits] + nbits);
         }
-        const uint32_t zrl = s_ac[ta][0xF0];
+        const uint32_t zrl = ((uint32_t)c_huff[1 + 2 * ta].size[0xF0] << 16) | c_huff[1 + 2 * ta].code[0xF0];
+        const uint32_t eob = ((uint32_t)c_huff[1 + 2 * ta].size[0x00] << 16) | c_huff[1 + 2 * ta].code[0x00];
         int r = 0;
         // Branch-free per coefficient: a zero contributes a zero-length code; runs of 16+ zeros
         // before a non-zero (ZRL) take a wave-uniform, rarely entered branch.
@@ -1303,10 +1308,10 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
             const int nbits = 32 - __clz(a);                       // 0 for c == 0
             const uint32_t cs = s_ac[ta][((r & 15) << 4) | nbits];
             const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
-            put(nzk ? v : 0u, nzk ? (int)(cs >> 16) + nbits : 0);
+            put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
             r = nzk ? 0 : r + 1;
         }
-        if (r > 0) put(s_ac[ta][0] & 0xFFFF, (int)(s_ac[ta][0] >> 16));   // EOB
+        if (r > 0) put(eob & 0xFFFF, (int)(eob >> 16));                   // EOB
         if (nacc > 0) {                                                   // shared with the next block
             const uint32_t w = (uint32_t)(acc << (32 - nacc));
             if (staged) atomicOr(&s_words[wpos - gw0], w);
