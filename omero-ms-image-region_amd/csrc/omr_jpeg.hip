@@ -1301,7 +1301,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         for (int k = 1; k < 64; ++k) {
             const int c = coef(k);
             const bool nzk = c != 0;
-            if (__ballot(nzk && r > 15)) {
+            if (k > 16 && __ballot(nzk && r > 15)) {                // r <= k - 1: no ZRL before k 17
                 if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
             }
             const int a = c < 0 ? -c : c;
