@@ -256,7 +256,18 @@ __global__ void __launch_bounds__(kBlock) k_project_v(K3Args A, uint32_t n_iter)
 #pragma unroll
         for (int u = 0; u < 8; ++u) fold(q[u]);
     }
-    for (; i < i1; ++i, p += pchunks) fold(__builtin_nontemporal_load(p));
+    if (i < i1) {
+        // the remainder (< 8 planes) as one batch of loads too: planes past i1 re-read the last
+        // one (a cache hit) and are not folded.  One load at a time here made the z split's
+        // wave with the remainder (the mean's 63 planes: 15 / 16 / 16 / 16) hold its workgroup
+        const uint32_t rem = i1 - i;
+        p32x4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = __builtin_nontemporal_load(p + (uint64_t)min((uint32_t)u, rem - 1) * pchunks);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if ((uint32_t)u < rem) fold(q[u]);
+    }
     if constexpr (SPLIT) {
         if (wave > 0) {
 #pragma unroll

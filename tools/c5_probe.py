@@ -38,7 +38,7 @@ def main():
     for t in range(B):
         data[t].copy_(src.view(uniq, -1)[t % uniq])
     out = torch.empty((B, T, T), dtype=torch.int32, device=dev)
-    ctx = omr.Context(0)
+    ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
     qd, binds, plane = make_qdef("rgb"), make_bindings(chans), T * T * 4
 
     def step():

@@ -19,7 +19,7 @@ def main():
     import bench
     B, T = 64, 1024
     dev = torch.device("cuda", 0)
-    ctx = omr.Context(0)
+    ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
     if os.environ.get("JPEG_PROBE_CASE", "c2") == "c1":
         g = torch.Generator(device=dev)
         g.manual_seed(20261015)

@@ -21,7 +21,7 @@ def main():
     from omr.context import make_qdef
     from omr.synthetic import c2_channels, tile_u16
     T = 1024
-    ctx = omr.Context(0)
+    ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
     planes = [torch.from_numpy(np.ascontiguousarray(p.astype(">u2")).view(np.uint8).reshape(-1)).to("cuda")
               for p in tile_u16(7, 4, T, T)]
     out = torch.empty((T, T), dtype=torch.int32, device="cuda")
