@@ -26,6 +26,7 @@ def main():
     qd, binds = make_qdef("rgb"), make_bindings(c2_channels(C))
     out = torch.empty((S, S), dtype=torch.int32, device=dev)
     ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
+    torch.cuda.synchronize()                    # inputs made by torch kernels
     res = {}
     for name, alg in (("max", _lib.PROJECTION_MAX), ("mean", _lib.PROJECTION_MEAN)):
         def step():

@@ -39,6 +39,7 @@ def main():
         data[t].copy_(src.view(uniq, -1)[t % uniq])
     out = torch.empty((B, T, T), dtype=torch.int32, device=dev)
     ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
+    torch.cuda.synchronize()                    # inputs made by torch kernels
     qd, binds, plane = make_qdef("rgb"), make_bindings(chans), T * T * 4
 
     def step():

@@ -37,6 +37,7 @@ def main():
     offs = torch.empty(B, dtype=torch.int64, device=dev)
     lens = torch.empty(B, dtype=torch.int32, device=dev)
     stat = torch.empty(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()                    # inputs made by torch kernels
     n = int(os.environ.get("JPEG_PROBE_ITERS", "5"))
     for _ in range(n):
         ctx.render_batch_strided_device(q, ch, data, nc * pb, pb, B, pt, T, T, argb, big_endian=be, bindings=binds)
