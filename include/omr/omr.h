@@ -382,6 +382,21 @@ omr_status omr_render_jpeg_batch_strided_device(omr_ctx* ctx, const omr_quantum_
                                                 int32_t flip_h, int32_t flip_v, float quality, uint8_t* d_out,
                                                 size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
                                                 int32_t* d_status);
+/*
+ * One render_image_region request in its default format (format=jpeg, ImageRegionCtx.java:146):
+ * renderAsPackedInt + flip + createBufferedImage + compressToStream
+ * (ImageRegionRequestHandler.java:559-582) of one tile whose planes are already in HBM, the JPEG
+ * file landing in `out` (host memory).  d_planes is a HOST array of size_c device pointers, one per
+ * channel (an inactive channel's may be null).  Same files as omr_render_packed_int_device +
+ * omr_encode_jpeg_device, in one call with one stream sync (K2's small-launch render + the one-tile
+ * JPEG pipeline: measured faster for a single tile than the fused kernel).  Synchronous; a pixel outside its LUT
+ * domain returns OMR_QUANTIZATION (-> 500); *out_len is set whenever the length is known
+ * (OMR_BUFFER_TOO_SMALL when cap is short).  Tiles up to 4096 x 4096.
+ */
+omr_status omr_render_jpeg(omr_ctx* ctx, const omr_quantum_def* qdef, const omr_channel_binding* channels,
+                           int32_t size_c, const void* const* d_planes, int64_t row_stride, int32_t pixel_type,
+                           int32_t big_endian, int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                           float quality, uint8_t* out, size_t cap, size_t* out_len);
 /* Same with a device plane-pointer table [tile][channel] (omr_render_batch_device's layout). */
 omr_status omr_render_jpeg_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,
                                         const omr_channel_binding* channels, int32_t size_c,

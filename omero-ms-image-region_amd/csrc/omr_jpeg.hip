@@ -1821,6 +1821,33 @@ static omr_status render_jpeg_batch(Ctx* ctx, const omr_quantum_def* qdef, const
                                       d_status, L, rstat);
 }
 
+// One render_image_region request in its default format: the small-launch render (K2 builds its
+// tables in LDS: no K1) into the context's aux ARGB tile, the context's sticky quantization flag
+// moved to pinned host memory behind it, then the one-tile JPEG pipeline landing the file in
+// pinned memory — one stream sync.  (The fused kernel, and the batch entry at n = 1, measured
+// slower for a single tile: tools/omr_latency.cpp.)
+static omr_status render_jpeg_one(Ctx* ctx, const omr_quantum_def* qdef, const omr_channel_binding* channels,
+                                  int32_t size_c, const void* const* d_planes, int64_t row_stride, int32_t pt,
+                                  int32_t be, int32_t W, int32_t H, int32_t fh, int32_t fv, float quality,
+                                  uint8_t* out, size_t cap, size_t* out_len) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (!d_planes || size_c <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "bad plane list");
+    if (W <= 0 || H <= 0 || W > kJpegBatchMaxDim || H > kJpegBatchMaxDim)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG request: tile dimensions must be 1..4096");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    omr_status st = ensure_aux(ctx, (size_t)W * H * 4);
+    if (st) return st;
+    uint32_t* argb = static_cast<uint32_t*>(ctx->aux);
+    omr_ctx* cx = static_cast<omr_ctx*>(ctx);
+    st = omr_render_packed_int_device(cx, qdef, channels, size_c, d_planes, row_stride, pt, be, W, H, fh, fv, argb);
+    if (st) return st;
+    OMR_HIP(ctx, launch_flag_out(ctx->stream, ctx->d_flag, ctx->h_flag));   // read after the JPEG's sync
+    const omr_status jst = encode_jpeg_single_batched(ctx, argb, W, H, quality, out, cap, out_len, 0);
+    if (*static_cast<volatile int32_t*>(ctx->h_flag))
+        return fail(ctx, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");
+    return jst;
+}
+
 }  // namespace omr
 
 extern "C" {
@@ -1837,6 +1864,14 @@ omr_status omr_render_jpeg_batch_strided_device(omr_ctx* ctx, const omr_quantum_
     return omr::render_jpeg_batch(ctx, qdef, channels, size_c, d_base, tile_stride_bytes, channel_stride_bytes,
                                   nullptr, n_tiles, row_stride, pixel_type, big_endian, width, height, flip_h, flip_v,
                                   quality, d_out, out_cap, d_offsets, d_lengths, d_status);
+}
+
+omr_status omr_render_jpeg(omr_ctx* ctx, const omr_quantum_def* qdef, const omr_channel_binding* channels,
+                           int32_t size_c, const void* const* d_planes, int64_t row_stride, int32_t pixel_type,
+                           int32_t big_endian, int32_t width, int32_t height, int32_t flip_h, int32_t flip_v,
+                           float quality, uint8_t* out, size_t cap, size_t* out_len) {
+    return omr::render_jpeg_one(ctx, qdef, channels, size_c, d_planes, row_stride, pixel_type, big_endian, width,
+                                height, flip_h, flip_v, quality, out, cap, out_len);
 }
 
 omr_status omr_render_jpeg_batch_device(omr_ctx* ctx, const omr_quantum_def* qdef,

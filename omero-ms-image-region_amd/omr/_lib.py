@@ -174,6 +174,8 @@ _SIGS = {
                                                     _i32, _i32, _i32, _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
     "omr_render_jpeg_batch_device": (_i32, [_vp, _QD, _CB, _i32, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
                                             _i32, _f32, _vp, _sz, _vp, _vp, _vp]),
+    "omr_render_jpeg": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp, _sz,
+                               ctypes.POINTER(_sz)]),
     "omr_jpeg_quant_tables_sem": (_i32, [_f32, ctypes.c_uint32, _vp, _vp]),
     "omr_tiff_max_bytes": (_sz, [_i32, _i32]),
     "omr_encode_tiff": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),

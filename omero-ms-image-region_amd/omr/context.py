@@ -291,6 +291,20 @@ class Context:
             row_stride, pixel_type, int(big_endian), width, height, int(flip_h), int(flip_v), float(quality),
             _ptr(d_out), d_out.numel(), _ptr(d_offsets), _ptr(d_lengths), _ptr(d_status)), self.h)
 
+    def render_jpeg_device(self, qdef, channels, planes, pixel_type, width, height, quality, big_endian=False,
+                           flip_h=False, flip_v=False, row_stride=0, bindings=None):
+        """One request in the default format (omr_render_jpeg): device planes (one tensor or
+        address per channel, None for an inactive one) -> JPEG bytes."""
+        arr, keep = make_bindings(channels) if bindings is None else bindings
+        ptrs = (ctypes.c_void_p * max(len(planes), 1))(*[_ptr(p) for p in planes])
+        cap = lib.omr_jpeg_max_bytes(width, height)
+        out = np.empty(cap, dtype=np.uint8)
+        n = ctypes.c_size_t(0)
+        check(lib.omr_render_jpeg(self.h, ctypes.byref(qdef), arr, len(channels), ptrs, row_stride, pixel_type,
+                                  int(big_endian), width, height, int(flip_h), int(flip_v), float(quality),
+                                  out.ctypes.data, cap, ctypes.byref(n)), self.h)
+        return out[:n.value].tobytes()
+
     def render_jpeg_batch_device(self, qdef, channels, d_plane_ptrs, n_tiles, pixel_type, width, height, quality,
                                  d_out, d_offsets, d_lengths, d_status=None, big_endian=False, flip_h=False,
                                  flip_v=False, row_stride=0, bindings=None):

@@ -200,3 +200,46 @@ def test_fast16_integral_and_fractional_window_starts(ctx, starts):
     files, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, True))
     assert st.tolist() == [0, 0]
     assert files == _expect(chans, tiles, _lib.PIXELS_UINT16, w, h, be=True, flip=(True, True))
+
+
+@pytest.mark.parametrize("pt,w,h", [(_lib.PIXELS_UINT16, 1024, 1024), (_lib.PIXELS_UINT16, 120, 72),
+                                    (_lib.PIXELS_UINT8, 256, 128), (_lib.PIXELS_FLOAT, 64, 48)])
+def test_render_jpeg_one_request(ctx, pt, w, h):
+    """omr_render_jpeg (one request, default format): device planes -> host JPEG, fused for
+    16-multiple 8/16-bit tiles, K2 + B1 otherwise; the restatement's render + JPEG file, with an
+    inactive channel passed as a null plane, flips, and a QuantizationException."""
+    import torch
+    rng = np.random.default_rng(w + h)
+    if pt == _lib.PIXELS_UINT16:
+        planes = [p.astype(">u2") for p in tile_u16(150, 4, h, w)]
+        chans = c2_channels(4)
+        be = True
+    elif pt == _lib.PIXELS_UINT8:
+        planes = [rng.integers(0, 256, (h, w)).astype(np.uint8) for _ in range(4)]
+        chans = [{"input_start": 10.0 * c, "input_end": 200.0 + c, "global_min": 0.0, "global_max": 255.0,
+                  "rgba": (255 * (c & 1), 255 * (c >> 1 & 1), 128, 255)} for c in range(4)]
+        be = False
+    else:
+        planes = [rng.uniform(-10, 300, (h, w)).astype(np.float32) for _ in range(4)]
+        chans = [{"input_start": 0.0, "input_end": 255.0, "rgba": (255, 0, 0, 255)},
+                 {"input_start": 5.0, "input_end": 200.0, "rgba": (0, 0, 255, 255)}] * 2
+        be = False
+    chans = [dict(c) for c in chans]
+    chans[2]["active"] = False
+    dev = [torch.from_numpy(np.ascontiguousarray(p).view(np.uint8).reshape(-1)).to("cuda") for p in planes]
+    dev[2] = None
+    q = make_qdef("rgb")
+    for fh, fv in [(False, False), (True, True)]:
+        got = ctx.render_jpeg_device(q, chans, dev, pt, w, h, 0.85, big_endian=be, flip_h=fh, flip_v=fv)
+        st, argb = O.render(chans, planes, pt, w, h, big_endian=be, flip_h=fh, flip_v=fv)
+        assert st == 0
+        assert got == O.encode_jpeg(argb, w, h, 0.85), (fh, fv)
+    if pt == _lib.PIXELS_UINT16:
+        bad = [dict(c) for c in chans]
+        bad[0]["global_max"] = 1000.0
+        with pytest.raises(_lib.OmrError) as e:
+            ctx.render_jpeg_device(q, bad, dev, pt, w, h, 0.85, big_endian=be)
+        assert e.value.status == _lib.QUANTIZATION
+        got = ctx.render_jpeg_device(q, chans, dev, pt, w, h, 0.85, big_endian=be)   # the flag was consumed
+        st, argb = O.render(chans, planes, pt, w, h, big_endian=be)
+        assert got == O.encode_jpeg(argb, w, h, 0.85)

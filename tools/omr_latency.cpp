@@ -6,6 +6,7 @@
 // 0000FF,00FF00,FF0000,FFFFFF): bindings filled per request (updateSettings, :689-741), then
 //   render  : omr_render_packed_int_device + omr_ctx_synchronize   (renderAsPackedInt, :559)
 //   jpeg    : render + omr_encode_jpeg_device to a host buffer      (+ compressToStream, :580-582)
+//   fused   : omr_render_jpeg (the same request in one call: render inside the JPEG's first kernel)
 // with the planes already in HBM.  Prints one JSON object: p50 / p90 / mean in ms.
 //
 // Usage: omr_latency [iters] [device]
@@ -105,10 +106,23 @@ int main(int argc, char** argv) {
         const double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         if (i >= 5) t_jpeg.push_back(ms);
     }
-    const Stats r = stats(t_render), j = stats(t_jpeg);
+    std::vector<double> t_fused;
+    size_t flen = 0;
+    for (int i = 0; i < iters + 5; ++i) {
+        const auto t0 = clk::now();
+        fill_bindings(ch);
+        if (!ok(omr_render_jpeg(ctx, &q, ch, kChannels, (const void* const*)d_planes, 0, OMR_PIXELS_UINT16, 1, kTile,
+                                kTile, 0, 0, 0.9f, jpeg.data(), cap, &flen), ctx, "render_jpeg"))
+            return 1;
+        const double ms = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        if (i >= 5) t_fused.push_back(ms);
+    }
+    if (flen != jlen) { std::fprintf(stderr, "fused JPEG length %zu != %zu\n", flen, jlen); return 1; }
+    const Stats r = stats(t_render), j = stats(t_jpeg), f = stats(t_fused);
     std::printf("{\"iters\": %d, \"render_device_resident\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f}, "
-                "\"render_to_jpeg_host\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f, \"jpeg_bytes\": %zu}}\n",
-                iters, r.p50, r.p90, r.mean, j.p50, j.p90, j.mean, jlen);
+                "\"render_to_jpeg_host\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f, \"jpeg_bytes\": %zu}, "
+                "\"render_jpeg_one_call\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f}}\n",
+                iters, r.p50, r.p90, r.mean, j.p50, j.p90, j.mean, jlen, f.p50, f.p90, f.mean);
     for (int c = 0; c < kChannels; ++c) (void)hipFree(d_planes[c]);
     (void)hipFree(d_argb);
     omr_ctx_destroy(ctx);
