@@ -377,7 +377,15 @@ __global__ void __launch_bounds__(kBlock) k_project_render(K3RArgs A) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) fold(q[k]);
         }
-        for (; i < i1; ++i, p += pchunks) fold(__builtin_nontemporal_load(p));
+        if (i < i1) {                   // the remainder (< 8 planes) as one batch, as K3 does
+            const uint32_t rem = i1 - i;
+            p32x4 q[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) q[k] = __builtin_nontemporal_load(p + (uint64_t)min((uint32_t)k, rem - 1) * pchunks);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if ((uint32_t)k < rem) fold(q[k]);
+        }
 #pragma unroll
         for (int j = 0; j < V; ++j) s_part[part][a][ch * V + j] = acc[j];
     }
