@@ -1843,6 +1843,7 @@ static omr_status render_jpeg_one(Ctx* ctx, const omr_quantum_def* qdef, const o
     if (st) return st;
     OMR_HIP(ctx, launch_flag_out(ctx->stream, ctx->d_flag, ctx->h_flag));   // read after the JPEG's sync
     const omr_status jst = encode_jpeg_single_batched(ctx, argb, W, H, quality, out, cap, out_len, 0);
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));     // (already idle unless the encode failed early)
     if (*static_cast<volatile int32_t*>(ctx->h_flag))
         return fail(ctx, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");
     return jst;

@@ -1036,8 +1036,10 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         K2Chan& k = F.ch[i];
         k.index = c.index;
         k.mode = c.mode;
-        k.lo = c.lo + bias;
-        k.hi = c.hi + bias;
+        // saturating: a window end at +-inf / NaN / beyond 2^31 is already clamped to INT32_MAX / MIN
+        auto sat = [](int64_t v) { return (int32_t)std::min<int64_t>(std::max<int64_t>(v, INT32_MIN), INT32_MAX); };
+        k.lo = sat((int64_t)c.lo + bias);
+        k.hi = sat((int64_t)c.hi + bias);
         k.gmin = c.gmin + bias;
         k.gmax = c.gmax + bias;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;

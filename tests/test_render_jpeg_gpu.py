@@ -243,3 +243,19 @@ def test_render_jpeg_one_request(ctx, pt, w, h):
         got = ctx.render_jpeg_device(q, chans, dev, pt, w, h, 0.85, big_endian=be)   # the flag was consumed
         st, argb = O.render(chans, planes, pt, w, h, big_endian=be)
         assert got == O.encode_jpeg(argb, w, h, 0.85)
+
+
+def test_int16_fused_window_ends_at_the_int32_limits(ctx):
+    """int16 through F1 moves the integer window ends by 32768; ends already clamped to the int32
+    limits (a window end at 1e12 / -1e12, or beyond) must saturate, not wrap."""
+    w, h = 64, 32
+    rng = np.random.default_rng(23)
+    tiles = [[rng.integers(-32768, 32768, (h, w)).astype(np.int16) for _ in range(2)] for _ in range(2)]
+    chans = [{"input_start": f32(-1e12), "input_end": f32(1e12), "global_min": -32768.0, "global_max": 32767.0,
+              "rgba": (255, 0, 0, 255)},
+             {"input_start": f32(-100.0), "input_end": f32(3e9), "global_min": -32768.0, "global_max": 32767.0,
+              "rgba": (0, 255, 0, 255), "reverse": True}]
+    for qd_kw in (None, {"cd_start": 10, "cd_end": 240}):     # Fast16, then Linear16 (integer ends)
+        files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h, qd_kw=qd_kw)
+        assert st.tolist() == [0, 0]
+        assert files == _expect(chans, tiles, _lib.PIXELS_INT16, w, h, qdef=make_qdef("rgb", **(qd_kw or {})))
