@@ -46,7 +46,7 @@ def _planes(rng, dtype, n, h, w):
 def _window(rng, dtype):
     lo, hi = _range(dtype)
     span = hi - lo
-    kind = rng.integers(0, 8)
+    kind = rng.integers(0, 9)
     a, b = sorted(rng.uniform(lo, hi, 2))
     if kind == 0:
         return b, a                                   # inverted
@@ -56,8 +56,10 @@ def _window(rng, dtype):
         return lo - 0.3 * span, hi + 0.3 * span       # beyond the type range
     if kind == 3:
         return float(np.floor(a)) + 0.25, float(np.floor(a)) + 0.75 + rng.integers(0, 9)
-    if kind == 4 and dtype == np.float32:
+    if kind == 4:
         return (float("nan"), b) if rng.integers(0, 2) else (a, float("inf"))
+    if kind == 5:
+        return (-1e12, b) if rng.integers(0, 2) else (a, 3e9)    # integer ends at the int32 limits
     return a, b
 
 
