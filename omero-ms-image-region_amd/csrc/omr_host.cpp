@@ -33,6 +33,12 @@ bool parse_hex2(const std::string& s, int32_t& out) {
     return true;
 }
 
+// Java int arithmetic: two's-complement wrap-around (JLS 15.17.1 / 15.18.2), which is
+// undefined behaviour on int32_t in C++, so go through uint32_t.
+inline int32_t jadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+inline int32_t jsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+inline int32_t jmul(int32_t a, int32_t b) { return (int32_t)((uint32_t)a * (uint32_t)b); }
+
 }  // namespace
 
 extern "C" {
@@ -100,8 +106,8 @@ omr_status omr_get_region_def(int32_t mode, const omr_region* request, int32_t r
         if (tsy > max_tile_length) tsy = max_tile_length;
         rd.width = tsx;
         rd.height = tsy;
-        rd.x = request->x * tsx;
-        rd.y = request->y * tsy;
+        rd.x = jmul(request->x, tsx);
+        rd.y = jmul(request->y, tsy);
     } else if (mode == 1) {
         if (!request) return OMR_INVALID_ARGUMENT;
         rd = *request;
@@ -110,21 +116,21 @@ omr_status omr_get_region_def(int32_t mode, const omr_region* request, int32_t r
         *out = rd;
         return OMR_OK;
     }
-    rd.width = std::min(rd.width, size_x - rd.x);
-    rd.height = std::min(rd.height, size_y - rd.y);
-    if (flip_h) rd.x = size_x - rd.width - rd.x;
-    if (flip_v) rd.y = size_y - rd.height - rd.y;
+    rd.width = std::min(rd.width, jsub(size_x, rd.x));
+    rd.height = std::min(rd.height, jsub(size_y, rd.y));
+    if (flip_h) rd.x = jsub(jsub(size_x, rd.width), rd.x);
+    if (flip_v) rd.y = jsub(jsub(size_y, rd.height), rd.y);
     *out = rd;
     return OMR_OK;
 }
 
-int32_t omr_resolution_level(int32_t n_levels, int32_t resolution) { return n_levels - resolution - 1; }
+int32_t omr_resolution_level(int32_t n_levels, int32_t resolution) { return jsub(jsub(n_levels, resolution), 1); }
 
 // checkPlaneDef (:651-681).
 omr_status omr_check_plane_def(omr_region* rd, int32_t size_x, int32_t size_y) {
     if (!rd) return OMR_OK;
-    if (rd->width + rd->x > size_x) rd->width = size_x - rd->x;
-    if (rd->height + rd->y > size_y) rd->height = size_y - rd->y;
+    if (jadd(rd->width, rd->x) > size_x) rd->width = jsub(size_x, rd->x);
+    if (jadd(rd->height, rd->y) > size_y) rd->height = jsub(size_y, rd->y);
     return OMR_OK;
 }
 
@@ -147,8 +153,8 @@ omr_status omr_parse_lut(const uint8_t* data, size_t n, uint8_t lut_out[768]) {
             while (k < j && (data[k] == ' ' || data[k] == '\t' || data[k] == ',' || data[k] == '\r')) ++k;
             if (k >= j) break;
             if (!std::isdigit(data[k])) { bad = true; break; }
-            long v = 0;
-            while (k < j && std::isdigit(data[k])) v = v * 10 + (data[k++] - '0');
+            long v = 0;   // saturates: anything above 255 is rejected below
+            while (k < j && std::isdigit(data[k])) v = std::min(v * 10 + (data[k++] - '0'), 1000000L);
             nums.push_back(v);
         }
         if (!bad && (nums.size() == 3 || nums.size() == 4)) {

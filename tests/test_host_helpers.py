@@ -113,6 +113,23 @@ def test_resolution_level_and_check_plane_def():
     assert (r.x, r.y, r.width, r.height) == (900, 10, 124, 1014)
 
 
+def test_region_arithmetic_wraps_like_java_int():
+    # getRegionDef multiplies tile index by tile size in Java int (:803-804) and
+    # truncate/flip subtract in int (:751-780): overflow wraps, it does not saturate.
+    def wrap(v):
+        return (v + 2**31) % 2**32 - 2**31
+    x = region_def(TILE, (2**20 + 1, 0, 0, 0), L1024, (4096, 256), max_tile=4096)
+    assert x[0] == wrap((2**20 + 1) * 4096) == 4096
+    assert x[2] == min(4096, wrap(1024 - 4096)) == -3072
+    big = region_def(REGION, (-2**31, 0, 100, 100), L1024, flip_h=True)
+    w = min(100, wrap(1024 + 2**31))                                # Math.min(w, sizeX - x)
+    assert big[2] == w == -2147482624 and big[0] == wrap(1024 - w + 2**31) == 0
+    assert lib.omr_resolution_level(-2**31, 0) == 2**31 - 1
+    r = Region(2**31 - 10, 0, 100, 50)
+    lib.omr_check_plane_def(ctypes.byref(r), 1024, 1024)          # width + x wraps negative: untouched
+    assert (r.x, r.width) == (2**31 - 10, 100)
+
+
 @pytest.mark.parametrize("color,exp", [
     ("FF0000", [255, 0, 0, 255]), ("00FF00", [0, 255, 0, 255]), ("0000FF", [0, 0, 255, 255]),
     ("abbccd", [0xAB, 0xBC, 0xCD, 0xFF]), ("abbccdde", [0xAB, 0xBC, 0xCD, 0xDE]),
