@@ -274,7 +274,12 @@ __global__ void __launch_bounds__(256) k_build_thresh(const RenderPlan* __restri
 // Buckets over the key range where a kModeThresh channel's code varies, [T[1], T[cmax]):
 // bucket b covers 2^shift keys; its entry is (#T <= its first key) | (#T inside it) << 8, so K2
 // searches only the few thresholds of its bucket (usually 0-2) instead of all 255.
-constexpr int kBucketsLog2 = 11, kBuckets = 1 << kBucketsLog2;
+#ifndef OMR_K2_BUCKETS_LOG2
+#define OMR_K2_BUCKETS_LOG2 11
+#endif
+constexpr int kBucketsLog2 = OMR_K2_BUCKETS_LOG2, kBuckets = 1 << kBucketsLog2;
+// channels whose threshold + bucket tables fit K2's 48 KiB LDS budget (8 at 2048 buckets)
+constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 2u * kBuckets));
 
 __device__ __forceinline__ uint32_t bucket_shift(uint32_t span) {
     const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
@@ -685,7 +690,7 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
         ++na;
     }
     P.n_active = na;
-    if (na > 8)   // threshold + bucket tables are 6 KiB of LDS per channel: keep K2 within 48 KiB
+    if (na > kMaxThreshActive)   // threshold + bucket tables (6 KiB of LDS per channel): K2 within 48 KiB
         for (int i = 0; i < na; ++i)
             if (P.ch[i].mode == kModeThresh) P.ch[i].mode = kModeEval;
     pp.plan_bytes = offsetof(RenderPlan, ch) + sizeof(ChanParam) * (size_t)(na > 0 ? na : 1);
@@ -939,7 +944,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     const uint64_t per_block = (uint64_t)kBlock * cpt_thread;
     a.n_work = (uint32_t)((total + per_block - 1) / per_block);
     const bool eval_mode = bpp >= 4;     // kK2Eval: grid-stride over the work blocks
-    const int grid = eval_mode ? (int)std::min<uint64_t>(a.n_work, (uint64_t)ctx->cu_count * 8) : (int)a.n_work;
+    // resident blocks per CU: 8 (2 per SIMD), fewer when the LDS tables (160 KiB per CU) allow fewer
+    const uint64_t k2_res = std::min<uint64_t>(8, (160u * 1024u) / k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0));
+    const int grid = eval_mode ? (int)std::min<uint64_t>(a.n_work, (uint64_t)ctx->cu_count * k2_res) : (int)a.n_work;
     hipError_t e;
     const bool be = big_endian != 0;
     KernelTimer timer(ctx, 2);
