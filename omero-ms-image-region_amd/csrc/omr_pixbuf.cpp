@@ -268,6 +268,11 @@ omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_
     const int bpp = bytes_per_pixel(pixel_type);
     if (!path || !bpp || size_x <= 0 || size_y <= 0 || size_z <= 0 || size_c <= 0 || size_t_ <= 0)
         return OMR_INVALID_ARGUMENT;
+    // file size = x * y * z * c * t * bpp: reject dimensions whose product overflows int64
+    // (a wrapped size could pass the file-size check below)
+    int64_t total = bpp;
+    for (const int32_t d : {size_x, size_y, size_z, size_c, size_t_})
+        if (__builtin_mul_overflow(total, (int64_t)d, &total)) return OMR_INVALID_ARGUMENT;
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return OMR_NOT_FOUND;
     auto* pb = new omr_pixel_buffer;
@@ -277,7 +282,7 @@ omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_
     pb->bpp = bpp;
     pb->row_bytes = (int64_t)size_x * bpp;
     pb->plane_bytes = pb->row_bytes * size_y;
-    pb->total = pb->plane_bytes * size_z * size_c * size_t_;
+    pb->total = total;
     struct stat sb;
     if (::fstat(fd, &sb) != 0 || (int64_t)sb.st_size < pb->total) {   // RomioPixelBuffer size check
         ::close(fd);

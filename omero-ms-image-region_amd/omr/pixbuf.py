@@ -79,6 +79,8 @@ class PixelBuffer:
 
     def get_tile(self, z, c, t, x, y, w, h):
         """PixelBuffer.getTile: [h][w] array in file (big-endian) byte order."""
+        if w < 0 or h < 0:   # DimensionsOutOfBoundsException, as the C bounds check
+            raise _lib.OmrError(_lib.INVALID_ARGUMENT, f"tile {w}x{h} out of bounds")
         out = np.empty((h, w), dtype=_BE_DTYPES[self.pixel_type])
         _lib.check(lib.omr_pixel_buffer_get_tile(self.h, z, c, t, x, y, w, h, out.ctypes.data, out.nbytes))
         return out
