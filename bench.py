@@ -526,22 +526,12 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
     import numpy as np
     from omr import _lib
     from omr.context import make_bindings, make_qdef
-    from omr.renderer import f32
-    from omr.synthetic import C2_COLORS
+    from omr.synthetic import c5_channels, c5_planes
     dev = torch.device("cuda", ctx.device)
     rng = np.random.default_rng(20261015 + 5)
     uniq = 4
-    host = np.stack([np.stack([rng.lognormal(5, 1.5, (TILE, TILE)).astype(np.float32),
-                               rng.normal(0, 300, (TILE, TILE)).astype(np.float32),
-                               rng.lognormal(5, 1.5, (TILE, TILE)).astype(np.float32)]) for _ in range(uniq)])
-    lut = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
-    chans = []
-    for c in range(3):
-        lo, hi = np.percentile(host[0, c], 1), np.percentile(host[0, c], 99)
-        chans.append({"input_start": f32(lo), "input_end": f32(hi), "rgba": C2_COLORS[c]})
-    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
-    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
-    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=lut)
+    host = np.stack([np.stack(c5_planes(TILE, TILE, rng)) for _ in range(uniq)])
+    chans = c5_channels(list(host[0]))      # p1/p99 windows; the x^0.5 window starts at >= 1.0
     be_host = host.astype(">f4")
     src = torch.from_numpy(np.ascontiguousarray(be_host).view(np.uint8)).to(dev)
     data = torch.empty((B, 3 * TILE * TILE * 4), dtype=torch.uint8, device=dev)
@@ -576,7 +566,10 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
                                            f"on {threads} threads (oracle/omr_oracle.c, {oracle_lib.FAST_BUILD})"}
         except Exception as e:
             log(f"c5 cpu baseline failed: {e}")
-    # render_shape_mask: 1024x1024 mask of random ellipses, FF000080, flip hv (host API, p50)
+    # render_shape_mask: 1024x1024 mask of random ellipses, FF000080, flip hv (host API, p50).  A
+    # 1024-wide mask with a flip is the reference's packed-buffer failure (404) by default, so the
+    # leg runs the pixel flip (OMR_SEM_MASK_PIXEL_FLIP) it evidently intends.
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
     yy, xx = np.mgrid[0:TILE, 0:TILE]
     m = np.zeros((TILE, TILE), bool)
     for _ in range(24):
@@ -589,8 +582,9 @@ def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):
         png = ctx.render_shape_mask_png(bits, TILE, TILE, (255, 0, 0, 128), flip_h=True, flip_v=True)
         if i >= 3:
             lat.append(time.perf_counter() - t0)
+    ctx.set_semantics(0)
     r["shape_mask_png"] = {"p50_ms": round(1e3 * float(np.median(lat)), 4), "png_bytes": len(png),
-                           "size": "1024x1024 1-bit, flip hv"}
+                           "size": "1024x1024 1-bit, flip hv", "semantics": "OMR_SEM_MASK_PIXEL_FLIP"}
     return r
 
 
@@ -634,7 +628,7 @@ def png_section(torch, ctx, data):
     return res
 
 
-def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8):
+def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8, pool_devices=None):
     """render_image_region JPEG tiles (q 0.9) served to concurrent clients from the ROMIO file:
     one request at a time on one context (the reference's shape: a Renderer per request) vs the
     batcher (omr_batcher_*: the dispatcher coalesces what the 8 client threads submit, 8 tiles
@@ -642,7 +636,7 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
     rendered once."""
     import threading
     import numpy as np
-    from omr import Batcher
+    from omr import Batcher, Pool
     reqs = [(0, 0, (i % grid) * TILE, ((i // grid) % grid) * TILE) for i in range(n_req)]
     dev = torch.empty((TILE, TILE), dtype=torch.int32, device="cuda")
     lat = []
@@ -655,9 +649,15 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
     el = time.perf_counter() - t0
     res = {"requests": n_req, "clients": clients,
            "one_at_a_time": {"tiles_per_s": round(64 / el, 1), "p50_ms": round(1e3 * float(np.median(lat)), 3)}}
-    for mb, wait_us in ((64, 1000),):
+    legs = [("batcher_max64_wait1000us", lambda: Batcher(ctx.device, max_batch=64, max_wait_us=1000))]
+    if pool_devices:
+        # omr_pool: one batcher per entry of pool_devices (the node's GPUs; on a one-GPU box the
+        # entries share the card), each job to the least-queued one
+        legs.append((f"pool_{len(pool_devices)}x_max64_wait1000us",
+                     lambda: Pool(pool_devices, max_batch=64, max_wait_us=1000)))
+    for name, make in legs:
         lats = []
-        with Batcher(ctx.device, max_batch=mb, max_wait_us=wait_us) as b:
+        with make() as b:
             def client(k):          # a viewer asks for a screenful (8 tiles) at a time
                 mine = list(range(k, n_req, clients))
                 for s0 in range(0, len(mine), 8):
@@ -677,14 +677,17 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
                     t.join()
                 el = time.perf_counter() - t0
             st = b.stats()
-        res[f"batcher_max{mb}_wait{wait_us}us"] = {"tiles_per_s": round(n_req / el, 1),
-                                                   "p50_ms": round(1e3 * float(np.median(lats)), 3),
-                                                   "rendered": st["rendered"], "dedup": st["dedup"],
-                                                   "rounds": st["batches"]}
+        if isinstance(st, list):
+            leg = {"devices": list(pool_devices), "jobs_per_device": [s["jobs"] for s in st],
+                   "rendered": sum(s["rendered"] for s in st), "dedup": sum(s["dedup"] for s in st),
+                   "rounds": sum(s["batches"] for s in st)}
+        else:
+            leg = {"rendered": st["rendered"], "dedup": st["dedup"], "rounds": st["batches"]}
+        res[name] = {"tiles_per_s": round(n_req / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3), **leg}
     return res
 
 
-def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
+def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, pool_devices=None):
     """The step before the path: C2 tiles read from a ROMIO repository
     file (big-endian XYZCT planes, as pixelsService.getPixelBuffer opens, ImageRegionRequestHandler
     .java:302-309) by omr_render_pixel_buffer_tiles: pread into pinned staging, H2D on a copy
@@ -758,7 +761,7 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu):
             res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
         _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
         _lib.lib.omr_pinned_free(ctx.h, pin)
-        res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid)
+        res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid, pool_devices=pool_devices)
         pb.close()
     finally:
         os.unlink(path)
@@ -830,6 +833,9 @@ def main():
                     help="skip the C3 (projection) and C5 (float32 families, shape mask) sections")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the single-tile latency probe (profiling runs: batch launches only)")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="batchers of the serving-pool leg (omr_pool over cuda:i %% visible GPUs); "
+                         "0 = one per visible GPU, at least 2")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,
                     help="untimed device warm-up before the W warm-up steps: the first ~25 K2 launches "
                          "after idle run 0.77 -> 0.60 ms while the GPU clocks ramp (profiles/r02/"
@@ -964,8 +970,10 @@ def main():
                 log(f"png section failed: {e}")
                 raise
             try:
+                n_pool = args.pool or max(2, n_dev)
                 extra["host_fed"] = host_fed_section(torch, ctx, uniq, 64, args.cpu_seconds / 4, threads,
-                                                     not args.no_cpu_baseline)
+                                                     not args.no_cpu_baseline,
+                                                     pool_devices=[i % n_dev for i in range(n_pool)])
             except Exception as e:
                 log(f"host-fed section failed: {e}")
                 raise

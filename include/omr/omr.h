@@ -155,7 +155,25 @@ enum {
      * original channel index (:525, :549): a rendered channel whose index is >= #active fails its
      * bounds check (DimensionsOutOfBoundsException -> 500, here OMR_INTERNAL). */
     OMR_SEM_PROJECTION_ALL_ACTIVE = 1u << 4,
-    OMR_SEM_ALL = 0x1Fu
+    /* S2 logarithmic map without the x <= 0 guard: f(x) = Math.log(x) for every x (NaN below 0,
+     * -Infinity at 0, propagated through both rounding stages as Java does: Math.round(NaN) = 0).
+     * By default f(x) = x > 0 ? log(x) : 0. */
+    OMR_SEM_LOG_UNGUARDED = 1u << 5,
+    /* S4 noise reduction off: a channel's noiseReduction flag has no effect.  By default the first
+     * and last decile of the window clip to cdStart / cdEnd. */
+    OMR_SEM_NOISE_REDUCTION_OFF = 1u << 6,
+    /* Exponential map on the window-normalised input (Appendix C): f(x) = exp(pow((x - start) /
+     * (end - start), k)).  By default f(x) = exp(pow(x, k)), which overflows to +Infinity above
+     * x ~ 709 for k = 1 (a 16-bit window then renders cdStart below its end). */
+    OMR_SEM_EXP_NORMALIZED = 1u << 7,
+    /* Shape mask, width % 8 == 0 with a flip: flip at pixel level (the evident intent).  By default
+     * the reference is reproduced: it flips the still bit-packed buffer as if it held one byte per
+     * pixel (ShapeMaskRequestHandler.java:175-181, :145-150), which indexes past the array
+     * (ArrayIndexOutOfBoundsException -> the future fails -> 404, ShapeMaskVerticle.java:119-128,
+     * here OMR_NOT_FOUND) unless the buffer holds >= width*height bytes, when the byte-flipped
+     * buffer is rendered as packed bits. */
+    OMR_SEM_MASK_PIXEL_FLIP = 1u << 8,
+    OMR_SEM_ALL = 0x1FFu
 };
 /* Semantics of every later call on this context (renders, projections' renders, JPEG). */
 omr_status omr_ctx_set_semantics(omr_ctx* ctx, uint32_t flags);
@@ -212,7 +230,8 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
  * batched JPEG launch, and identical tiles in flight together are rendered once.
  * submit/wait are thread-safe; the pixel buffer must outlive its jobs.
  */
-enum { OMR_FORMAT_JPEG = 0, OMR_FORMAT_PNG = 1, OMR_FORMAT_ARGB = 2 /* packed int[] */ };
+enum { OMR_FORMAT_JPEG = 0, OMR_FORMAT_PNG = 1, OMR_FORMAT_ARGB = 2 /* packed int[] */,
+       OMR_FORMAT_TIFF = 3 /* TIFFImageWriter branch, :583-596 */ };
 typedef struct omr_tile_job {
     const omr_pixel_buffer* pb;
     const struct omr_quantum_def* qdef;            /* copied at submit */
@@ -233,8 +252,33 @@ omr_status omr_batcher_submit(omr_batcher* b, const omr_tile_job* job, uint64_t*
 omr_status omr_batcher_wait(omr_batcher* b, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
 /* jobs submitted, dispatch rounds, tiles rendered, duplicate tiles served from a sibling job */
 omr_status omr_batcher_stats(omr_batcher* b, uint64_t stats_out[4]);
-/* OMR_SEM_* flags of the batcher's context (call before submitting). */
+/* OMR_SEM_* flags for jobs submitted after this call (each job keeps the flags it was submitted
+ * under; jobs with different flags never share a render). */
 omr_status omr_batcher_set_semantics(omr_batcher* b, uint32_t flags);
+
+/* ---- node-level serving pool: the request batches of all worker threads over the node's GPUs ---- */
+/*
+ * The reference's only parallelism is N worker-verticle instances over one worker pool
+ * (ImageRegionMicroserviceVerticle.java:84-85, :149-165).  A pool holds one batcher per entry of
+ * devices[] (its own context, stream, dispatcher thread and plan / LUT replicas in that GPU's
+ * HBM; an ordinal may repeat, e.g. two batchers on one card) and sends each submitted job to the
+ * batcher with the fewest jobs queued or in flight.  Tiles are independent, so nothing crosses
+ * between GPUs: no collective, no peer copies.  submit / wait are thread-safe and keep the
+ * batcher's per-tile statuses (OMR_QUANTIZATION fails only its own tile).  At most 256 devices.
+ */
+typedef struct omr_pool omr_pool;
+omr_status omr_pool_create(const int32_t* devices, int32_t n_devices, int32_t max_batch, int32_t max_wait_us,
+                           omr_pool** out);
+void       omr_pool_destroy(omr_pool* p);
+int32_t    omr_pool_size(const omr_pool* p);
+omr_status omr_pool_submit(omr_pool* p, const omr_tile_job* job, uint64_t* ticket);
+/* omr_batcher_wait of the batcher holding the ticket. */
+omr_status omr_pool_wait(omr_pool* p, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
+/* Index into devices[] of the batcher a ticket went to (-1: not a ticket of this pool). */
+int32_t    omr_pool_device_index(const omr_pool* p, uint64_t ticket);
+omr_status omr_pool_set_semantics(omr_pool* p, uint32_t flags);
+/* stats_out[4*i .. 4*i+3] = omr_batcher_stats of device i; n_entries >= omr_pool_size. */
+omr_status omr_pool_stats(omr_pool* p, uint64_t* stats_out, int32_t n_entries);
 
 /* ---- render (quantize + codomain + composite + flip) ------------------ */
 /*
@@ -434,8 +478,12 @@ omr_status omr_encode_tiff_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t 
 /*
  * ShapeMaskRequestHandler.renderShapeMask(Color, byte[], w, h) (:165-207): MSB-first bit mask
  * (no row padding) -> flip -> 2-entry palette PNG (index 0 transparent, index 1 = rgba).
- * Deviation: flips at pixel level also when width % 8 == 0 (the reference flips the
- * still-packed buffer there and fails, :175-181).  Host in/out.
+ * width % 8 == 0 with a flip follows the reference's packed-buffer flip unless the context has
+ * OMR_SEM_MASK_PIXEL_FLIP (see there).  Every exception the reference raises inside
+ * renderShapeMask (a null or short mask, a zero size, the packed-buffer flip's
+ * ArrayIndexOutOfBoundsException, width*height past Java int) completes its future exceptionally,
+ * which ShapeMaskVerticle.java:119-128 answers with 404: OMR_NOT_FOUND.  A null rgba or out is
+ * OMR_INVALID_ARGUMENT.  Host in/out.
  */
 omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n_bytes,
                                      int32_t width, int32_t height, const uint8_t rgba[4],
@@ -445,7 +493,9 @@ omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n
 /* ---- host-side request helpers (no device work) ---------------------------------- */
 /* ImageRegionRequestHandler.splitHTMLColor (:865-890), bug-compatible; OMR_INVALID_ARGUMENT = null. */
 omr_status omr_split_html_color(const char* color, int32_t rgba_out[4]);
-/* ShapeMaskRequestHandler.renderShapeMask(Mask) fill colour (:97-106). */
+/* ShapeMaskRequestHandler.renderShapeMask(Mask) fill colour (:97-106).  OMR_INVALID_ARGUMENT where the
+ * reference throws (NPE on an unparsable colour, Color's IAE); inside renderShapeMask that fails the
+ * future, which the verticle answers with 404 (ShapeMaskVerticle.java:119-128). */
 omr_status omr_shape_mask_fill_color(int32_t has_mask_fill, int32_t mask_fill_color,
                                      const char* request_color, uint8_t rgba_out[4]);
 /*

@@ -12,6 +12,7 @@
 // are rendered once.
 #include "omr_internal.h"
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -29,7 +30,8 @@ struct Job {
     std::vector<omr_channel_binding> ch;
     std::vector<std::vector<uint8_t>> luts;     // owned copies of the .lut tables
     omr_tile_job spec{};
-    std::string group_key;                       // image + settings + size + flip + format
+    uint32_t sem = 0;                            // OMR_SEM_* of the batcher when the job was submitted
+    std::string group_key;                       // image + settings + semantics + size + flip + format
     std::chrono::steady_clock::time_point t_submit;
 };
 
@@ -54,6 +56,8 @@ struct omr_batcher {
     uint64_t next_ticket = 1;
     bool stop = false;
     uint64_t n_jobs = 0, n_batches = 0, n_rendered = 0, n_dedup = 0;
+    uint32_t sem = 0;                        // OMR_SEM_* copied into every job at submit (under m)
+    std::atomic<int64_t> outstanding{0};     // jobs submitted and not yet completed (pool dispatch)
     // device buffers of the dispatcher (grown on demand)
     uint32_t* d_argb = nullptr;
     size_t argb_cap = 0;
@@ -93,38 +97,47 @@ static std::string settings_key(const Job& j) {
     const omr_tile_job& s = j.spec;
     const int32_t geo[5] = {s.width, s.height, s.flip_h, s.flip_v, s.format};
     append(k, geo, sizeof(geo));
+    append(k, &j.sem, sizeof(j.sem));
     append(k, &s.quality, sizeof(s.quality));
     return k;
 }
 
+// Every pointer is cleared (and its capacity zeroed) as soon as it is freed, so a failed
+// hipMalloc leaves nothing for omr_batcher_destroy to free twice.
+template <typename T>
+static omr_status regrow(omr_ctx* c, T*& p, size_t bytes) {
+    if (p) {
+        const hipError_t e = hipFree(p);
+        p = nullptr;
+        OMR_HIP(c, e);
+    }
+    OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&p), bytes));
+    return OMR_OK;
+}
+
 static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
     omr_ctx* c = B->ctx;
+    omr_status st;
     if (argb > B->argb_cap) {
-        if (B->d_argb) OMR_HIP(c, hipFree(B->d_argb));
-        B->d_argb = nullptr;
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_argb), argb));
+        B->argb_cap = 0;
+        if ((st = regrow(c, B->d_argb, argb))) return st;
         B->argb_cap = argb;
     }
     if (jpeg > B->jpeg_cap) {
-        if (B->d_jpeg) OMR_HIP(c, hipFree(B->d_jpeg));
-        B->d_jpeg = nullptr;
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_jpeg), jpeg));
+        B->jpeg_cap = 0;
+        if ((st = regrow(c, B->d_jpeg, jpeg))) return st;
         B->jpeg_cap = jpeg;
     }
     if (n > B->meta_cap) {
-        if (B->d_offs) OMR_HIP(c, hipFree(B->d_offs));
-        if (B->d_lens) OMR_HIP(c, hipFree(B->d_lens));
-        if (B->d_stat) OMR_HIP(c, hipFree(B->d_stat));
-        if (B->d_rstat) OMR_HIP(c, hipFree(B->d_rstat));
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_rstat), sizeof(int32_t) * n));
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_offs), sizeof(uint64_t) * n));
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_lens), sizeof(uint32_t) * n));
-        OMR_HIP(c, hipMalloc(reinterpret_cast<void**>(&B->d_stat), sizeof(int32_t) * n));
+        B->meta_cap = 0;
+        if ((st = regrow(c, B->d_rstat, sizeof(int32_t) * n))) return st;
+        if ((st = regrow(c, B->d_offs, sizeof(uint64_t) * n))) return st;
+        if ((st = regrow(c, B->d_lens, sizeof(uint32_t) * n))) return st;
+        if ((st = regrow(c, B->d_stat, sizeof(int32_t) * n))) return st;
         B->meta_cap = n;
     }
     return OMR_OK;
 }
-
 // Render + encode one group (same image, settings, size, flip, format).  jobs[u] are the
 // distinct tiles; out[u] receives each one's bytes, or OMR_QUANTIZATION for a tile with a pixel
 // outside the LUT domain — only that tile fails, as only that request's Renderer would throw
@@ -132,6 +145,7 @@ static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
 static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
     omr_ctx* c = B->ctx;
     const Job& j0 = *jobs[0];
+    c->sem = j0.sem;      // the group's semantics (every job of a group has the same), dispatcher thread only
     const int n = (int)jobs.size();
     const int W = j0.spec.width, H = j0.spec.height;
     const size_t px = (size_t)W * H;
@@ -176,6 +190,15 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
             if (out[i].st) continue;
             size_t len = 0;
             st = omr_encode_png_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
+            if (st) return st;
+            out[i].bytes.assign(buf.begin(), buf.begin() + len);
+        }
+    } else if (j0.spec.format == OMR_FORMAT_TIFF) {        // TIFFImageWriter branch (:583-596)
+        std::vector<uint8_t> buf(omr_tiff_max_bytes(W, H));
+        for (int i = 0; i < n; ++i) {
+            if (out[i].st) continue;
+            size_t len = 0;
+            st = omr_encode_tiff_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
             if (st) return st;
             out[i].bytes.assign(buf.begin(), buf.begin() + len);
         }
@@ -244,6 +267,7 @@ static void dispatch_loop(omr_batcher* B) {
         }
         lk.lock();
         for (auto& r : results) B->done[r.first] = std::move(r.second);
+        B->outstanding -= (int64_t)results.size();
         B->n_batches += 1;
         B->n_rendered += rendered;
         B->n_dedup += dedup;
@@ -294,7 +318,8 @@ omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t*
     if (!B || !job || !ticket || !job->pb || !job->qdef || !job->channels || job->size_c <= 0)
         return OMR_INVALID_ARGUMENT;
     if (job->width <= 0 || job->height <= 0) return OMR_INVALID_ARGUMENT;
-    if (job->format != OMR_FORMAT_JPEG && job->format != OMR_FORMAT_PNG && job->format != OMR_FORMAT_ARGB)
+    if (job->format != OMR_FORMAT_JPEG && job->format != OMR_FORMAT_PNG && job->format != OMR_FORMAT_ARGB &&
+        job->format != OMR_FORMAT_TIFF)
         return OMR_NOT_FOUND;                              // unknown format -> null -> 404 (:602-603)
     auto j = std::make_unique<Job>();
     j->pb = job->pb;
@@ -309,14 +334,16 @@ omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t*
     j->spec = *job;
     j->spec.qdef = nullptr;
     j->spec.channels = nullptr;
-    j->group_key = settings_key(*j);
     j->t_submit = std::chrono::steady_clock::now();
     {
         std::lock_guard<std::mutex> g(B->m);
+        j->sem = B->sem;                  // semantics fixed at submit: a later set_semantics cannot
+        j->group_key = settings_key(*j);  // reach a job already queued or a group in flight
         j->ticket = B->next_ticket++;
         *ticket = j->ticket;
         B->pending.push_back(std::move(j));
         B->n_jobs++;
+        B->outstanding++;
     }
     B->cv_in.notify_one();
     return OMR_OK;
@@ -341,8 +368,12 @@ omr_status omr_batcher_wait(omr_batcher* B, uint64_t ticket, uint8_t* out, size_
 
 omr_status omr_batcher_set_semantics(omr_batcher* B, uint32_t flags) {
     if (!B) return OMR_INVALID_ARGUMENT;
-    std::lock_guard<std::mutex> g(B->m);   // the dispatcher reads it between rounds
-    return omr_ctx_set_semantics(B->ctx, flags);
+    if (flags & ~(uint32_t)OMR_SEM_ALL) return OMR_INVALID_ARGUMENT;
+    // jobs carry the flags from submit; the dispatcher applies a group's flags to its own context
+    // (run_group), so this never touches the context another thread is rendering with
+    std::lock_guard<std::mutex> g(B->m);
+    B->sem = flags;
+    return OMR_OK;
 }
 
 omr_status omr_batcher_stats(omr_batcher* B, uint64_t stats_out[4]) {
@@ -352,6 +383,100 @@ omr_status omr_batcher_stats(omr_batcher* B, uint64_t stats_out[4]) {
     stats_out[1] = B->n_batches;
     stats_out[2] = B->n_rendered;
     stats_out[3] = B->n_dedup;
+    return OMR_OK;
+}
+
+// ---- node-level pool: one batcher per GPU ------------------------------------
+// The reference scales a node with N worker-verticle instances over one worker pool
+// (ImageRegionMicroserviceVerticle.java:84-85, :149-165).  The pool spreads the workers' tile
+// jobs over the node's GPUs: every device has its own batcher (context, stream, dispatcher thread,
+// and its own plan / LUT replicas in its HBM), a job goes to the batcher with the fewest jobs
+// queued or in flight (ties rotate), and the ticket remembers which batcher holds it.  Tiles are
+// independent: there is no collective and no peer traffic.
+struct omr_pool {
+    std::vector<omr_batcher*> b;
+    std::vector<int32_t> devices;
+    std::atomic<uint32_t> rr{0};
+};
+
+static constexpr int kPoolIndexBits = 8;   // up to 256 batchers; ticket = batcher ticket << 8 | index
+
+omr_status omr_pool_create(const int32_t* devices, int32_t n_devices, int32_t max_batch, int32_t max_wait_us,
+                           omr_pool** out) {
+    if (!out) return OMR_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (!devices || n_devices <= 0 || n_devices > (1 << kPoolIndexBits) || max_batch <= 0 || max_wait_us < 0)
+        return OMR_INVALID_ARGUMENT;
+    auto* P = new omr_pool;
+    for (int i = 0; i < n_devices; ++i) {
+        omr_batcher* b = nullptr;
+        const omr_status st = omr_batcher_create(devices[i], max_batch, max_wait_us, &b);
+        if (st) {
+            for (omr_batcher* x : P->b) omr_batcher_destroy(x);
+            delete P;
+            return st;
+        }
+        P->b.push_back(b);
+        P->devices.push_back(devices[i]);
+    }
+    *out = P;
+    return OMR_OK;
+}
+
+void omr_pool_destroy(omr_pool* P) {
+    if (!P) return;
+    for (omr_batcher* b : P->b) omr_batcher_destroy(b);
+    delete P;
+}
+
+int32_t omr_pool_size(const omr_pool* P) { return P ? (int32_t)P->b.size() : 0; }
+
+omr_status omr_pool_submit(omr_pool* P, const omr_tile_job* job, uint64_t* ticket) {
+    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
+    const int n = (int)P->b.size();
+    const uint32_t start = P->rr.fetch_add(1, std::memory_order_relaxed) % (uint32_t)n;
+    int best = (int)start;
+    int64_t best_q = P->b[best]->outstanding.load(std::memory_order_relaxed);
+    for (int k = 1; k < n; ++k) {                      // least queued, first from a rotating start
+        const int i = (int)((start + k) % (uint32_t)n);
+        const int64_t q = P->b[i]->outstanding.load(std::memory_order_relaxed);
+        if (q < best_q) { best = i; best_q = q; }
+    }
+    uint64_t t = 0;
+    const omr_status st = omr_batcher_submit(P->b[best], job, &t);
+    if (st) return st;
+    *ticket = (t << kPoolIndexBits) | (uint64_t)best;
+    return OMR_OK;
+}
+
+int32_t omr_pool_device_index(const omr_pool* P, uint64_t ticket) {
+    if (!P) return -1;
+    const uint64_t i = ticket & ((1u << kPoolIndexBits) - 1);
+    return i < P->b.size() ? (int32_t)i : -1;
+}
+
+omr_status omr_pool_wait(omr_pool* P, uint64_t ticket, uint8_t* out, size_t cap, size_t* len) {
+    const int32_t i = omr_pool_device_index(P, ticket);
+    if (i < 0) return OMR_INVALID_ARGUMENT;
+    return omr_batcher_wait(P->b[i], ticket >> kPoolIndexBits, out, cap, len);
+}
+
+omr_status omr_pool_set_semantics(omr_pool* P, uint32_t flags) {
+    if (!P) return OMR_INVALID_ARGUMENT;
+    if (flags & ~(uint32_t)OMR_SEM_ALL) return OMR_INVALID_ARGUMENT;
+    for (omr_batcher* b : P->b) {
+        const omr_status st = omr_batcher_set_semantics(b, flags);
+        if (st) return st;
+    }
+    return OMR_OK;
+}
+
+omr_status omr_pool_stats(omr_pool* P, uint64_t* stats_out, int32_t n_entries) {
+    if (!P || !stats_out || n_entries < (int32_t)P->b.size()) return OMR_INVALID_ARGUMENT;
+    for (size_t i = 0; i < P->b.size(); ++i) {
+        const omr_status st = omr_batcher_stats(P->b[i], stats_out + 4 * i);
+        if (st) return st;
+    }
     return OMR_OK;
 }
 

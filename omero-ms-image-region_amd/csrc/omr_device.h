@@ -18,14 +18,9 @@ __device__ __forceinline__ int64_t java_round_d(double a) {
     return (int64_t)f;
 }
 
-// Family maps (SEMANTICS TABLE S2 in oracle/omr_oracle.c).
-__device__ __forceinline__ double family_map(int family, double x, double k) {
-    switch (family) {
-    case OMR_FAMILY_POLYNOMIAL: return pow(x, k);
-    case OMR_FAMILY_LOGARITHMIC: return x > 0 ? log(x) : 0.0;
-    case OMR_FAMILY_EXPONENTIAL: return exp(pow(x, k));
-    default: return x;
-    }
+// Family maps (SEMANTICS TABLE S2 in oracle/omr_oracle.c) of a channel.
+__device__ __forceinline__ double family_map(const ChanParam& p, double x) {
+    return family_map_code(p.family, x, p.k, p.ws, p.we);
 }
 
 // q(x) of an integer pixel (the LUT types): window, noise reduction, family map, two rounding
@@ -39,7 +34,7 @@ __device__ __forceinline__ int quantize_eval(double x, const ChanParam& p, int c
         if (x < p.ws + p.dec) return cds & 0xFF;
         if (x >= p.we - p.dec) return cde & 0xFF;
     }
-    const double v = (double)java_round_d(p.a0 * (family_map(p.family, x, p.k) - p.ys));
+    const double v = (double)java_round_d(p.a0 * (family_map(p, x) - p.ys));
     return (int)(java_round_d(p.a1 * v + (double)cds) & 0xFF);
 }
 

@@ -33,13 +33,35 @@ enum ChanMode : int32_t {
                        // thresholds of q in key space, K2 binary-searches them in LDS
 };
 
+// Family map the kernels evaluate (ChanParam::family): the omr.h family with the OMR_SEM_* variant
+// of its map folded in by the host (prepare_plan).
+enum FamilyCode : int32_t {
+    kFamLinear = OMR_FAMILY_LINEAR,
+    kFamPoly = OMR_FAMILY_POLYNOMIAL,
+    kFamLog = OMR_FAMILY_LOGARITHMIC,       // x > 0 ? log(x) : 0
+    kFamExp = OMR_FAMILY_EXPONENTIAL,       // exp(pow(x, k))
+    kFamLogRaw = 4,                         // log(x) for every x (OMR_SEM_LOG_UNGUARDED)
+    kFamExpNorm = 5                         // exp(pow((x - ws)/(we - ws), k)) (OMR_SEM_EXP_NORMALIZED)
+};
+// Host and device evaluate the same expressions (-ffp-contract=off): the CPU restatement's S2.
+__host__ __device__ inline double family_map_code(int family, double x, double k, double ws, double we) {
+    switch (family) {
+    case kFamPoly: return pow(x, k);
+    case kFamLog: return x > 0 ? log(x) : 0.0;
+    case kFamExp: return exp(pow(x, k));
+    case kFamLogRaw: return log(x);
+    case kFamExpNorm: return exp(pow((x - ws) / (we - ws), k));
+    default: return x;
+    }
+}
+
 // One active channel as the kernels see it (device memory, read uniformly).
 struct ChanParam {
     int32_t index;      // channel index into the [tile][size_c] plane table
     int32_t mode;
     int32_t lo, hi;     // integer window thresholds: x < lo -> cdStart, x >= hi -> cdEnd
     int32_t gmin, gmax; // LUT domain (QuantizationException outside)
-    int32_t family, nr;
+    int32_t family, nr; // FamilyCode; noise reduction in effect
     int32_t reverse, has_lut;
     int32_t second;     // apply the a1*v + cdStart rounding stage (not identity)
     int32_t pad0;

@@ -1270,10 +1270,29 @@ omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n
                                      int32_t height, const uint8_t rgba[4], int32_t flip_h, int32_t flip_v,
                                      uint8_t* out, size_t cap, size_t* out_len) {
     if (!ctx) return OMR_INVALID_ARGUMENT;
-    if (width <= 0 || height <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "Attempted to flip image with 0 size");
-    const int64_t npx = (int64_t)width * height;
-    if (!bits || (int64_t)n_bytes * 8 < npx) return fail(ctx, OMR_INVALID_ARGUMENT, "mask shorter than width*height bits");
     if (!rgba) return fail(ctx, OMR_INVALID_ARGUMENT, "null fill colour");
+    // Every exception the reference raises inside renderShapeMask fails its future, which
+    // ShapeMaskVerticle.java:119-128 answers with 404 ("Cannot render Mask").
+    if (width <= 0 || height <= 0) return fail(ctx, OMR_NOT_FOUND, "Attempted to flip image with 0 size");
+    const int64_t npx = (int64_t)width * height;
+    if (npx > INT32_MAX) return fail(ctx, OMR_NOT_FOUND, "width*height overflows a Java int");
+    if (!bits) return fail(ctx, OMR_NOT_FOUND, "NullPointerException: null mask bytes");
+    if ((int64_t)n_bytes * 8 < npx) return fail(ctx, OMR_NOT_FOUND, "mask shorter than width*height bits");
+    // width % 8 == 0: the reference skips the unpack (:175-178) and flips the still-packed buffer as
+    // one byte per pixel (:179-181, :145-150) unless OMR_SEM_MASK_PIXEL_FLIP asks for the pixel flip
+    std::vector<uint8_t> packed_flip;
+    if (width % 8 == 0 && (flip_h || flip_v) && !(ctx->sem & OMR_SEM_MASK_PIXEL_FLIP)) {
+        if ((int64_t)n_bytes < npx)
+            return fail(ctx, OMR_NOT_FOUND, "ArrayIndexOutOfBoundsException: flip of the packed mask reads " +
+                                                std::to_string(npx) + " bytes of " + std::to_string(n_bytes));
+        packed_flip.assign(n_bytes, 0);   // new byte[src.length]; bytes past width*height stay 0
+        for (int64_t y = 0; y < height; ++y) {
+            const int64_t drow = (flip_v ? height - 1 - y : y) * width;
+            for (int64_t x = 0; x < width; ++x) packed_flip[drow + (flip_h ? width - 1 - x : x)] = bits[y * width + x];
+        }
+        bits = packed_flip.data();        // rendered as packed bits, no further flip
+        flip_h = flip_v = 0;
+    }
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const int kind = width % 8 == 0 ? kIdx1 : kIdx8;   // bitsPerPixel 1 or 8 (:174-178)
     const size_t nb = align_up(n_bytes, 256);

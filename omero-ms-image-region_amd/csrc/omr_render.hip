@@ -188,7 +188,7 @@ __device__ __forceinline__ double pixel_double(const Chunk<BPP, VEC>& c, int j) 
 
 // General q(x) in double (float / 32-bit types): Java semantics, selects instead of branches.
 __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds, int cde) {
-    const double f = family_map(p.family, x, p.k);
+    const double f = family_map(p, x);
     const double a = p.a0 * (f - p.ys);
     double r = floor(a + 0.5);
     r = (a == 0x1.fffffffffffffp-2 || r != r) ? 0.0 : r;
@@ -556,14 +556,7 @@ struct PreparedPlan {
     size_t lut_bytes = 0;
 };
 
-static double host_family_map(int family, double x, double k) {
-    switch (family) {
-    case OMR_FAMILY_POLYNOMIAL: return pow(x, k);
-    case OMR_FAMILY_LOGARITHMIC: return x > 0 ? log(x) : 0.0;
-    case OMR_FAMILY_EXPONENTIAL: return exp(pow(x, k));
-    default: return x;
-    }
-}
+static double host_family_map(const ChanParam& p, double x) { return family_map_code(p.family, x, p.k, p.ws, p.we); }
 
 static int32_t java_d2i_host(double v) {   // Java (int) of a double: NaN -> 0, saturating
     if (v != v) return 0;
@@ -583,7 +576,8 @@ static int32_t ceil_to_i32(double v) {
 // kModeThresh precondition: q is monotone non-decreasing in x.  Below ws it is cdStart, at or
 // above we cdEnd, and inside [ws, we) it is round(a1*round(a0*(f(x) - f(ws))) + cdStart) with
 // a0, a1 >= 0 — monotone once f is increasing and finite on [ws, we]: always for linear; for
-// log / poly / exp when ws > 0 and k > 0 (x^k, ln x, e^(x^k) increase on x > 0).  Noise
+// log / poly / exp when ws > 0 and k > 0 (x^k, ln x, e^(x^k) increase on x > 0); for the
+// window-normalised exp (OMR_SEM_EXP_NORMALIZED) when k > 0 (its input is in [0, 1)).  Noise
 // reduction only widens the two constant ends.  Codes must stay inside one byte without wrap.
 static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixel_type) {
     if (pixel_type != OMR_PIXELS_FLOAT && pixel_type != OMR_PIXELS_INT32 && pixel_type != OMR_PIXELS_UINT32)
@@ -596,12 +590,13 @@ static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixe
     if (p.a0 != p.a0) return true;
     if (!std::isfinite(p.ys) || !std::isfinite(p.a0) || !(p.a0 > 0) || !std::isfinite(p.a1) || p.a1 < 0) return false;
     if (p.nr && !std::isfinite(p.dec)) return false;
-    if (p.family == OMR_FAMILY_LINEAR) return true;
-    const double ye = host_family_map(p.family, p.we, p.k);
+    if (p.family == kFamLinear) return true;
+    const double ye = host_family_map(p, p.we);
     if (!std::isfinite(ye) || !(ye > p.ys)) return false;
-    if (!(p.ws > 0)) return false;
-    if (p.family != OMR_FAMILY_LOGARITHMIC && !(p.k > 0 && std::isfinite(p.k))) return false;
-    return true;
+    const bool is_log = p.family == kFamLog || p.family == kFamLogRaw;
+    if (!is_log && !(p.k > 0 && std::isfinite(p.k))) return false;
+    if (p.family == kFamExpNorm) return true;
+    return p.ws > 0;
 }
 
 static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch,
@@ -631,15 +626,17 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
         ChanParam& p = P.ch[na];
         p.index = c;
         p.family = b.family;
-        p.nr = b.noise_reduction != 0;
+        if (b.family == OMR_FAMILY_LOGARITHMIC && (P.sem & OMR_SEM_LOG_UNGUARDED)) p.family = kFamLogRaw;
+        if (b.family == OMR_FAMILY_EXPONENTIAL && (P.sem & OMR_SEM_EXP_NORMALIZED)) p.family = kFamExpNorm;
+        p.nr = b.noise_reduction != 0 && !(P.sem & OMR_SEM_NOISE_REDUCTION_OFF);
         p.reverse = b.reverse != 0;
         p.has_lut = b.lut != nullptr;
         if (b.lut) std::memcpy(p.lut_rgb, b.lut, 768);
         p.ws = b.input_start;
         p.we = b.input_end;
         p.k = b.coefficient;
-        p.ys = host_family_map(b.family, p.ws, p.k);
-        const double ye = host_family_map(b.family, p.we, p.k);
+        p.ys = host_family_map(p, p.ws);
+        const double ye = host_family_map(p, p.we);
         p.a0 = (double)q->bit_resolution / (ye - p.ys);
         p.a1 = (double)(q->cd_end - q->cd_start) / (double)q->bit_resolution;
         p.dec = (p.we - p.ws) / 10.0;

@@ -41,7 +41,13 @@ PROJECTION_MAX, PROJECTION_MEAN, PROJECTION_SUM = 0, 1, 2
 # OMR_SEM_* switches of the un-vendored upstream semantics (include/omr/omr.h)
 SEM_WINDOW_INT_BOUNDS, SEM_ALPHA_SEPARATE, SEM_GREYSCALE_LUT, SEM_JPEG_CHROMA_DIV2 = 1, 2, 4, 8
 SEM_PROJECTION_ALL_ACTIVE = 16
-SEM_ALL = 0x1F
+SEM_LOG_UNGUARDED, SEM_NOISE_REDUCTION_OFF, SEM_EXP_NORMALIZED, SEM_MASK_PIXEL_FLIP = 32, 64, 128, 256
+SEM_ALL = 0x1FF
+SEM_FLAGS = {"WINDOW_INT_BOUNDS": SEM_WINDOW_INT_BOUNDS, "ALPHA_SEPARATE": SEM_ALPHA_SEPARATE,
+             "GREYSCALE_LUT": SEM_GREYSCALE_LUT, "JPEG_CHROMA_DIV2": SEM_JPEG_CHROMA_DIV2,
+             "PROJECTION_ALL_ACTIVE": SEM_PROJECTION_ALL_ACTIVE, "LOG_UNGUARDED": SEM_LOG_UNGUARDED,
+             "NOISE_REDUCTION_OFF": SEM_NOISE_REDUCTION_OFF, "EXP_NORMALIZED": SEM_EXP_NORMALIZED,
+             "MASK_PIXEL_FLIP": SEM_MASK_PIXEL_FLIP}
 
 PIXEL_TYPE_NAMES = {"int8": PIXELS_INT8, "uint8": PIXELS_UINT8, "int16": PIXELS_INT16,
                     "uint16": PIXELS_UINT16, "int32": PIXELS_INT32, "uint32": PIXELS_UINT32,
@@ -76,7 +82,7 @@ class TileJob(ctypes.Structure):
                 ("quality", ctypes.c_float)]
 
 
-FORMAT_JPEG, FORMAT_PNG, FORMAT_ARGB = 0, 1, 2
+FORMAT_JPEG, FORMAT_PNG, FORMAT_ARGB, FORMAT_TIFF = 0, 1, 2, 3
 
 
 class Region(ctypes.Structure):
@@ -145,6 +151,14 @@ _SIGS = {
     "omr_batcher_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_batcher_stats": (_i32, [_vp, _vp]),
     "omr_batcher_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
+    "omr_pool_create": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
+    "omr_pool_destroy": (None, [_vp]),
+    "omr_pool_size": (_i32, [_vp]),
+    "omr_pool_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "omr_pool_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
+    "omr_pool_device_index": (_i32, [_vp, ctypes.c_uint64]),
+    "omr_pool_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
+    "omr_pool_stats": (_i32, [_vp, _vp, _i32]),
     "omr_render_pixel_buffer_tiles": (_i32, [_vp, _vp, _QD, _CB, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _vp,
                                              _i32]),
     "omr_render_packed_int": (_i32, [_vp, _QD, _CB, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32,

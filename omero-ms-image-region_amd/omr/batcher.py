@@ -1,7 +1,14 @@
-"""Batcher: concurrent tile requests coalesced into GPU batches (omr_batcher_*, SURVEY.md 8(f)
-rank 4).  Worker threads call submit()/wait(); a dispatcher thread in libomr.so groups pending
-jobs by image + settings, renders and JPEG-encodes each group in one batch, and renders
-identical in-flight tiles once (ImageRegionCtx.cacheKey, ImageRegionCtx.java:165-177)."""
+"""Batcher and Pool: concurrent tile requests coalesced into GPU batches.
+
+Batcher (omr_batcher_*): worker threads call submit()/wait(); a dispatcher
+thread in libomr.so groups pending jobs by image + settings, renders and encodes each group in
+one batch, and renders identical in-flight tiles once (ImageRegionCtx.cacheKey,
+ImageRegionCtx.java:165-177).
+
+Pool (omr_pool_*): one batcher per GPU of the node, each job to the least-queued
+one -- the reference's N worker-verticle instances over one worker pool
+(ImageRegionMicroserviceVerticle.java:84-85, :149-165) spread over the node's GPUs.
+"""
 import ctypes
 
 import numpy as np
@@ -10,20 +17,24 @@ from . import _lib
 from ._lib import lib
 from .context import make_bindings
 
-FORMATS = {"jpeg": _lib.FORMAT_JPEG, "png": _lib.FORMAT_PNG, "argb": _lib.FORMAT_ARGB}
+FORMATS = {"jpeg": _lib.FORMAT_JPEG, "png": _lib.FORMAT_PNG, "argb": _lib.FORMAT_ARGB,
+           "tif": _lib.FORMAT_TIFF}
 
 
-class Batcher:
-    def __init__(self, device=0, max_batch=64, max_wait_us=500):
-        h = ctypes.c_void_p()
-        st = lib.omr_batcher_create(device, max_batch, max_wait_us, ctypes.byref(h))
-        if st != _lib.OK:
-            raise _lib.OmrError(st, "omr_batcher_create failed")
-        self.h = h
+def _job(pixbuf, qdef, channels, z, t, x, y, width, height, flip_h, flip_v, fmt, quality, bindings):
+    arr, keep = bindings if bindings is not None else make_bindings(channels)
+    job = _lib.TileJob(pixbuf.h.value if hasattr(pixbuf.h, "value") else pixbuf.h,
+                       ctypes.addressof(qdef), ctypes.addressof(arr), len(channels), z, t, x, y, width, height,
+                       int(flip_h), int(flip_v), FORMATS.get(fmt, 99), float(quality))
+    return job, (arr, keep)
+
+
+class _Queue:
+    _submit = _wait = _set_semantics = _destroy = None
 
     def close(self):
         if self.h:
-            lib.omr_batcher_destroy(self.h)
+            type(self)._destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -40,29 +51,67 @@ class Batcher:
 
     def submit(self, pixbuf, qdef, channels, z, t, x, y, width, height, flip_h=False, flip_v=False,
                fmt="jpeg", quality=0.85, bindings=None):
-        arr, keep = bindings if bindings is not None else make_bindings(channels)
-        job = _lib.TileJob(pixbuf.h.value if hasattr(pixbuf.h, "value") else pixbuf.h,
-                           ctypes.addressof(qdef), ctypes.addressof(arr), len(channels), z, t, x, y, width, height,
-                           int(flip_h), int(flip_v), FORMATS.get(fmt, 99), float(quality))
+        job, keep = _job(pixbuf, qdef, channels, z, t, x, y, width, height, flip_h, flip_v, fmt, quality,
+                         bindings)
         ticket = ctypes.c_uint64()
-        _lib.check(lib.omr_batcher_submit(self.h, ctypes.byref(job), ctypes.byref(ticket)))
+        _lib.check(type(self)._submit(self.h, ctypes.byref(job), ctypes.byref(ticket)))
         return ticket.value
 
     def set_semantics(self, flags):
-        """OMR_SEM_* switches of the batcher's context (before submitting)."""
-        _lib.check(lib.omr_batcher_set_semantics(self.h, int(flags)))
+        """OMR_SEM_* switches for the jobs submitted after this call."""
+        _lib.check(type(self)._set_semantics(self.h, int(flags)))
 
     def wait(self, ticket, cap=1 << 22):
         n = ctypes.c_size_t(0)
         out = np.empty(cap, dtype=np.uint8)
-        st = lib.omr_batcher_wait(self.h, ticket, out.ctypes.data, cap, ctypes.byref(n))
+        st = type(self)._wait(self.h, ticket, out.ctypes.data, cap, ctypes.byref(n))
         if st == _lib.BUFFER_TOO_SMALL:
             out = np.empty(n.value, dtype=np.uint8)
-            st = lib.omr_batcher_wait(self.h, ticket, out.ctypes.data, n.value, ctypes.byref(n))
+            st = type(self)._wait(self.h, ticket, out.ctypes.data, n.value, ctypes.byref(n))
         _lib.check(st)
         return out[:n.value].tobytes()
+
+
+class Batcher(_Queue):
+    _submit = lib.omr_batcher_submit
+    _wait = lib.omr_batcher_wait
+    _set_semantics = lib.omr_batcher_set_semantics
+    _destroy = lib.omr_batcher_destroy
+
+    def __init__(self, device=0, max_batch=64, max_wait_us=500):
+        h = ctypes.c_void_p()
+        st = lib.omr_batcher_create(device, max_batch, max_wait_us, ctypes.byref(h))
+        if st != _lib.OK:
+            raise _lib.OmrError(st, "omr_batcher_create failed")
+        self.h = h
 
     def stats(self):
         s = (ctypes.c_uint64 * 4)()
         _lib.check(lib.omr_batcher_stats(self.h, s))
         return {"jobs": s[0], "batches": s[1], "rendered": s[2], "dedup": s[3]}
+
+
+class Pool(_Queue):
+    _submit = lib.omr_pool_submit
+    _wait = lib.omr_pool_wait
+    _set_semantics = lib.omr_pool_set_semantics
+    _destroy = lib.omr_pool_destroy
+
+    def __init__(self, devices, max_batch=64, max_wait_us=500):
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        st = lib.omr_pool_create(devs, len(devices), max_batch, max_wait_us, ctypes.byref(h))
+        if st != _lib.OK:
+            raise _lib.OmrError(st, "omr_pool_create failed")
+        self.h = h
+        self.devices = list(devices)
+
+    def device_index(self, ticket):
+        return lib.omr_pool_device_index(self.h, ticket)
+
+    def stats(self):
+        n = len(self.devices)
+        s = (ctypes.c_uint64 * (4 * n))()
+        _lib.check(lib.omr_pool_stats(self.h, s, n))
+        return [{"jobs": s[4 * i], "batches": s[4 * i + 1], "rendered": s[4 * i + 2], "dedup": s[4 * i + 3]}
+                for i in range(n)]

@@ -357,7 +357,7 @@ class ShapeMaskRequestHandler:
         col = self.smc.color.encode() if self.smc.color is not None else None
         st = lib.omr_shape_mask_fill_color(int(mask_fill_color is not None),
                                            int(mask_fill_color or 0), col, rgba)
-        if st != _lib.OK:
-            raise RequestError(_lib.INTERNAL, f"IllegalArgumentException: colour '{self.smc.color}'")
+        if st != _lib.OK:   # NPE / IAE inside renderShapeMask: the future fails -> 404 (ShapeMaskVerticle:119-128)
+            raise RequestError(_lib.NOT_FOUND, f"NullPointerException: colour '{self.smc.color}'")
         return self.ctx.render_shape_mask_png(mask_bytes, width, height, list(rgba),
                                               self.smc.flipHorizontal, self.smc.flipVertical)

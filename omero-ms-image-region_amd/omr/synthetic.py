@@ -63,3 +63,34 @@ def torch_tiles_u16(n_tiles, channels, h, w, device, seed=SEED):
             u = img.clamp(0, 65535).to(torch.int32)
             out[t, c] = (u - 65536 * (u >= 32768).to(torch.int32)).to(torch.int16)
     return out
+
+
+C5_LUT = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
+# x^0.5 needs a window start above 0: on the +-normal channel p1 is about -700, where pow(ws, 0.5)
+# is NaN, a0 is NaN and the whole channel would quantize to cdStart (a constant that never
+# exercises the +-1 float bar).  The window start is held at 1.0 there.
+C5_POLY_MIN_START = 1.0
+
+
+def c5_planes(h, w, rng):
+    """C5 (BASELINE configs[4]): 3-channel float32, lognormal(5, 1.5) / normal(0, 300) / lognormal."""
+    return [rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32),
+            rng.normal(0, 300, size=(h, w)).astype(np.float32),
+            rng.lognormal(5, 1.5, size=(h, w)).astype(np.float32)]
+
+
+def c5_channels(planes):
+    """C5 render settings: windows at p1/p99 of each channel; log (reverse) / poly k = 0.5 (window
+    start >= C5_POLY_MIN_START) / poly k = 2 + .lut."""
+    from . import _lib
+    from .renderer import f32
+    chans = []
+    for i, p in enumerate(planes):
+        lo, hi = float(np.percentile(p, 1)), float(np.percentile(p, 99))
+        if i == 1:
+            lo = max(lo, C5_POLY_MIN_START)
+        chans.append({"input_start": f32(lo), "input_end": f32(hi), "rgba": C2_COLORS[i]})
+    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
+    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
+    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=C5_LUT)
+    return chans

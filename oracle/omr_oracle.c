@@ -50,6 +50,17 @@
  *   OMR_SEM_ALPHA_SEPARATE     S7: (int)((int)(c/255f * v) * (alpha/255f)).
  *   OMR_SEM_GREYSCALE_LUT      S8: a .lut channel in greyscale renders (R[v],G[v],B[v]).
  *   OMR_SEM_JPEG_CHROMA_DIV2   S10: chroma base table K2Div2Chrominance = K2.getScaledInstance(0.5f).
+ *   OMR_SEM_PROJECTION_ALL_ACTIVE  (libomr.so glue only; the oracle's glue is the tests' loop)
+ *   OMR_SEM_LOG_UNGUARDED      S2: logarithmic f(x) = log(x) for every x (NaN below 0, -inf at 0).
+ *   OMR_SEM_NOISE_REDUCTION_OFF S4: the noise-reduction flag has no effect.
+ *   OMR_SEM_EXP_NORMALIZED     S2: exponential f(x) = exp(pow((x - start)/(end - start), k)).
+ *   OMR_SEM_MASK_PIXEL_FLIP    S11: shape mask with width % 8 == 0 flips at pixel level instead of
+ *                              reproducing the reference's flip of the still-packed buffer.
+ *   S11[H] shape mask (ShapeMaskRequestHandler.java:165-221): MSB-first bit stream; width % 8 != 0
+ *          unpacks to a byte per pixel first; flip(bytes, w, h) then runs on whatever buffer it is
+ *          given, so with width % 8 == 0 it walks w*h indices of a w*h/8-byte buffer and throws
+ *          ArrayIndexOutOfBoundsException -> the future fails -> 404 (ShapeMaskVerticle.java:
+ *          119-128).  Every exception inside renderShapeMask is that 404 (OMR_NOT_FOUND).
  */
 #include "omr_oracle.h"
 
@@ -87,11 +98,16 @@ uint32_t oracle_get_semantics(void) { return g_sem; }
 
 /* ------------------------------------------------------------------ quantization (S2-S5) */
 
-static double family_map(int family, double x, double k) {
+/* ws / we: the channel window (OMR_SEM_EXP_NORMALIZED maps x to (x - ws)/(we - ws) first). */
+static double family_map(int family, double x, double k, double ws, double we) {
     switch (family) {
     case OMR_FAMILY_POLYNOMIAL: return pow(x, k);
-    case OMR_FAMILY_LOGARITHMIC: return x > 0 ? log(x) : 0.0;
-    case OMR_FAMILY_EXPONENTIAL: return exp(pow(x, k));
+    case OMR_FAMILY_LOGARITHMIC:
+        if (g_sem & OMR_SEM_LOG_UNGUARDED) return log(x);
+        return x > 0 ? log(x) : 0.0;
+    case OMR_FAMILY_EXPONENTIAL:
+        if (g_sem & OMR_SEM_EXP_NORMALIZED) return exp(pow((x - ws) / (we - ws), k));
+        return exp(pow(x, k));
     default: return x;
     }
 }
@@ -104,17 +120,17 @@ static int32_t quantize_impl(double x, const omr_channel_binding* cb, const omr_
     const double hi = int_bounds ? (double)java_d2i(we) : we;
     if (x < lo) return q->cd_start & 0xFF;
     if (x >= hi) return q->cd_end & 0xFF;
-    if (cb->noise_reduction) {
+    if (cb->noise_reduction && !(g_sem & OMR_SEM_NOISE_REDUCTION_OFF)) {
         const double dec = (we - ws) / 10.0;
         if (x < ws + dec) return q->cd_start & 0xFF;
         if (x >= we - dec) return q->cd_end & 0xFF;
     }
     const double k = cb->coefficient;
-    const double ys = family_map(cb->family, ws, k);
-    const double ye = family_map(cb->family, we, k);
+    const double ys = family_map(cb->family, ws, k, ws, we);
+    const double ye = family_map(cb->family, we, k, ws, we);
     const double a0 = (double)q->bit_resolution / (ye - ys);
     const double a1 = (double)(q->cd_end - q->cd_start) / (double)q->bit_resolution;
-    const double v = (double)oracle_java_round(a0 * (family_map(cb->family, x, k) - ys));
+    const double v = (double)oracle_java_round(a0 * (family_map(cb->family, x, k, ws, we) - ys));
     return (int32_t)(oracle_java_round(a1 * v + (double)q->cd_start) & 0xFF);
 }
 
@@ -373,18 +389,29 @@ omr_status oracle_project_stack(const void* stack, int32_t pixel_type, int32_t b
     return OMR_OK;
 }
 
-/* ------------------------------------------------------------------ shape mask */
-/* ShapeMaskRequestHandler.java:165-221: MSB-first bit stream -> 0/1 per pixel -> flip
- * (pixel level; see the deviation note in omr.h). */
+/* ------------------------------------------------------------------ shape mask (S11) */
+/* ShapeMaskRequestHandler.java:165-221 -> 0/1 palette index per pixel.  OMR_NOT_FOUND is every
+ * exception the reference raises there (404 via ShapeMaskVerticle.java:119-128). */
 omr_status oracle_mask_indices(const uint8_t* bits, size_t n_bytes, int32_t width,
                                int32_t height, int32_t flip_h, int32_t flip_v, uint8_t* idx) {
-    if (width <= 0 || height <= 0 || !bits) return OMR_INVALID_ARGUMENT;
+    if (width <= 0 || height <= 0 || !bits) return OMR_NOT_FOUND;      /* IAE / NPE */
     const int64_t n = (int64_t)width * height;
-    if ((int64_t)n_bytes * 8 < n) return OMR_INVALID_ARGUMENT;
+    if (n > INT32_MAX) return OMR_NOT_FOUND;                            /* Java int w*h wraps */
+    if ((int64_t)n_bytes * 8 < n) return OMR_NOT_FOUND;                 /* IOOBE / RasterFormatException */
+    const int flip = flip_h || flip_v;
+    if (width % 8 == 0 && flip && !(g_sem & OMR_SEM_MASK_PIXEL_FLIP)) {
+        /* :179-181 flips the packed buffer: flip(bytes, w, h) reads and writes w*h byte indices */
+        if ((int64_t)n_bytes < n) return OMR_NOT_FOUND;                 /* ArrayIndexOutOfBounds */
+        uint8_t* dest = (uint8_t*)calloc(n_bytes, 1);                   /* new byte[src.length] */
+        oracle_flip_byte(bits, dest, width, height, flip_h, flip_v);
+        for (int64_t i = 0; i < n; ++i) idx[i] = (dest[i >> 3] >> (7 - (i & 7))) & 1;
+        free(dest);
+        return OMR_OK;
+    }
     uint8_t* tmp = (uint8_t*)malloc((size_t)n);
     for (int64_t i = 0; i < n; ++i) tmp[i] = (bits[i >> 3] >> (7 - (i & 7))) & 1;
     omr_status rc = oracle_flip_byte(tmp, idx, width, height, flip_h, flip_v);
-    if (!flip_h && !flip_v) memcpy(idx, tmp, (size_t)n);
+    if (!flip) memcpy(idx, tmp, (size_t)n);
     free(tmp);
     return rc;
 }

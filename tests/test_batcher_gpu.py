@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from omr import Batcher, PixelBuffer, _lib, write_romio
+from omr import Batcher, PixelBuffer, Pool, _lib, write_romio
 from omr.synthetic import c2_channels
 
 pytestmark = pytest.mark.gpu
@@ -118,7 +118,8 @@ def test_every_format_against_the_oracle(romio):
                 ("rgb", 0, 0, 0, False, "argb", 0.9), ("rgb", 1, 256, 256, True, "argb", 0.9),
                 ("rgb", 0, 512, 0, False, "jpeg", 0.9), ("rgb", 1, 768, 512, True, "jpeg", 0.9),
                 ("greyscale", 0, 256, 512, False, "jpeg", 0.5), ("rgb", 1, 0, 256, False, "png", 0.9),
-                ("greyscale", 0, 512, 512, True, "png", 0.9), ("greyscale", 1, 768, 0, False, "argb", 0.9)])]
+                ("greyscale", 0, 512, 512, True, "png", 0.9), ("greyscale", 1, 768, 0, False, "argb", 0.9),
+                ("rgb", 0, 256, 0, True, "tif", 0.9), ("greyscale", 1, 512, 256, False, "tif", 0.9)])]
     ch = c2_channels(3)
     with Batcher(0, max_batch=16, max_wait_us=20000) as b:
         tickets = [b.submit(pb, O.make_qdef(j["model"]), ch, j["z"], 0, j["x"], j["y"], TW, TH, flip_h=j["flip"],
@@ -130,9 +131,139 @@ def test_every_format_against_the_oracle(romio):
             np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(TH, TW), exp)
         elif j["fmt"] == "jpeg":
             assert got == O.encode_jpeg(exp, TW, TH, j["q"]), j
-        else:
-            rgb = np.asarray(Image.open(io.BytesIO(got)).convert("RGB"))
+        else:                                            # PNG / TIFF: decoded pixels
+            im = Image.open(io.BytesIO(got))
+            assert im.format == {"png": "PNG", "tif": "TIFF"}[j["fmt"]]
+            rgb = np.asarray(im.convert("RGB"))
             np.testing.assert_array_equal(rgb, exp.view(np.uint8).reshape(TH, TW, 4)[..., 2::-1])
+    pb.close()
+
+
+def _check_against_oracle(px, jobs, outs, ch_of, flags_of=lambda j: 0):
+    import io
+    from PIL import Image
+    for j, got in zip(jobs, outs):
+        with O.semantics(flags_of(j)):
+            planes = [np.ascontiguousarray(px[0, c, j["z"], j["y"]:j["y"] + TH, j["x"]:j["x"] + TW]).astype(">u2")
+                      for c in range(C)]
+            s, exp = O.render(ch_of(j), planes, _lib.PIXELS_UINT16, TW, TH, big_endian=True, flip_h=j["flip"],
+                              model=j["model"])
+            assert s == 0
+            if j["fmt"] == "argb":
+                np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(TH, TW), exp)
+            elif j["fmt"] == "jpeg":
+                assert got == O.encode_jpeg(exp, TW, TH, j["q"]), j
+            else:
+                rgb = np.asarray(Image.open(io.BytesIO(got)).convert("RGB"))
+                np.testing.assert_array_equal(rgb, exp.view(np.uint8).reshape(TH, TW, 4)[..., 2::-1])
+
+
+def _fractional_channels():
+    ch = c2_channels(3)
+    for c, (s, e) in enumerate([(100.5, 60000.25), (1755.5, 51199.5), (3218.75, 26623.25)]):
+        ch[c]["input_start"], ch[c]["input_end"] = s, e
+    return ch
+
+
+def test_semantics_fixed_at_submit(romio):
+    """Jobs keep the OMR_SEM_* flags they were submitted under: a set_semantics between two
+    submits (while the first jobs are still queued) changes only the later jobs, and jobs with
+    different flags never share a render (the dispatcher used to read the context's
+    flags without a lock, mid-round)."""
+    path, px = romio
+    pb = PixelBuffer(path, X, Y, Z, C, T, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    for c, rgba in enumerate([(255, 129, 100, 101), (17, 200, 255, 250), (90, 90, 90, 3)]):
+        ch[c]["rgba"] = rgba                   # translucent colours: OMR_SEM_ALPHA_SEPARATE changes pixels
+    spots = [(0, 0), (256, 256), (512, 0), (768, 512)]
+    jobs, tickets = [], []
+    with Batcher(0, max_batch=64, max_wait_us=200000) as b:
+        for flags in (0, _lib.SEM_ALPHA_SEPARATE, 0):
+            b.set_semantics(flags)
+            for x, y in spots:
+                j = dict(model="rgb", z=1, x=x, y=y, flip=False, fmt="argb", q=0.9, flags=flags)
+                jobs.append(j)
+                tickets.append(b.submit(pb, O.make_qdef("rgb"), ch, 1, 0, x, y, TW, TH, fmt="argb"))
+        outs = [b.wait(t) for t in tickets]
+        st = b.stats()
+    assert st["dedup"] == len(spots)          # the two flag-0 rounds share; the other flags never do
+    _check_against_oracle(px, jobs, outs, lambda j: ch, lambda j: j["flags"])
+    assert outs[0] != outs[len(spots)]
+    with Batcher(0) as b2, pytest.raises(_lib.OmrError):
+        b2.set_semantics(1 << 20)
+    pb.close()
+
+
+def test_pool_spreads_jobs_over_devices(romio):
+    """omr_pool with two batchers (cuda:{i % device_count}: two contexts on one card when the
+    box has one GPU): concurrent workers, every format, each output against the CPU restatement,
+    and both batchers served jobs."""
+    import torch
+    path, px = romio
+    pb = PixelBuffer(path, X, Y, Z, C, T, _lib.PIXELS_UINT16)
+    devices = [i % torch.cuda.device_count() for i in range(2)]
+    ch = c2_channels(3)
+    rng = np.random.default_rng(17)
+    jobs = [dict(model=["rgb", "greyscale"][i % 2], z=int(rng.integers(0, Z)), x=int(rng.integers(0, X // TW)) * TW,
+                 y=int(rng.integers(0, Y // TH)) * TH, flip=bool(i % 3 == 0), fmt=["jpeg", "argb", "png", "tif"][i % 4],
+                 q=[0.9, 0.6][i % 2]) for i in range(48)]
+    outs, where = [None] * len(jobs), [None] * len(jobs)
+    with Pool(devices, max_batch=16, max_wait_us=3000) as pool:
+        import threading
+
+        def worker(k):
+            for i in range(k, len(jobs), 6):
+                j = jobs[i]
+                t = pool.submit(pb, O.make_qdef(j["model"]), ch, j["z"], 0, j["x"], j["y"], TW, TH,
+                                flip_h=j["flip"], fmt=j["fmt"], quality=j["q"])
+                where[i] = pool.device_index(t)
+                outs[i] = pool.wait(t)
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        stats = pool.stats()
+    assert sorted(set(where)) == [0, 1]
+    assert sum(s["jobs"] for s in stats) == len(jobs) and all(s["jobs"] > 0 for s in stats)
+    _check_against_oracle(px, jobs, outs, lambda j: ch)
+    pb.close()
+
+
+def test_pool_per_tile_errors_and_semantics(tmp_path):
+    import torch
+    rng = np.random.default_rng(6)
+    px = rng.integers(0, 50000, (T, C, 1, 512, 1024), dtype=np.uint16)
+    px[0, 2, 0, 10, 20] = 65000                                     # inside tile (0, 0)
+    path = tmp_path / "pixels"
+    write_romio(path, px, _lib.PIXELS_UINT16)
+    pb = PixelBuffer(path, 1024, 512, 1, C, T, _lib.PIXELS_UINT16)
+    ch = _fractional_channels()
+    for c in ch:
+        c["global_max"] = 60000.0
+    devices = [i % torch.cuda.device_count() for i in range(3)]
+    tiles = [(x, y) for y in (0, 256) for x in (0, 256, 512, 768)]
+    with Pool(devices, max_batch=4, max_wait_us=1000) as pool:
+        pool.set_semantics(_lib.SEM_WINDOW_INT_BOUNDS)
+        tickets = [pool.submit(pb, O.make_qdef("rgb"), ch, 0, 0, x, y, TW, TH, fmt="argb") for x, y in tiles]
+        res = []
+        for t in tickets:
+            try:
+                res.append(pool.wait(t))
+            except _lib.OmrError as e:
+                res.append(e.status)
+        with pytest.raises(_lib.OmrError):
+            pool.submit(pb, O.make_qdef("rgb"), ch, 0, 0, 0, 0, TW, TH, fmt="gif")
+        with pytest.raises(_lib.OmrError):
+            pool.set_semantics(1 << 20)
+    for (x, y), r in zip(tiles, res):
+        if (x, y) == (0, 0):
+            assert r == _lib.QUANTIZATION
+            continue
+        planes = [np.ascontiguousarray(px[0, c, 0, y:y + TH, x:x + TW]).astype(">u2") for c in range(C)]
+        with O.semantics(_lib.SEM_WINDOW_INT_BOUNDS):
+            s, exp = O.render(ch, planes, _lib.PIXELS_UINT16, TW, TH, big_endian=True)
+        np.testing.assert_array_equal(np.frombuffer(r, np.uint32).reshape(TH, TW), exp)
     pb.close()
 
 

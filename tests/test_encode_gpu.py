@@ -125,9 +125,21 @@ def test_shape_mask_reference_dimensions(ctx, w, h):   # testRenderShapeMask{Byt
     assert decode(png).size == (w, h)
 
 
+@pytest.fixture
+def pixel_flip(ctx):
+    """Masks flipped at pixel level also when width % 8 == 0 (OMR_SEM_MASK_PIXEL_FLIP, in both
+    libomr.so and the restatement); the default reproduction of the reference's packed-buffer
+    flip is tested in test_semantics_gpu.py::test_mask_packed_flip."""
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+    with O.semantics(_lib.SEM_MASK_PIXEL_FLIP):
+        yield ctx
+    ctx.set_semantics(0)
+
+
 @pytest.mark.parametrize("w,h", [(8, 2), (4, 4), (64, 33), (37, 21), (1024, 1024)])
 @pytest.mark.parametrize("fh,fv", [(False, False), (True, False), (False, True), (True, True)])
-def test_shape_mask_pixels(ctx, w, h, fh, fv):
+def test_shape_mask_pixels(pixel_flip, w, h, fh, fv):
+    ctx = pixel_flip
     rng = np.random.default_rng(w + 7 * h)
     bits = rng.integers(0, 256, (w * h + 7) // 8, dtype=np.uint8).tobytes()
     rgba = (255, 0, 0, 128)
@@ -198,7 +210,8 @@ def test_png_deflate_decodes_and_compresses(ctx, name):
 
 
 @pytest.mark.parametrize("w,h", [(1024, 1024), (333, 77)])
-def test_shape_mask_png_compresses(ctx, w, h):
+def test_shape_mask_png_compresses(pixel_flip, w, h):
+    ctx = pixel_flip
     yy, xx = np.mgrid[0:h, 0:w]
     m = ((yy - h / 2) / (h / 3)) ** 2 + ((xx - w / 3) / (w / 4)) ** 2 <= 1
     m |= ((yy - h / 4) / (h / 6)) ** 2 + ((xx - 3 * w / 4) / (w / 8)) ** 2 <= 1

@@ -179,7 +179,7 @@ def test_mask_unpack_known_answers(oracle):
     assert idx.tolist() == [[0, 1, 0, 1]] * 4
     st, idx = oracle.mask_indices(bytes([0b10000000, 0b10000000]), 3, 3, fh=True)   # bits 0 and 8
     assert idx.tolist() == [[0, 0, 1], [0, 0, 0], [1, 0, 0]]
-    assert oracle.mask_indices(bytes([0xFF]), 4, 4)[0] == _lib.INVALID_ARGUMENT   # too few bits
+    assert oracle.mask_indices(bytes([0xFF]), 4, 4)[0] == _lib.NOT_FOUND   # too few bits: IOOBE -> 404
 
 
 def test_render_golden_regression(oracle):

@@ -185,6 +185,16 @@ def test_shape_mask_handler(ctx):
     with pytest.raises(RequestError) as e:
         ShapeMaskRequestHandler(ctx, smc).render_shape_mask(None, w, h)
     assert e.value.http_status == 404
+    # an unparsable colour: splitHTMLColor -> null -> NPE inside renderShapeMask -> 404
+    bad = ShapeMaskRequestHandler(ctx, ShapeMaskCtx({"shapeId": "9", "color": "nope"}))
+    with pytest.raises(RequestError) as e:
+        bad.render_shape_mask(bits, w, h)
+    assert e.value.http_status == 404
+    # width % 8 == 0 with a flip: the reference's flip of the packed buffer fails -> 404
+    with pytest.raises(_lib.OmrError) as e:
+        ShapeMaskRequestHandler(ctx, ShapeMaskCtx({"shapeId": "9", "flip": "h"})).render_shape_mask(
+            bytes(2), 8, 2)
+    assert e.value.status == _lib.NOT_FOUND and _lib.HTTP_STATUS[e.value.status] == 404
 
 
 @pytest.mark.parametrize("kw", [

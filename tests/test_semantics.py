@@ -180,3 +180,129 @@ def test_jpeg_psnr_vs_libjpeg_turbo(q, div2):
 def test_ctx_semantics_flags_validated():
     assert _lib.lib.omr_ctx_set_semantics(None, 1) == _lib.INVALID_ARGUMENT
     assert _lib.lib.omr_ctx_get_semantics(None) == 0
+
+
+# ---- round 3: the remaining [L] rules of the SEMANTICS TABLE (S2 log guard, S4 noise reduction,
+# ---- the exponential input normalisation of Appendix C) and the packed-mask flip (S11)
+
+def _grey_ramp(ch, lo, n, flags=0, pt=_lib.PIXELS_UINT16):
+    px = _ramp_u16(lo, n)
+    with O.semantics(flags):
+        st, a = O.render(ch, [px], pt, n, 1, model="greyscale")
+    assert st == 0
+    return dict(zip(range(lo, lo + n), _grey(a[0])))
+
+
+def test_log_guard_switch():
+    """Window 0:100, log family.  Guarded (default): f(0) = 0, so the window maps
+    round(255 ln x / ln 100).  Unguarded: f(0) = log(0) = -inf, a0 = 255/(ln 100 + inf) = 0 and
+    0 * (f(x) + inf) = NaN, Math.round(NaN) = 0 -> every window pixel is cdStart."""
+    import math
+    ch = [_chan(0.0, 100.0, family=_lib.FAMILY_LOGARITHMIC)]
+    a = _grey_ramp(ch, 0, 120)
+    for x in (1, 2, 37, 50, 99):
+        assert a[x] == int(math.floor(255 * math.log(x) / math.log(100) + 0.5)), x
+    assert a[0] == 0 and a[100] == 255
+    b = _grey_ramp(ch, 0, 120, _lib.SEM_LOG_UNGUARDED)
+    assert all(b[x] == 0 for x in range(100)) and all(b[x] == 255 for x in range(100, 120))
+    # a window inside x > 0: the guard never fires and both rules agree
+    ch2 = [_chan(5.0, 90.0, family=_lib.FAMILY_LOGARITHMIC)]
+    assert _grey_ramp(ch2, 0, 120) == _grey_ramp(ch2, 0, 120, _lib.SEM_LOG_UNGUARDED)
+
+
+def test_log_guard_switch_float_negative_pixels():
+    """float pixels below 0 inside a window that starts below 0: guarded f = 0 there; unguarded
+    log(x < 0) = NaN -> round(NaN) = 0 (and f(ws) = NaN makes a0 NaN: the window is cdStart)."""
+    x = np.linspace(-50, 150, 801).astype(np.float32).reshape(1, -1)
+    ch = [{"input_start": -10.0, "input_end": 100.0, "family": _lib.FAMILY_LOGARITHMIC,
+           "rgba": (255, 255, 255, 255)}]
+    st, a = O.render(ch, [x], _lib.PIXELS_FLOAT, x.shape[1], 1, model="greyscale")
+    with O.semantics(_lib.SEM_LOG_UNGUARDED):
+        st2, b = O.render(ch, [x], _lib.PIXELS_FLOAT, x.shape[1], 1, model="greyscale")
+    ga, gb = _grey(a[0]), _grey(b[0])
+    inside = (x[0] >= -10) & (x[0] < 100)
+    assert (ga[inside] > 0).any() and (gb[inside] == 0).all()
+    assert (ga[x[0] >= 100] == 255).all() and (gb[x[0] >= 100] == 255).all()
+
+
+def test_noise_reduction_switch():
+    """Window 0:1000 with noise reduction: the default clips x < 100 and x >= 900 (the deciles);
+    OMR_SEM_NOISE_REDUCTION_OFF renders the plain linear ramp round(0.255 x)."""
+    ch = [_chan(0.0, 1000.0, noise_reduction=True)]
+    a = _grey_ramp(ch, 0, 1100)
+    assert a[50] == 0 and a[99] == 0 and a[100] == 26 and a[899] == 229 and a[900] == 255
+    b = _grey_ramp(ch, 0, 1100, _lib.SEM_NOISE_REDUCTION_OFF)
+    assert all(b[x] == int(np.floor(0.255 * x + 0.5)) for x in range(1000))
+    assert b[50] == 13 and b[950] == 242
+    plain = _grey_ramp([_chan(0.0, 1000.0)], 0, 1100)
+    assert b == plain
+
+
+def test_exp_normalized_switch():
+    """Window 100:200, exponential k = 1.  Default exp(x): exp(200)/exp(150) ~ 5e21, so the window
+    is cdStart up to x = 193 and rises only in its last pixels.  Normalised: f = exp((x-100)/100),
+    f(ws) = 1, f(we) = e, q = round(255 (exp(t) - 1)/(e - 1))."""
+    import math
+    ch = [_chan(100.0, 200.0, family=_lib.FAMILY_EXPONENTIAL, coefficient=1.0)]
+    a = _grey_ramp(ch, 90, 120)
+    assert all(a[x] == 0 for x in range(90, 194))
+    for x in range(194, 200):
+        assert a[x] == int(math.floor(255 / (math.exp(200) - math.exp(100)) * (math.exp(x) - math.exp(100)) + 0.5))
+    b = _grey_ramp(ch, 90, 120, _lib.SEM_EXP_NORMALIZED)
+    for x in range(100, 200):
+        t = (x - 100) / 100.0
+        assert b[x] == int(math.floor(255.0 / (math.e - 1.0) * (math.exp(t) - 1.0) + 0.5)), x
+    assert b[150] == 96 and b[99] == 0 and b[200] == 255
+
+
+def test_exp_default_overflows_on_16bit_windows():
+    """exp(65535) is +inf: with the default map a full 16-bit window renders cdStart below its end;
+    the normalised map renders a curve."""
+    ch = [_chan(0.0, 65535.0, family=_lib.FAMILY_EXPONENTIAL, coefficient=1.0)]
+    a = _grey_ramp(ch, 0, 65536)
+    assert all(a[x] == 0 for x in range(0, 65535, 97)) and a[65535] == 255
+    b = _grey_ramp(ch, 0, 65536, _lib.SEM_EXP_NORMALIZED)
+    assert len({b[x] for x in range(0, 65536, 7)}) > 200
+
+
+@pytest.mark.parametrize("fh,fv", [(True, False), (False, True), (True, True)])
+def test_mask_packed_flip_reproduced(fh, fv):
+    """width % 8 == 0 with a flip: the reference flips the packed w*h/8-byte buffer as w*h bytes
+    (ArrayIndexOutOfBoundsException -> 404); OMR_SEM_MASK_PIXEL_FLIP flips pixels."""
+    w, h = 16, 3
+    rng = np.random.default_rng(7)
+    bits = rng.integers(0, 256, w * h // 8, dtype=np.uint8).tobytes()
+    st, _ = O.mask_indices(bits, w, h, fh, fv)
+    assert st == _lib.NOT_FOUND
+    with O.semantics(_lib.SEM_MASK_PIXEL_FLIP):
+        st, idx = O.mask_indices(bits, w, h, fh, fv)
+    assert st == 0
+    unpacked = np.unpackbits(np.frombuffer(bits, np.uint8)).reshape(h, w)
+    exp = unpacked[::-1 if fv else 1, ::-1 if fh else 1]
+    np.testing.assert_array_equal(idx, exp)
+    # a buffer of >= w*h bytes: the byte flip succeeds and the first w*h/8 flipped bytes render
+    big = rng.integers(0, 256, w * h + 5, dtype=np.uint8)
+    st, idx = O.mask_indices(big.tobytes(), w, h, fh, fv)
+    assert st == 0
+    dest = np.zeros_like(big)
+    dest[: w * h] = big[: w * h].reshape(h, w)[::-1 if fv else 1, ::-1 if fh else 1].reshape(-1)
+    np.testing.assert_array_equal(idx, np.unpackbits(dest[: w * h // 8]).reshape(h, w))
+    # no flip, or width % 8 != 0: the switch changes nothing
+    for args in ((w, h, False, False), (12, 4, fh, fv)):
+        st1, i1 = O.mask_indices(bits if args[0] == w else bits[:6], *args)
+        with O.semantics(_lib.SEM_MASK_PIXEL_FLIP):
+            st2, i2 = O.mask_indices(bits if args[0] == w else bits[:6], *args)
+        assert st1 == st2 == 0
+        np.testing.assert_array_equal(i1, i2)
+
+
+def test_mask_reference_failures_are_404():
+    """Exceptions inside renderShapeMask fail the future -> ShapeMaskVerticle answers 404."""
+    assert O.mask_indices(bytes([0xFF]), 4, 4)[0] == _lib.NOT_FOUND      # IndexOutOfBounds (bits)
+    assert O.mask_indices(bytes([0xFF]), 0, 4)[0] == _lib.NOT_FOUND      # zero size
+    assert O.mask_indices(b"", 8, 1)[0] == _lib.NOT_FOUND                # null / empty mask
+
+
+def test_semantics_flag_set_complete():
+    assert _lib.SEM_ALL == sum(_lib.SEM_FLAGS.values()) == 0x1FF
+    assert len(set(_lib.SEM_FLAGS.values())) == 9

@@ -173,3 +173,263 @@ def test_semantics_reject_unknown_flags(sem_ctx):
         sem_ctx.set_semantics(1 << 20)
     sem_ctx.set_semantics(_lib.SEM_ALL)
     assert sem_ctx.semantics == _lib.SEM_ALL
+
+
+# ---- round 3: S2 log guard, S4 noise reduction, exp input normalisation, packed mask flip ----
+# Every kernel path the switch can reach runs against the restatement under the same switch:
+#   K1+K2 one-tile launch (K2 builds its tables in LDS), the full K2 batch launch (K1 tables,
+#   2 chunks per lane), the fused render -> JPEG (F1; integer types: byte-identical to the unfused
+#   GPU render + JPEG, and to the restatement's JPEG when the family is linear), and the
+#   projection glue (K3 + K2 and K3R; integer types), plus the float threshold / Eval modes.
+# Transcendental families are held to +-1 code value per component (device log/pow/exp vs glibc,
+# DESIGN.md §2); linear ones are bit-exact.
+
+PRIMARY = [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255)]
+
+
+def _assert_close(got, exp, tol):
+    if tol == 0:
+        np.testing.assert_array_equal(got, exp)
+        return
+    for sh in (16, 8, 0):
+        d = np.abs(((got >> sh) & 0xFF).astype(int) - ((exp >> sh) & 0xFF).astype(int))
+        assert d.max() <= tol, f"component {sh}: max diff {d.max()}"
+
+
+def _k3r_context():
+    import os
+    import omr
+    os.environ["OMR_K3R"] = "1"
+    try:
+        return omr.Context(0)
+    finally:
+        del os.environ["OMR_K3R"]
+
+
+def _every_path(ctx, flags, chans, planes, pt, w, h, tol, k3r_ctx=None, jpeg=True):
+    """Renders `planes` (numpy, native order) under `flags` through every kernel path and checks
+    each against the restatement.  Returns the one-tile ARGB."""
+    import torch
+    ctx.set_semantics(flags)
+    q = make_qdef("rgb")
+    with O.semantics(flags):
+        st, exp = O.render(chans, planes, pt, w, h, qdef=q)
+    assert st == 0
+    got = ctx.render_packed_int(q, chans, planes, pt, w, h)                      # one-tile launch
+    _assert_close(got, exp, tol)
+    # full batch launch: enough tiles that K2 leaves its small-launch instantiation
+    nb = max(2, -(-4_300_000 // (w * h)))
+    plane_bytes = planes[0].nbytes
+    one = np.concatenate([p.reshape(-1).view(np.uint8) for p in planes])
+    data = torch.from_numpy(np.tile(one, nb)).to("cuda")
+    out = torch.empty((nb, h, w), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.render_batch_strided_device(q, chans, data, len(planes) * plane_bytes, plane_bytes, nb, pt, w, h, out)
+    ctx.synchronize()
+    allg = out.cpu().numpy().view(np.uint32)
+    for t in (0, nb - 1):
+        _assert_close(allg[t], exp, tol)
+    assert (allg == allg[0]).all()
+    if jpeg and _lib.BYTES_PER_PIXEL[pt] <= 2 and w % 16 == 0 and h % 16 == 0:
+        n = 3
+        cap = n * (lib_jpeg_max(w, h))
+        d_out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+        offs = torch.empty(n, dtype=torch.int64, device="cuda")
+        lens = torch.empty(n, dtype=torch.int32, device="cuda")
+        ctx.render_jpeg_batch_strided_device(q, chans, data, len(planes) * plane_bytes, plane_bytes, n, pt, w, h,
+                                             0.9, d_out, offs, lens)
+        ctx.synchronize()
+        fused = _files(d_out, offs, lens, n)
+        unfused = ctx.encode_jpeg_batch(out[:n].contiguous(), n, w, h, 0.9)
+        assert fused == unfused
+        if tol == 0:
+            with O.semantics(flags):
+                assert fused[0] == O.encode_jpeg(exp, w, h, 0.9)
+    ctx.set_semantics(0)
+    return got
+
+
+def lib_jpeg_max(w, h):
+    return int(_lib.lib.omr_jpeg_max_bytes(w, h))
+
+
+def _files(d_out, offs, lens, n):
+    b = d_out.cpu().numpy()
+    o = offs.cpu().numpy()
+    ln = lens.cpu().numpy().view(np.uint32)
+    return [b[o[i]:o[i] + ln[i]].tobytes() for i in range(n)]
+
+
+def _glue_paths(ctx, k3r, flags, chans, stacks, pt, w, h, z, tol):
+    import torch
+    for c in (ctx, k3r):
+        c.set_semantics(flags)
+        q = make_qdef("rgb")
+        out = torch.empty((h, w), dtype=torch.int32, device="cuda")
+        devs = [torch.from_numpy(s.reshape(-1).view(np.uint8).copy()).to("cuda") for s in stacks]
+        torch.cuda.synchronize()
+        c.render_projected_device(q, chans, devs, pt, w, h, z, _lib.PROJECTION_MAX, 0, z - 1, out)
+        c.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        planes = []
+        for s in stacks:
+            st, p = O.project(s, pt, w, h, z, _lib.PROJECTION_MAX, 0, z - 1)
+            planes.append(p)
+        with O.semantics(flags):
+            st, exp = O.render(chans, planes, pt, w, h, qdef=q)
+        _assert_close(got, exp, tol)
+        c.set_semantics(0)
+
+
+@pytest.fixture(scope="module")
+def k3r_ctx():
+    c = _k3r_context()
+    yield c
+    c.close()
+
+
+def _u16_ramps(h, w, seed, hi=65536):
+    rng = np.random.default_rng(seed)
+    planes = [rng.integers(0, hi, (h, w)).astype(np.uint16) for _ in range(3)]
+    planes[0].reshape(-1)[:4096] = np.arange(4096)
+    return planes
+
+
+def test_log_unguarded_integer_paths(sem_ctx, k3r_ctx):
+    h, w = 64, 256
+    planes = _u16_ramps(h, w, 31)
+    chans = [{"input_start": 0.0, "input_end": 5000.0, "global_min": 0.0, "global_max": 65535.0,
+              "family": _lib.FAMILY_LOGARITHMIC, "rgba": PRIMARY[0]},
+             {"input_start": 300.0, "input_end": 40000.0, "global_min": 0.0, "global_max": 65535.0,
+              "family": _lib.FAMILY_LOGARITHMIC, "rgba": PRIMARY[1]},
+             {"input_start": 0.0, "input_end": 65535.0, "global_min": 0.0, "global_max": 65535.0,
+              "rgba": PRIMARY[2]}]
+    a = _every_path(sem_ctx, 0, chans, planes, _lib.PIXELS_UINT16, w, h, tol=1)
+    b = _every_path(sem_ctx, _lib.SEM_LOG_UNGUARDED, chans, planes, _lib.PIXELS_UINT16, w, h, tol=1)
+    assert (((a >> 16) & 0xFF) != ((b >> 16) & 0xFF)).any()      # window from 0: -inf start
+    np.testing.assert_array_equal((a >> 8) & 0xFF, (b >> 8) & 0xFF)  # window inside x > 0: unchanged
+    i16 = [(p.astype(np.int32) - 32768).astype(np.int16) for p in planes]
+    ci = [dict(c, global_min=-32768.0, global_max=32767.0) for c in chans]
+    ci[0].update(input_start=-100.0, input_end=3000.0)
+    _every_path(sem_ctx, _lib.SEM_LOG_UNGUARDED, ci, i16, _lib.PIXELS_INT16, w, h, tol=1)
+    u8 = [(p & 0xFF).astype(np.uint8) for p in planes]
+    c8 = [dict(c, input_start=0.0, input_end=200.0, global_max=255.0) for c in chans]
+    _every_path(sem_ctx, _lib.SEM_LOG_UNGUARDED, c8, u8, _lib.PIXELS_UINT8, w, h, tol=1)
+    z = 5
+    stacks = [np.stack([np.roll(p, k) for k in range(z)]) for p in planes]
+    _glue_paths(sem_ctx, k3r_ctx, _lib.SEM_LOG_UNGUARDED, chans, stacks, _lib.PIXELS_UINT16, w, h, z, tol=1)
+
+
+def test_log_unguarded_float_paths(sem_ctx):
+    """Threshold mode (window above 0) and Eval mode (window from / below 0) under the switch."""
+    h, w = 64, 256
+    rng = np.random.default_rng(5)
+    planes = [rng.uniform(-50, 6000, (h, w)).astype(np.float32) for _ in range(3)]
+    planes[0].reshape(-1)[:8] = [0.0, -0.0, -1.0, 1e-30, np.inf, -np.inf, np.nan, 1.0]
+    chans = [{"input_start": -10.0, "input_end": 100.0, "family": _lib.FAMILY_LOGARITHMIC, "rgba": PRIMARY[0]},
+             {"input_start": 1.5, "input_end": 5000.0, "family": _lib.FAMILY_LOGARITHMIC, "rgba": PRIMARY[1]},
+             {"input_start": 0.0, "input_end": 3000.0, "family": _lib.FAMILY_LOGARITHMIC, "rgba": PRIMARY[2]}]
+    a = _every_path(sem_ctx, 0, chans, planes, _lib.PIXELS_FLOAT, w, h, tol=1)
+    b = _every_path(sem_ctx, _lib.SEM_LOG_UNGUARDED, chans, planes, _lib.PIXELS_FLOAT, w, h, tol=1)
+    assert (a != b).any()
+
+
+@pytest.mark.parametrize("pt", [_lib.PIXELS_UINT16, _lib.PIXELS_INT16, _lib.PIXELS_UINT8, _lib.PIXELS_FLOAT])
+def test_noise_reduction_off_paths(sem_ctx, k3r_ctx, pt):
+    """Linear family with noise reduction: bit-exact on every path, with and without the switch."""
+    h, w = 64, 256
+    planes = _u16_ramps(h, w, 44)
+    if pt == _lib.PIXELS_INT16:
+        planes = [(p.astype(np.int32) - 32768).astype(np.int16) for p in planes]
+        lo, hi = -32768.0, 32767.0
+    elif pt == _lib.PIXELS_UINT8:
+        planes = [(p & 0xFF).astype(np.uint8) for p in planes]
+        lo, hi = 0.0, 255.0
+    elif pt == _lib.PIXELS_FLOAT:
+        planes = [p.astype(np.float32) * np.float32(0.37) for p in planes]
+        lo, hi = 0.0, 0.0
+    else:
+        lo, hi = 0.0, 65535.0
+    span = (hi - lo) if hi > lo else 24000.0
+    chans = [{"input_start": lo + 0.1 * span, "input_end": lo + 0.6 * span, "global_min": lo, "global_max": hi,
+              "noise_reduction": True, "rgba": PRIMARY[c]} for c in range(3)]
+    chans[2]["noise_reduction"] = False
+    chans[1]["reverse"] = True
+    a = _every_path(sem_ctx, 0, chans, planes, pt, w, h, tol=0)
+    b = _every_path(sem_ctx, _lib.SEM_NOISE_REDUCTION_OFF, chans, planes, pt, w, h, tol=0)
+    assert (a != b).any()
+    np.testing.assert_array_equal(a & 0xFF, b & 0xFF)    # channel without noise reduction unchanged
+    if pt != _lib.PIXELS_FLOAT:
+        z = 4
+        stacks = [np.stack([np.roll(p, 3 * k) for k in range(z)]) for p in planes]
+        _glue_paths(sem_ctx, k3r_ctx, _lib.SEM_NOISE_REDUCTION_OFF, chans, stacks, pt, w, h, z, tol=0)
+
+
+@pytest.mark.parametrize("pt", [_lib.PIXELS_UINT16, _lib.PIXELS_FLOAT, _lib.PIXELS_UINT32])
+def test_exp_normalized_paths(sem_ctx, k3r_ctx, pt):
+    h, w = 64, 256
+    planes = _u16_ramps(h, w, 71)
+    if pt == _lib.PIXELS_FLOAT:
+        planes = [p.astype(np.float32) / np.float32(600.0) - np.float32(5.0) for p in planes]
+        wins = [(-5.0, 50.0), (1.0, 20.0), (0.0, 100.0)]
+    elif pt == _lib.PIXELS_UINT32:
+        planes = [p.astype(np.uint32) * np.uint32(3) for p in planes]
+        wins = [(0.0, 196605.0), (1000.0, 9000.0), (50.0, 120000.0)]
+    else:
+        wins = [(0.0, 65535.0), (1000.0, 2000.0), (100.0, 30000.0)]
+    ks = [1.0, 0.5, 2.0]
+    chans = [{"input_start": s, "input_end": e, "global_min": 0.0, "global_max": 65535.0 if pt == _lib.PIXELS_UINT16 else 0.0,
+              "family": _lib.FAMILY_EXPONENTIAL, "coefficient": k, "rgba": PRIMARY[c]}
+             for c, ((s, e), k) in enumerate(zip(wins, ks))]
+    a = _every_path(sem_ctx, 0, chans, planes, pt, w, h, tol=1)
+    b = _every_path(sem_ctx, _lib.SEM_EXP_NORMALIZED, chans, planes, pt, w, h, tol=1)
+    assert len(np.unique((b >> 16) & 0xFF)) > 100 and (a != b).any()
+    if pt == _lib.PIXELS_UINT16:
+        z = 3
+        stacks = [np.stack([np.roll(p, 5 * k) for k in range(z)]) for p in planes]
+        _glue_paths(sem_ctx, k3r_ctx, _lib.SEM_EXP_NORMALIZED, chans, stacks, pt, w, h, z, tol=1)
+
+
+def _mask_png_indices(png):
+    from PIL import Image
+    im = Image.open(io.BytesIO(png))
+    return (np.asarray(im.convert("RGBA"))[..., 3] > 0).astype(np.uint8)
+
+
+@pytest.mark.parametrize("w,h", [(8, 2), (64, 33), (1024, 1024), (37, 21)])
+@pytest.mark.parametrize("fh,fv", [(True, False), (False, True), (True, True)])
+def test_mask_packed_flip(sem_ctx, w, h, fh, fv):
+    """Default: the reference's packed-buffer flip (404 for a w*h/8-byte mask when w % 8 == 0);
+    OMR_SEM_MASK_PIXEL_FLIP: pixel flip.  Width % 8 != 0 unpacks first: both settings agree."""
+    rng = np.random.default_rng(w * 31 + h)
+    bits = rng.integers(0, 256, (w * h + 7) // 8, dtype=np.uint8).tobytes()
+    rgba = (255, 0, 0, 255)
+    for flags in (0, _lib.SEM_MASK_PIXEL_FLIP):
+        sem_ctx.set_semantics(flags)
+        with O.semantics(flags):
+            st, idx = O.mask_indices(bits, w, h, fh, fv)
+        if st:
+            assert st == _lib.NOT_FOUND and w % 8 == 0 and flags == 0
+            with pytest.raises(_lib.OmrError) as e:
+                sem_ctx.render_shape_mask_png(bits, w, h, rgba, fh, fv)
+            assert e.value.status == _lib.NOT_FOUND
+            continue
+        png = sem_ctx.render_shape_mask_png(bits, w, h, rgba, fh, fv)
+        np.testing.assert_array_equal(_mask_png_indices(png), idx)
+    if w % 8 == 0 and w * h <= 4096:
+        # a mask array of >= w*h bytes: the reference's byte flip succeeds and its first w*h/8
+        # bytes render as packed bits
+        big = rng.integers(0, 256, w * h + 3, dtype=np.uint8).tobytes()
+        sem_ctx.set_semantics(0)
+        st, idx = O.mask_indices(big, w, h, fh, fv)
+        assert st == 0
+        png = sem_ctx.render_shape_mask_png(big, w, h, rgba, fh, fv)
+        np.testing.assert_array_equal(_mask_png_indices(png), idx)
+    sem_ctx.set_semantics(0)
+
+
+def test_mask_reference_failures_are_not_found(sem_ctx):
+    for bits, w, h in ((bytes([0xFF]), 4, 4), (bytes([0xFF]), 0, 4), (b"", 8, 1)):
+        with pytest.raises(_lib.OmrError) as e:
+            sem_ctx.render_shape_mask_png(bits, w, h, (1, 2, 3, 4))
+        assert e.value.status == _lib.NOT_FOUND

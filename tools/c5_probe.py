@@ -16,22 +16,12 @@ def main():
     import omr
     from omr import _lib
     from omr.context import make_bindings, make_qdef
-    from omr.renderer import f32
-    from omr.synthetic import C2_COLORS
+    from omr.synthetic import c5_channels, c5_planes
     T, uniq = 1024, 4
     B = int(os.environ.get("C5_TILES", "32"))
     rng = np.random.default_rng(20261015 + 5)
-    host = np.stack([np.stack([rng.lognormal(5, 1.5, (T, T)).astype(np.float32),
-                               rng.normal(0, 300, (T, T)).astype(np.float32),
-                               rng.lognormal(5, 1.5, (T, T)).astype(np.float32)]) for _ in range(uniq)])
-    lut = np.concatenate([np.arange(256), np.arange(256) // 2, 255 - np.arange(256)]).astype(np.uint8)
-    chans = []
-    for c in range(3):
-        lo, hi = np.percentile(host[0, c], 1), np.percentile(host[0, c], 99)
-        chans.append({"input_start": f32(lo), "input_end": f32(hi), "rgba": C2_COLORS[c]})
-    chans[0].update(family=_lib.FAMILY_LOGARITHMIC, reverse=True)
-    chans[1].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5)
-    chans[2].update(family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0, lut=lut)
+    host = np.stack([np.stack(c5_planes(T, T, rng)) for _ in range(uniq)])
+    chans = c5_channels(list(host[0]))       # the bench's C5 settings
     dev = torch.device("cuda", 0)
     src = torch.from_numpy(np.ascontiguousarray(host.astype(">f4")).view(np.uint8)).to(dev)
     data = torch.empty((B, 3 * T * T * 4), dtype=torch.uint8, device=dev)

@@ -45,6 +45,7 @@ def main():
         m |= ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1
     bits = np.packbits(m.reshape(-1)).tobytes()
     mlat = []
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)     # flip hv of a 1024-wide mask: pixel flip
     for i in range(43):
         t0 = time.perf_counter()
         mpng = ctx.render_shape_mask_png(bits, T, T, (255, 0, 0, 128), flip_h=True, flip_v=True)
