@@ -3,7 +3,9 @@ package com.glencoesoftware.omero.ms.image.region.gpu;
 /**
  * JNI facade over libomr.so (jni/omr_jni.c, include/omr/omr.h).  One context per Vert.x worker
  * thread (contexts are not thread-safe; distinct contexts may run concurrently), or one shared
- * batcher per GPU.  Every native method throws {@link OmrException} on failure.
+ * batcher per GPU, or one pool over the node's GPUs for every worker.  Every native method throws
+ * {@link OmrException} on failure; array arguments are copied in and out (no critical region is
+ * held across a GPU call), and a short or null array is INVALID_ARGUMENT.
  *
  * Paths are relative to src/main/java/com/glencoesoftware/omero/ms/image/region/ of the reference.
  * Not compiled in this repository's image (no JDK); the C side it binds is built and tested here.
@@ -19,10 +21,11 @@ public final class OmrNative implements AutoCloseable {
     public static final int FAMILY_LINEAR = 0, FAMILY_POLYNOMIAL = 1, FAMILY_LOGARITHMIC = 2,
             FAMILY_EXPONENTIAL = 3;
     public static final int MODEL_GREYSCALE = 0, MODEL_RGB = 1;
-    public static final int FORMAT_JPEG = 0, FORMAT_PNG = 1, FORMAT_ARGB = 2;
+    public static final int FORMAT_JPEG = 0, FORMAT_PNG = 1, FORMAT_ARGB = 2, FORMAT_TIFF = 3;
     /** OMR_SEM_* switches of the un-vendored upstream semantics. */
     public static final int SEM_WINDOW_INT_BOUNDS = 1, SEM_ALPHA_SEPARATE = 2, SEM_GREYSCALE_LUT = 4,
-            SEM_JPEG_CHROMA_DIV2 = 8, SEM_PROJECTION_ALL_ACTIVE = 16;
+            SEM_JPEG_CHROMA_DIV2 = 8, SEM_PROJECTION_ALL_ACTIVE = 16, SEM_LOG_UNGUARDED = 32,
+            SEM_NOISE_REDUCTION_OFF = 64, SEM_EXP_NORMALIZED = 128, SEM_MASK_PIXEL_FLIP = 256;
     /** doubles per channel in the packed settings array. */
     public static final int CHANNEL_FIELDS = 13;
 
@@ -100,6 +103,18 @@ public final class OmrNative implements AutoCloseable {
     public static native long batcherSubmit(long batcher, long pixelBuffer, int model, double[] settings,
                                             byte[][] luts, int z, int t, int x, int y, int width, int height,
                                             boolean flipH, boolean flipV, int format, float quality);
-    /** Blocks until the job is done; the encoded tile (JPEG / PNG) or the packed ARGB bytes. */
+    /** Blocks until the job is done; the encoded tile (JPEG / PNG / TIFF) or the packed ARGB bytes. */
     public static native byte[] batcherWait(long batcher, long ticket);
+    /** OMR_SEM_* flags for jobs submitted after this call. */
+    public static native void batcherSetSemantics(long batcher, int flags);
+
+    // ---- node pool: one batcher per GPU (ImageRegionMicroserviceVerticle.java:84-85, :149-165) -------
+    /** devices[i]: the GPU ordinal of batcher i (may repeat); jobs go to the least-queued batcher. */
+    public static native long poolCreate(int[] devices, int maxBatch, int maxWaitUs);
+    public static native void poolDestroy(long pool);
+    public static native void poolSetSemantics(long pool, int flags);
+    public static native long poolSubmit(long pool, long pixelBuffer, int model, double[] settings,
+                                         byte[][] luts, int z, int t, int x, int y, int width, int height,
+                                         boolean flipH, boolean flipV, int format, float quality);
+    public static native byte[] poolWait(long pool, long ticket);
 }
