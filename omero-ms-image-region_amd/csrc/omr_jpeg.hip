@@ -768,9 +768,13 @@ __device__ __forceinline__ void load_pair(const uint32_t* img, int W, int x, int
     }
 }
 
-// Block stride of the per-wave LDS MCU buffer: 73 words makes both FDCT passes (48 lanes on
-// rows of stride 8, then on columns) hit 48 distinct banks; 64 gave 6-way conflicts.
-constexpr int kBS = 73;
+// Per-wave LDS MCU buffer: block b, row r, column c at b*kBS + r*kRS + c.  ds_read_b32 /
+// ds_write_b32 bank = word mod 32 per 32-lane half (MI355X_MICROARCH.md §LDS): a row stride of 9
+// and a block stride of 72 (8 mod 32) put the 32 rows (pass 0) and the 32 columns (pass 1) of
+// four blocks on 32 distinct banks.  The round-2 layout (rows of 8, blocks of 73) was laid out
+// for 64 banks: every pass-0 access was 2-way (rows r and r+4), 41 % of B1's LDS-active cycles
+// were conflicts (profiles/r02/jpeg_pmc_c2_r02h.txt).
+constexpr int kBS = 72, kRS = 9;
 
 // B1's pixel source: rendered ARGB tiles in HBM.  issue(m) loads the four pixels this lane
 // needs for MCU m (the next MCU's loads are in flight while the current one is transformed);
@@ -953,13 +957,16 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
     const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
     const int m0 = (blockIdx.x * 4 + wv) * A.mpw;
     const int m1 = min(m0 + A.mpw, A.n_mcu);
-    auto fetch = [&](int m) {
-        const int mx = m % A.mcux, my = m / A.mcux;
-        src.issue(mx * 16 + 2 * cx, my * 16 + 2 * cy);
+    const int nat_off = (nat >> 3) * kRS + (nat & 7);   // zig-zag position `lane` in the block
+    // MCU coordinates advance incrementally (no per-MCU division by the MCU row length)
+    int mx = m0 % A.mcux, my = m0 / A.mcux;
+    int nx = mx, ny = my;                          // the prefetched MCU
+    auto fetch = [&]() {
+        src.issue(nx * 16 + 2 * cx, ny * 16 + 2 * cy);
+        if (++nx == A.mcux) { nx = 0; ++ny; }
     };
-    if (m0 < m1) fetch(m0);
+    if (m0 < m1) fetch();
     for (int m = m0; m < m1; ++m) {   // wave-uniform loop
-        const int mx = m % A.mcux, my = m / A.mcux;
         // Grey MCU (every pixel r == g == b, e.g. the greyscale model's output): IJG's Y is then
         // (65536 v + 32768) >> 16 = v exactly and Cb = Cr = 128, so both chroma blocks are zero —
         // the colour transform, their FDCT and their quantisation are skipped.  Wave-uniform; the
@@ -969,24 +976,24 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
             const int x0 = mx * 16 + 2 * cx;
             Rgb px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
             src.take(px);
-            if (m + 1 < m1) fetch(m + 1);
+            if (m + 1 < m1) fetch();
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             auto isg = [](const Rgb& p) { return p.r == p.g && p.g == p.b; };
             grey = __ballot(!(isg(px[0]) && isg(px[1]) && isg(px[2]) && isg(px[3])) || cyg >= chv) == 0;
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
-            const int o = ((2 * cy) & 7) * 8 + ((2 * cx) & 7);
+            const int o = blk * kBS + ((2 * cy) & 7) * kRS + ((2 * cx) & 7);
             if (grey) {
-                S[blk * kBS + o] = px[0].b - 128;
-                S[blk * kBS + o + 1] = px[1].b - 128;
-                S[blk * kBS + o + 8] = px[2].b - 128;
-                S[blk * kBS + o + 9] = px[3].b - 128;
+                S[o] = px[0].b - 128;
+                S[o + 1] = px[1].b - 128;
+                S[o + kRS] = px[2].b - 128;
+                S[o + kRS + 1] = px[3].b - 128;
             } else {
-            ycc(px[0], y, cb0, cr0); S[blk * kBS + o] = y - 128;
-            ycc(px[1], y, cb1, cr1); S[blk * kBS + o + 1] = y - 128;
-            ycc(px[2], y, cb2, cr2); S[blk * kBS + o + 8] = y - 128;
-            ycc(px[3], y, cb3, cr3); S[blk * kBS + o + 9] = y - 128;
+            ycc(px[0], y, cb0, cr0); S[o] = y - 128;
+            ycc(px[1], y, cb1, cr1); S[o + 1] = y - 128;
+            ycc(px[2], y, cb2, cr2); S[o + kRS] = y - 128;
+            ycc(px[3], y, cb3, cr3); S[o + kRS + 1] = y - 128;
             if (cyg >= chv) {
                 const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
                 const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
@@ -994,19 +1001,19 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
                 ycc(src.at(xa, r1), y, cb2, cr2); ycc(src.at(xb, r1), y, cb3, cr3);
             }
             const int bias = (cx & 1) ? 2 : 1;
-            S[4 * kBS + cy * 8 + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
-            S[5 * kBS + cy * 8 + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
+            S[4 * kBS + cy * kRS + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
+            S[5 * kBS + cy * kRS + cx] = ((cr0 + cr1 + cr2 + cr3 + bias) >> 2) - 128;
             }
         }
         const int nfd = grey ? 32 : 48;   // lanes with a block row / column to transform
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < nfd) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * 8, 1);
+        if (lane < nfd) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * kRS, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < nfd) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), 8);
+        if (lane < nfd) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), kRS);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1014,6 +1021,9 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         int16_t* out = A.coefs + b0 * 64;
         int dc[6];
         uint32_t aclen[6];
+        int coef[6];                              // all six blocks' coefficients read back to back
+#pragma unroll
+        for (int k = 0; k < 6; ++k) coef[k] = (k >= 4 && grey) ? 0 : S[k * kBS + nat_off];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             if (k >= 4 && grey) {                 // zero chroma block: DC 0, EOB only
@@ -1022,7 +1032,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
                 aclen[k] = lane == 0 ? eob1 : 0u;
                 continue;
             }
-            int q = k < 4 ? quant_recip(S[k * kBS + nat], hy, my_) : quant_recip(S[k * kBS + nat], hc, mc_);
+            int q = k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
             if (k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
@@ -1066,6 +1076,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (++mx == A.mcux) { mx = 0; ++my; }
     }
 }
 

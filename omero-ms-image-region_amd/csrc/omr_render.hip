@@ -609,7 +609,9 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
     const int bpp = bytes_per_pixel(pixel_type);
     if (!bpp) return fail(ctx, OMR_INVALID_ARGUMENT, "unsupported pixel type");
     RenderPlan& P = pp.plan;
-    std::memset(&P, 0, sizeof(P));
+    // header only: a channel's slot is cleared when it is filled (the plan is ~29 KiB at 32
+    // channels, and only its first n_active slots are staged or read)
+    std::memset(&P, 0, offsetof(RenderPlan, ch));
     P.cd_start = q->cd_start;
     P.cd_end = q->cd_end;
     P.greyscale = q->model == OMR_MODEL_GREYSCALE;
@@ -624,6 +626,7 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
         if (b.family < OMR_FAMILY_LINEAR || b.family > OMR_FAMILY_EXPONENTIAL)
             return fail(ctx, OMR_INVALID_ARGUMENT, "unknown family");
         ChanParam& p = P.ch[na];
+        std::memset(&p, 0, offsetof(ChanParam, lut_rgb));   // the 768-byte LUT copy only when used
         p.index = c;
         p.family = b.family;
         if (b.family == OMR_FAMILY_LOGARITHMIC && (P.sem & OMR_SEM_LOG_UNGUARDED)) p.family = kFamLogRaw;

@@ -90,9 +90,9 @@ def test_project_stack(jctx, alg):
            1, sz - 1, 2, out, 1)
     st, exp = O.project(stack, _lib.PIXELS_UINT16, sx, sy, sz, alg, 1, sz - 1, 2, be_in=True, be_out=True)
     assert st == 0 and M.to_bytes(out) == exp.tobytes()
-    with pytest.raises(M.JavaException) as e:                   # ProjectionService's ValidationException
+    with pytest.raises(M.JavaException) as e:     # zIntervalBoundsCheck: start >= sizeZ (ValidationException)
         M.call("projectStack", jctx, M.jbytes(stack.view(np.uint8).reshape(-1)), _lib.PIXELS_UINT16, 1, sx, sy, sz,
-               alg, 5, 2, 1, out, 1)
+               alg, sz, 2, 1, out, 1)
     assert e.value.status == _lib.INVALID_ARGUMENT
 
 

@@ -8,6 +8,10 @@
 //   jpeg    : render + omr_encode_jpeg_device to a host buffer      (+ compressToStream, :580-582)
 //   fused   : omr_render_jpeg (the same request in one call: render inside the JPEG's first kernel)
 // with the planes already in HBM.  Prints one JSON object: p50 / p90 / mean in ms.
+// Then C3 (BASELINE configs[2]: 3-channel uint16 512x512x64 big-endian stacks, p=intmax|0:63 and
+// intmean): omr_render_projected_device requests issued back to back on one context (the
+// projection glue, ImageRegionRequestHandler.java:506-575), seven windows of >= 50 ms each with
+// one stream sync per window: the median window rate in requests/s (no Python in the loop).
 //
 // Usage: omr_latency [iters] [device]
 #include <hip/hip_runtime.h>
@@ -118,11 +122,51 @@ int main(int argc, char** argv) {
         if (i >= 5) t_fused.push_back(ms);
     }
     if (flen != jlen) { std::fprintf(stderr, "fused JPEG length %zu != %zu\n", flen, jlen); return 1; }
+    // ---- C3: projection glue requests back to back
+    constexpr int kS = 512, kZ = 64, kC = 3;
+    void* d_stacks[kC];
+    std::vector<uint16_t> stack((size_t)kS * kS * kZ);
+    for (int c = 0; c < kC; ++c) {
+        for (auto& v : stack) { seed = seed * 1664525u + 1013904223u; v = (uint16_t)(seed >> 16); }
+        if (hipMalloc(&d_stacks[c], stack.size() * 2) != hipSuccess) return 1;
+        if (hipMemcpy(d_stacks[c], stack.data(), stack.size() * 2, hipMemcpyHostToDevice) != hipSuccess) return 1;
+    }
+    double c3_rate[2];
+    for (int a = 0; a < 2; ++a) {
+        const int alg = a == 0 ? OMR_PROJECTION_MAX : OMR_PROJECTION_MEAN;
+        auto c3 = [&]() {
+            fill_bindings(ch);
+            return omr_render_projected_device(ctx, &q, ch, kC, (const void* const*)d_stacks, OMR_PIXELS_UINT16, 1, kS,
+                                               kS, kZ, alg, 0, kZ - 1, 1, 0, 0, d_argb);
+        };
+        for (int i = 0; i < 200; ++i)
+            if (!ok(c3(), ctx, "render_projected")) return 1;
+        if (!ok(omr_ctx_synchronize(ctx), ctx, "synchronize")) return 1;
+        std::vector<double> rates;
+        for (int w = 0; w < 7; ++w) {
+            const auto t0 = clk::now();
+            long n = 0;
+            double el = 0;
+            do {
+                for (int i = 0; i < 32; ++i)
+                    if (!ok(c3(), ctx, "render_projected")) return 1;
+                n += 32;
+                el = std::chrono::duration<double>(clk::now() - t0).count();
+            } while (el < 0.05);
+            if (!ok(omr_ctx_synchronize(ctx), ctx, "synchronize")) return 1;
+            rates.push_back(n / std::chrono::duration<double>(clk::now() - t0).count());
+        }
+        std::sort(rates.begin(), rates.end());
+        c3_rate[a] = rates[rates.size() / 2];
+    }
+    for (int c = 0; c < kC; ++c) (void)hipFree(d_stacks[c]);
     const Stats r = stats(t_render), j = stats(t_jpeg), f = stats(t_fused);
     std::printf("{\"iters\": %d, \"render_device_resident\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f}, "
                 "\"render_to_jpeg_host\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f, \"jpeg_bytes\": %zu}, "
-                "\"render_jpeg_one_call\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f}}\n",
-                iters, r.p50, r.p90, r.mean, j.p50, j.p90, j.mean, jlen, f.p50, f.p90, f.mean);
+                "\"render_jpeg_one_call\": {\"p50_ms\": %.4f, \"p90_ms\": %.4f, \"mean_ms\": %.4f}, "
+                "\"c3_requests_per_s\": {\"max\": %.1f, \"mean\": %.1f, "
+                "\"method\": \"median of 7 windows >= 50 ms, one context, no Python\"}}\n",
+                iters, r.p50, r.p90, r.mean, j.p50, j.p90, j.mean, jlen, f.p50, f.p90, f.mean, c3_rate[0], c3_rate[1]);
     for (int c = 0; c < kChannels; ++c) (void)hipFree(d_planes[c]);
     (void)hipFree(d_argb);
     omr_ctx_destroy(ctx);
