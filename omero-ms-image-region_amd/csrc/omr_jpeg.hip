@@ -16,6 +16,7 @@
 #include "omr_k2.h"
 
 #include <memory>
+#include <type_traits>
 
 namespace omr {
 
@@ -743,18 +744,26 @@ __constant__ uint8_t c_zigzag[64] = {
     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// Measurement-only ablations of B1 / F1 (tools/ablate_jpeg.sh builds libomr variants with
+// -DOMR_ABL=<mask>; their outputs are wrong).  0 in every real build.
+#ifndef OMR_ABL
+#define OMR_ABL 0
+#endif
+enum : int { kAblAclen = 1, kAblColour = 2, kAblFdct = 4, kAblLane0 = 8, kAblCoefStore = 16, kAblRender = 32,
+             kAblQuant = 64 };
+
 struct B1Args {
     const uint32_t* argb;
     int64_t tile_stride;  // pixels between tiles
     int16_t* coefs;       // [tile][nb][64] zig-zag order
-    uint16_t* aclen;      // [tile][nb] AC bits incl. ZRL/EOB
-    int16_t* dcs;         // [tile][nb] DC after dummy-block propagation
+    uint32_t* blk;        // [tile][nb] AC bits incl. ZRL/EOB | DC after dummy-block propagation << 16
     int32_t W, H, mcux, n_mcu, nb;
     int32_t mpw;          // MCUs per wave (prefetch depth vs. waves in flight)
     QTabs qt;
 };
 
 constexpr int kB1McuPerWave = 8;   // big batches; a few tiles use 1 so the grid still fills the chip
+static_assert(6 * kB1McuPerWave <= 64, "one per-block record per lane");
 
 // Pixels (x, y) and (x+1, y) of one row (clamped to the image), as one 8-byte load when both
 // are inside the row.
@@ -776,38 +785,40 @@ __device__ __forceinline__ void load_pair(const uint32_t* img, int W, int x, int
 // were conflicts (profiles/r02/jpeg_pmc_c2_r02h.txt).
 constexpr int kBS = 72, kRS = 9;
 
-// B1's pixel source: rendered ARGB tiles in HBM.  issue(m) loads the four pixels this lane
-// needs for MCU m (the next MCU's loads are in flight while the current one is transformed);
-// take() hands them over at the start of that MCU.
+// B1's pixel source: rendered ARGB tiles in HBM.  issue<S>() loads the four pixels this lane
+// needs for an MCU into prefetch slot S (two slots: the MCUs two ahead are in flight while the
+// current one is transformed); take<S>() hands them over at the start of that MCU.
 struct ArgbSource {
     const uint32_t* img;
     int W, H;
     bool even_w;
-    uint2 na = make_uint2(0, 0), nb = make_uint2(0, 0);
-    bool nclamp = false;
+    uint2 na[2] = {make_uint2(0, 0), make_uint2(0, 0)}, nb[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+    bool nclamp[2] = {false, false};
     __device__ ArgbSource(const B1Args& A, int tile)
         : img(A.argb + (int64_t)tile * A.tile_stride), W(A.W), H(A.H),
           // 8-byte pixel-pair loads need every row start 8-byte aligned
           even_w((A.W & 1) == 0 && (A.tile_stride & 1) == 0 && ((uintptr_t)A.argb & 7) == 0) {}
     // Even widths: two unconditional 8-byte loads per lane at clamped addresses; the edge
     // replication select happens when the pixels are used, so nothing waits on the prefetch.
+    template <int S>
     __device__ __forceinline__ void issue(int x0, int y0) {
         const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
         if (even_w) {
             const int xl = min(x0, W - 2);                        // even, W >= 2
-            na = *reinterpret_cast<const uint2*>(img + (int64_t)ya * W + xl);
-            nb = *reinterpret_cast<const uint2*>(img + (int64_t)yb * W + xl);
-            nclamp = x0 > W - 1;                                   // both columns clamp to W-1
+            na[S] = *reinterpret_cast<const uint2*>(img + (int64_t)ya * W + xl);
+            nb[S] = *reinterpret_cast<const uint2*>(img + (int64_t)yb * W + xl);
+            nclamp[S] = x0 > W - 1;                                // both columns clamp to W-1
         } else {
             const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
-            na = make_uint2(img[(int64_t)ya * W + xa], img[(int64_t)ya * W + xb]);
-            nb = make_uint2(img[(int64_t)yb * W + xa], img[(int64_t)yb * W + xb]);
-            nclamp = false;
+            na[S] = make_uint2(img[(int64_t)ya * W + xa], img[(int64_t)ya * W + xb]);
+            nb[S] = make_uint2(img[(int64_t)yb * W + xa], img[(int64_t)yb * W + xb]);
+            nclamp[S] = false;
         }
     }
+    template <int S>
     __device__ __forceinline__ void take(Rgb (&px)[4]) {
-        px[0] = rgb_of(nclamp ? na.y : na.x); px[1] = rgb_of(na.y);
-        px[2] = rgb_of(nclamp ? nb.y : nb.x); px[3] = rgb_of(nb.y);
+        px[0] = rgb_of(nclamp[S] ? na[S].y : na[S].x); px[1] = rgb_of(na[S].y);
+        px[2] = rgb_of(nclamp[S] ? nb[S].y : nb[S].x); px[3] = rgb_of(nb[S].y);
     }
     __device__ __forceinline__ uint32_t at(int x, int y) const { return img[(int64_t)y * W + x]; }
 };
@@ -830,7 +841,7 @@ struct PlaneSource {
     const FusedArgs& F;
     const uint32_t* s_contrib;   // LDS [n_active][256]
     const uint8_t* base[kFusedMaxActive];
-    uint32_t raw[kFusedMaxActive][2];
+    uint32_t raw[2][kFusedMaxActive][2];       // [prefetch slot][channel][row]
     int W, H;
     bool err = false;
     __device__ PlaneSource(const FusedArgs& f, const uint32_t* sc, int tile, int w, int h)
@@ -846,6 +857,7 @@ struct PlaneSource {
     }
     // Output pixels (x0, x0+1) x (y0, y0+1), x0 even, come from the source pair starting at sx
     // (reversed under flip_h) on rows sy0, sy1.
+    template <int S>
     __device__ __forceinline__ void issue(int x0, int y0) {
         const int sx = F.flip_h ? W - 2 - x0 : x0;
         const int64_t r0 = (int64_t)(F.flip_v ? H - 1 - y0 : y0) * F.row_stride + sx;
@@ -853,11 +865,11 @@ struct PlaneSource {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             if constexpr (BPP == 2) {   // global, not flat, loads: see ld_global
-                raw[a][0] = ld_global<uint32_t>(base[a] + r0 * 2);
-                raw[a][1] = ld_global<uint32_t>(base[a] + r1 * 2);
+                raw[S][a][0] = ld_global<uint32_t>(base[a] + r0 * 2);
+                raw[S][a][1] = ld_global<uint32_t>(base[a] + r1 * 2);
             } else {
-                raw[a][0] = ld_global<uint16_t>(base[a] + r0);
-                raw[a][1] = ld_global<uint16_t>(base[a] + r1);
+                raw[S][a][0] = ld_global<uint16_t>(base[a] + r0);
+                raw[S][a][1] = ld_global<uint16_t>(base[a] + r1);
             }
         }
     }
@@ -891,11 +903,12 @@ struct PlaneSource {
             return tab[v];
         }
     }
+    template <int S>
     __device__ __forceinline__ void take(Rgb (&px)[4]) {
         uint32_t acc[4] = {0, 0, 0, 0};         // source order: (lo, hi) of row 0, then row 1
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-            uint32_t w0 = raw[a][0], w1 = raw[a][1];
+            uint32_t w0 = raw[S][a][0], w1 = raw[S][a][1];
             if constexpr (BPP == 2) {
                 if constexpr (BE) { w0 = bswap16x2(w0); w1 = bswap16x2(w1); }
                 // int16 pixels biased to unsigned (x + 32768, one XOR per pixel pair); the host
@@ -907,6 +920,10 @@ struct PlaneSource {
                     mn[a] = pk_min_u16(mn[a], pk_min_u16(w0, w1));
                     mx[a] = pk_max_u16(mx[a], pk_max_u16(w0, w1));
                 }
+            }
+            if constexpr ((OMR_ABL & kAblRender) != 0) {   // raw words instead of quantize + table
+                acc[0] += w0 & 0x3FF; acc[1] += w0 >> 22; acc[2] += w1 & 0x3FF; acc[3] += w1 >> 22;
+                continue;
             }
             acc[0] += entry(a, w0, 0);
             acc[1] += entry(a, w0, 1);
@@ -955,28 +972,39 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
     // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
     const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
     const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
-    const int m0 = (blockIdx.x * 4 + wv) * A.mpw;
-    const int m1 = min(m0 + A.mpw, A.n_mcu);
+    // The workgroup's 4 * mpw MCUs are dealt round robin: at step j its four waves transform four
+    // horizontally adjacent MCUs (m = base + 4j + wave), so each row's 4 x 32 bytes of 16-bit
+    // planes (or 4 x 64 bytes of ARGB) are one 128-byte line read by the four waves together.
+    const int mbase = blockIdx.x * 4 * A.mpw;
+    const int cnt = max(0, min(A.mpw, (A.n_mcu - mbase - wv + 3) / 4));   // steps with m < n_mcu
     const int nat_off = (nat >> 3) * kRS + (nat & 7);   // zig-zag position `lane` in the block
     // MCU coordinates advance incrementally (no per-MCU division by the MCU row length)
-    int mx = m0 % A.mcux, my = m0 / A.mcux;
-    int nx = mx, ny = my;                          // the prefetched MCU
-    auto fetch = [&]() {
-        src.issue(nx * 16 + 2 * cx, ny * 16 + 2 * cy);
-        if (++nx == A.mcux) { nx = 0; ++ny; }
+    int mx = (mbase + wv) % A.mcux, my = (mbase + wv) / A.mcux;
+    int nx = mx, ny = my;                          // the next MCU to prefetch
+    auto step = [&](int& x, int& y) {              // m += 4
+        x += 4;
+        while (x >= A.mcux) { x -= A.mcux; ++y; }
     };
-    if (m0 < m1) fetch();
-    for (int m = m0; m < m1; ++m) {   // wave-uniform loop
-        // Grey MCU (every pixel r == g == b, e.g. the greyscale model's output): IJG's Y is then
-        // (65536 v + 32768) >> 16 = v exactly and Cb = Cr = 128, so both chroma blocks are zero —
-        // the colour transform, their FDCT and their quantisation are skipped.  Wave-uniform; the
-        // bottom-edge chroma rows (odd heights) take the general path.
+    auto fetch = [&](auto slot) {
+        src.template issue<decltype(slot)::value>(nx * 16 + 2 * cx, ny * 16 + 2 * cy);
+        step(nx, ny);
+    };
+    int abl_sink = 0;                             // ablation builds only: keeps dropped results live
+    int rec = 0;                                  // per-block records of this wave's MCUs (lane 6j + k)
+    // Grey MCU (every pixel r == g == b, e.g. the greyscale model's output): IJG's Y is then
+    // (65536 v + 32768) >> 16 = v exactly and Cb = Cr = 128, so both chroma blocks are zero —
+    // the colour transform, their FDCT and their quantisation are skipped.  Wave-uniform; the
+    // bottom-edge chroma rows (odd heights) take the general path.
+    // Two prefetch slots: step j's pixels arrive in slot j & 1, loaded two steps ahead.
+    auto mcu = [&](auto slot, int j) {
+        constexpr int SL = decltype(slot)::value;
+        const int m = mbase + 4 * j + wv;
         bool grey;
         {
             const int x0 = mx * 16 + 2 * cx;
             Rgb px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
-            src.take(px);
-            if (m + 1 < m1) fetch();
+            src.template take<SL>(px);
+            if (j + 2 < cnt) fetch(slot);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             auto isg = [](const Rgb& p) { return p.r == p.g && p.g == p.b; };
@@ -989,6 +1017,10 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
                 S[o + 1] = px[1].b - 128;
                 S[o + kRS] = px[2].b - 128;
                 S[o + kRS + 1] = px[3].b - 128;
+            } else if constexpr ((OMR_ABL & kAblColour) != 0) {
+                S[o] = px[0].r; S[o + 1] = px[1].g; S[o + kRS] = px[2].b; S[o + kRS + 1] = px[3].r;
+                S[4 * kBS + cy * kRS + cx] = px[0].g;
+                S[5 * kBS + cy * kRS + cx] = px[1].b;
             } else {
             ycc(px[0], y, cb0, cr0); S[o] = y - 128;
             ycc(px[1], y, cb1, cr1); S[o + 1] = y - 128;
@@ -1009,17 +1041,17 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < nfd) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * kRS, 1);
+        if ((OMR_ABL & kAblFdct) == 0 && lane < nfd) fdct8<0>(S + (lane >> 3) * kBS + (lane & 7) * kRS, 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (lane < nfd) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), kRS);
+        if ((OMR_ABL & kAblFdct) == 0 && lane < nfd) fdct8<1>(S + (lane >> 3) * kBS + (lane & 7), kRS);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int64_t b0 = (int64_t)tile * A.nb + (int64_t)m * 6;
         int16_t* out = A.coefs + b0 * 64;
-        int dc[6];
+        int qv[6];
         uint32_t aclen[6];
         int coef[6];                              // all six blocks' coefficients read back to back
 #pragma unroll
@@ -1027,18 +1059,17 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             if (k >= 4 && grey) {                 // zero chroma block: DC 0, EOB only
-                dc[k] = 0;
-                out[k * 64 + lane] = 0;
+                qv[k] = 0;
                 aclen[k] = lane == 0 ? eob1 : 0u;
                 continue;
             }
-            int q = k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
+            int q = (OMR_ABL & kAblQuant) ? coef[k] : k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
             if (k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
             }
-            dc[k] = q;
-            out[k * 64 + lane] = (int16_t)q;    // lane 0's DC is rewritten below, after propagation
+            qv[k] = q;
+            if constexpr ((OMR_ABL & kAblAclen) != 0) { aclen[k] = (uint32_t)q & 7u; continue; }
             // AC Huffman length, branch-free: run of zeros before this coefficient from the
             // previous non-zero (bit 0 stands for the DC, so an empty `below` gives prev = 0).
             const bool nzl = lane != 0 && q != 0;
@@ -1057,27 +1088,55 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         // one 32-bit wave sum in 16-bit halves: three DPP scans instead of six.
 #pragma unroll
         for (int k = 0; k < 6; k += 2) {
+            if constexpr ((OMR_ABL & kAblAclen) != 0) break;
             const uint32_t s2 = wave_sum(aclen[k] | (aclen[k + 1] << 16));
             aclen[k] = s2 & 0xFFFF;
             aclen[k + 1] = s2 >> 16;
         }
-        if (lane == 0) {   // jccoefct.c dummy-block DC propagation
+        // jccoefct.c dummy-block DC propagation on the wave-uniform DCs (lane 0's coefficient),
+        // then each block's 64 coefficients in one store (lane 0 stores the propagated DC)
+        int dc[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dc[k] = __builtin_amdgcn_readfirstlane(qv[k]);
+        {
             const bool c1 = mx * 2 + 1 >= ywib, row1 = my * 2 + 1 >= yhib;
             if (c1) dc[1] = dc[0];
             if (row1) { dc[2] = dc[1]; dc[3] = dc[1]; }
             else if (c1) dc[3] = dc[2];
+        }
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                out[k * 64] = (int16_t)dc[k];
-                A.dcs[b0 + k] = (int16_t)dc[k];
-                A.aclen[b0 + k] = (uint16_t)aclen[k];
-            }
+        for (int k = 0; k < 6; ++k) {
+            const int v = lane == 0 ? dc[k] : qv[k];
+            if constexpr ((OMR_ABL & kAblCoefStore) != 0) abl_sink ^= v;
+            else out[k * 64 + lane] = (int16_t)v;
+        }
+        // the six per-block records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in the
+        // wave's run); one store per wave after the loop instead of 18 one-lane stores per MCU
+        if constexpr ((OMR_ABL & kAblLane0) != 0) {
+            abl_sink ^= dc[0] + dc[5] + (int)aclen[0] + (int)aclen[3];
+        } else {
+            const int slot = lane - 6 * j;
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                rec = slot == k ? (int)((aclen[k] & 0xFFFFu) | ((uint32_t)dc[k] << 16)) : rec;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (++mx == A.mcux) { mx = 0; ++my; }
+        step(mx, my);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    if (cnt > 0) fetch(S0{});
+    if (cnt > 1) fetch(S1{});
+    for (int j = 0; j < cnt; j += 2) {   // wave-uniform loop, two steps per trip (static slots)
+        mcu(S0{}, j);
+        if (j + 1 < cnt) mcu(S1{}, j + 1);
     }
+    if ((OMR_ABL & kAblLane0) == 0 && lane < 6 * cnt)
+        A.blk[(int64_t)tile * A.nb + (int64_t)(mbase + 4 * (lane / 6) + wv) * 6 + lane % 6] = (uint32_t)rec;
+    if constexpr (OMR_ABL != 0)
+        if (abl_sink == 0x7FFF1234) A.blk[lane] = (uint32_t)abl_sink;
 }
 
 __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
@@ -1117,15 +1176,6 @@ __device__ __forceinline__ int prev_block_in_tile(int b) {
     return k == 0 ? (m - 1) * 6 + 3 : (m - 1) * 6 + k;
 }
 
-__device__ __forceinline__ uint32_t dc_bits(const int16_t* dcs, int b, const HuffLds& h) {
-    const int pb = prev_block_in_tile(b);
-    int d = dcs[b] - (pb >= 0 ? dcs[pb] : 0);
-    if (d < 0) d = -d;
-    const int nbits = d ? 32 - __clz(d) : 0;
-    const int t = (b % 6) < 4 ? 0 : 2;
-    return h.size[t][nbits] + nbits;
-}
-
 constexpr int kTileThreads = 1024;
 constexpr int kB3LdsWords = 4096;   // B3: a group's stream staged in LDS up to 512 bits per block
 constexpr int kGrp = 256;   // blocks per B3 workgroup = chunks per B4a/B6 group
@@ -1139,8 +1189,7 @@ __device__ __forceinline__ uint32_t block_reduce_sum(uint32_t v, uint32_t* s_wav
 // B2a: one lane per 8x8 block: its bit length (AC part from B1, DC part needs the previous
 // block's DC in scan order); per-256-block group sums.
 struct B2aArgs {
-    const uint16_t* aclen;
-    const int16_t* dcs;
+    const uint32_t* blk;   // B1's per-block records (AC bits | DC << 16)
     uint16_t* bits;        // [tile][nb]
     uint32_t* gsum;        // [tile][ngb]
     int32_t nb, ngb;
@@ -1154,12 +1203,13 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     const int tile = blockIdx.y, b = blockIdx.x * kGrp + threadIdx.x;
     uint32_t bits = 0;
     if (b < A.nb) {
-        const int16_t* dcs = A.dcs + (int64_t)tile * A.nb;
+        const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
         const int pb = prev_block_in_tile(b);
-        int d = dcs[b] - (pb >= 0 ? dcs[pb] : 0);
+        const uint32_t rb = blk[b];
+        int d = (int)(int16_t)(rb >> 16) - (pb >= 0 ? (int)(int16_t)(blk[pb] >> 16) : 0);
         if (d < 0) d = -d;
         const int nbits = d ? 32 - __clz(d) : 0;
-        bits = A.aclen[(int64_t)tile * A.nb + b] + s_dc[(b % 6) < 4 ? 0 : 1][nbits] + nbits;
+        bits = (rb & 0xFFFFu) + s_dc[(b % 6) < 4 ? 0 : 1][nbits] + nbits;
         A.bits[(int64_t)tile * A.nb + b] = (uint16_t)bits;
     }
     const uint32_t total = block_reduce_sum(bits, sw);
@@ -1219,7 +1269,7 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs 
 
 struct B3Args {
     const int16_t* coefs;
-    const int16_t* dcs;
+    const uint32_t* blk;     // B1's per-block records (DC << 16)
     const uint16_t* bits;    // [tile][nb]
     const uint32_t* goff;    // [tile][ngb] exclusive bit offset of each 256-block group
     uint32_t* words;
@@ -1271,7 +1321,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = src[i];
         const int pb = prev_block_in_tile(b);
-        const int pred = pb >= 0 ? A.dcs[(int64_t)tile * A.nb + pb] : 0;
+        const int pred = pb >= 0 ? (int)(int16_t)(A.blk[(int64_t)tile * A.nb + pb] >> 16) : 0;
         uint64_t acc = 0;
         int nacc = (int)(boff & 31);
         uint32_t wpos = boff >> 5;
@@ -1551,7 +1601,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
 // Batch workspace layout.
 struct JpegBatchLayout {
     int64_t n_mcu, nb, ngb, slot_words, slot_chunks, slot_groups;
-    size_t coef, aclen, dcs, bits, gsum, tbits, words, cnt, csum, ngroups, stuffed, hdr, total;
+    size_t coef, blk, bits, gsum, tbits, words, cnt, csum, ngroups, stuffed, hdr, total;
 };
 
 static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
@@ -1565,8 +1615,7 @@ static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
     size_t o = align_up(base, 256);
     auto take = [&](size_t bytes) { const size_t r = o; o = align_up(o + bytes, 256); return r; };
     L.coef = take((size_t)n * L.nb * 128);
-    L.aclen = take((size_t)n * L.nb * 2);
-    L.dcs = take((size_t)n * L.nb * 2);
+    L.blk = take((size_t)n * L.nb * 4);
     L.bits = take((size_t)n * L.nb * 2);
     L.gsum = take((size_t)n * L.ngb * 4);
     L.tbits = take((size_t)n * 4);
@@ -1630,8 +1679,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     a1.argb = d_argb;
     a1.tile_stride = tile_stride;
     a1.coefs = reinterpret_cast<int16_t*>(ws + L.coef);
-    a1.aclen = reinterpret_cast<uint16_t*>(ws + L.aclen);
-    a1.dcs = reinterpret_cast<int16_t*>(ws + L.dcs);
+    a1.blk = reinterpret_cast<uint32_t*>(ws + L.blk);
     a1.W = W;
     a1.H = H;
     a1.mcux = (W + 15) / 16;
@@ -1642,9 +1690,9 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
     set_recips(a1.qt);
     uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
-    B2aArgs a2{a1.aclen, a1.dcs, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
+    B2aArgs a2{a1.blk, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
     GroupScanArgs a2b{u32(L.gsum), nullptr, u32(L.tbits), u32(L.words), nullptr, L.ngb, L.slot_words, (int32_t)L.ngb};
-    B3Args a3{a1.coefs, a1.dcs, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
+    B3Args a3{a1.coefs, a1.blk, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
     B4aArgs a4{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), u32(L.ngroups), L.slot_words, L.slot_chunks,
                L.slot_groups};
     GroupScanArgs a4b{u32(L.csum), u32(L.ngroups), u32(L.stuffed), nullptr, u32(L.tbits), L.slot_groups, 0, 0};
@@ -1667,6 +1715,10 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
         } else {
             launch_render_fdct(g1, ctx->stream, a1, fused->args, fused->bpp, fused->be);
         }
+    }
+    if constexpr (OMR_ABL != 0) {   // ablation builds time B1 / F1 only: their outputs are not a stream
+        OMR_HIP(ctx, hipGetLastError());
+        return OMR_OK;
     }
     hipLaunchKernelGGL(k_jpeg_block_bits, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a2);
     hipLaunchKernelGGL(k_jpeg_group_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a2b);
