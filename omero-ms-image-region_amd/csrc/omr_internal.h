@@ -119,6 +119,7 @@ struct Ctx {
     // PNG D3 (Huffman tables) on the device (env OMR_PNG_DEVICE_D3=1): no mid-encode host round
     // trip, but the single-workgroup build measured slower than the host's
     bool png_device_d3 = false;
+    bool f1_f32 = true;              // F1's Fast16 quantize in f32 when proven exact (OMR_F1_F32=0: f64)
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
     int k2_eval_cpt = 2;

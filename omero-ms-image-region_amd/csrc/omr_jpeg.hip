@@ -894,6 +894,8 @@ struct PlaneSource {
                 v = fast16(x, p);
             } else if constexpr (MODE == kFusedFast16I) {
                 v = fast16i(x, p);
+            } else if constexpr (MODE == kFusedFast16F) {
+                v = fast16f(x, p.wsi, F.R.fa[a], F.R.fb[a]);
             } else if (MODE == kFusedLinear16 || p.mode == kModeLinear16) {   // uniform
                 v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
             } else {
@@ -1643,7 +1645,8 @@ template <bool BE>
 static void launch_render_fdct_mode(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f) {
     switch (f.R.mode) {
     case kFusedFast16:
-        if (f.R.ws_int) launch_render_fdct_na<2, BE, kFusedFast16I>(g, st, a1, f);
+        if (f.R.f32) launch_render_fdct_na<2, BE, kFusedFast16F>(g, st, a1, f);
+        else if (f.R.ws_int) launch_render_fdct_na<2, BE, kFusedFast16I>(g, st, a1, f);
         else launch_render_fdct_na<2, BE, kFusedFast16>(g, st, a1, f);
         break;
     case kFusedLinear16: launch_render_fdct_na<2, BE, kFusedLinear16>(g, st, a1, f); break;

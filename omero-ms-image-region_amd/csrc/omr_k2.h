@@ -16,6 +16,7 @@ struct K2Chan {
     int32_t gmin, gmax; // LUT domain
     int32_t check;      // pixel values may fall outside [gmin, gmax] (QuantizationException)
     int32_t second;     // the a1*v + cdStart rounding stage is not the identity
+    int32_t wsi;        // integral window start (FusedRender::f32: x - wsi in int32)
     double ws, a0, a1;
     uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
 };
@@ -58,6 +59,15 @@ __device__ __forceinline__ uint32_t fast16i(int x, const K2Chan& p) {
     return (uint32_t)min(max(v, 0), 255);
 }
 
+// fast16i in single precision: round(a0*(x - ws)) clamped is a non-decreasing step function of
+// x with 255 steps, and so is trunc(fma(x - ws, fa, fb)) clamped; the host picks (fa, fb) so that
+// the two step at the same 255 pixel values (fast16_f32_params), i.e. agree on every x of the
+// type, or the launch keeps the f64 form.  Full-rate f32 instead of four f64 operations.
+__device__ __forceinline__ uint32_t fast16f(int x, int wsi, float fa, float fb) {
+    const float y = __builtin_amdgcn_fmed3f(__builtin_fmaf((float)(x - wsi), fa, fb), 0.0f, 255.0f);
+    return (uint32_t)(int)y;                     // toward zero; y in [0, 255]
+}
+
 
 __device__ __forceinline__ uint32_t pack_contrib(const ChanParam& p, int v, int cds, int cde, int grey, uint32_t sem) {
     const int vv = p.reverse ? ((cde - v + cds) & 0xFF) : v;
@@ -97,7 +107,8 @@ __device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__
 // quantizes + composites each pixel as K2 does (same helpers, same tables) and encodes it.
 constexpr int kFusedMaxActive = 4;
 enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4,
-                           kFusedFast16I = 5 /* launch-only: Fast16 with integral window starts */ };
+                           kFusedFast16I = 5 /* launch-only: Fast16 with integral window starts */,
+                           kFusedFast16F = 6 /* launch-only: Fast16I in f32 (FusedRender::f32) */ };
 struct FusedRender {
     K2Chan ch[kFusedMaxActive];
     const uint32_t* contrib;     // [n_active][256] (workspace; built by K1 unless the kernel builds it)
@@ -107,7 +118,14 @@ struct FusedRender {
     int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
     int32_t any_check;           // some channel's LUT domain is narrower than its pixel type
     int32_t ws_int;              // every window start is an integer (|ws| < 2^30): x - ws in int32
+    int32_t f32;                 // Fast16 with every channel's (fa, fb) proven exact: kFusedFast16F
+    float fa[kFusedMaxActive], fb[kFusedMaxActive];
 };
+
+// (fa, fb) for fast16f such that fast16f(x) == fast16i(x) for every x in [0, xmax] (the pixel
+// domain, int16 biased to unsigned) given the window start wsi and slope a0; false when no
+// candidate near (a0, 0.5) steps at exactly fast16i's 255 pixel values.
+bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* fb);
 
 // Host side (omr_render.hip).  render_fused_plan: true when the fused kernel covers these
 // settings (8/16-bit integer pixels, 1..4 active channels); *st != OMR_OK is a request error.

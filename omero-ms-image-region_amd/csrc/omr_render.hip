@@ -804,6 +804,54 @@ static bool fast_linear_ok(const ChanParam& c, const RenderPlan& P) {
     return true;
 }
 
+// fast16i on the host, operation for operation (the library builds with -ffp-contract=off)
+static int host_fast16i(int64_t t, double a0) {
+    const double e = a0 * (double)t + 0.5;
+    if (!(e < 256.0)) return 255;                      // also covers e beyond the int range
+    return e < 1.0 ? 0 : (int)e;                       // trunc, clamped below at 0
+}
+
+static int host_fast16f(int64_t t, float fa, float fb) {
+    const float y = std::fmaf((float)t, fa, fb);       // correctly rounded, as v_fma_f32
+    if (!(y < 256.0f)) return 255;
+    return y < 1.0f ? 0 : (int)y;
+}
+
+bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* fb) {
+    if (!(a0 > 0) || !(a0 < 1e6) || wsi < -(1 << 23) || wsi > (1 << 23)) return false;
+    // fast16i steps from k-1 to k at x = wsi + bp[k]: t = x - wsi over [tlo, thi]
+    const int64_t tlo = -wsi, thi = (int64_t)xmax - wsi;
+    int64_t bp[256];
+    for (int k = 1; k <= 255; ++k) {
+        int64_t t = (int64_t)std::ceil((k - 0.5) / a0);
+        t = std::max<int64_t>(tlo, std::min<int64_t>(thi + 1, t));
+        while (t > tlo && host_fast16i(t - 1, a0) >= k) --t;
+        while (t <= thi && host_fast16i(t, a0) < k) ++t;
+        bp[k] = t;                                     // thi + 1: level k is never reached
+    }
+    // both functions are non-decreasing in t, so agreeing on both sides of every step means
+    // agreeing everywhere
+    auto exact = [&](float A, float B) {
+        for (int k = 1; k <= 255; ++k) {
+            const int64_t b = bp[k];
+            if (b <= thi && host_fast16f(b, A, B) < k) return false;
+            if (b > tlo && host_fast16f(b - 1, A, B) >= k) return false;
+        }
+        return true;
+    };
+    const float A0 = (float)a0;
+    for (int da = 0; da < 5; ++da) {                   // A0, +1, -1, +2, -2 ulps
+        float A = A0;
+        for (int i = 0; i < (da + 1) / 2; ++i) A = std::nextafterf(A, (da & 1) ? INFINITY : 0.0f);
+        for (int db = 0; db < 9; ++db) {               // 0.5, then +-1..4 ulps
+            float B = 0.5f;
+            for (int i = 0; i < (db + 1) / 2; ++i) B = std::nextafterf(B, (db & 1) ? INFINITY : 0.0f);
+            if (A > 0 && exact(A, B)) { *fa = A; *fb = B; return true; }
+        }
+    }
+    return false;
+}
+
 static void type_bounds(int32_t t, double& lo, double& hi) {
     switch (t) {
     case OMR_PIXELS_INT8: lo = -128; hi = 127; break;
@@ -1051,12 +1099,21 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.gmax = c.gmax + bias;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
         F.any_check |= k.check;
-        F.ws_int = (i == 0 ? 1 : F.ws_int) & ((c.ws == std::floor(c.ws) && std::fabs(c.ws) < 1073741824.0) ? 1 : 0);
+        const bool wint = c.ws == std::floor(c.ws) && std::fabs(c.ws) < 1073741824.0;
+        F.ws_int = (i == 0 ? 1 : F.ws_int) & (wint ? 1 : 0);
         k.second = c.second;
         k.ws = c.ws + (double)bias;
+        k.wsi = wint ? (int32_t)k.ws : 0;
         k.a0 = c.a0;
         k.a1 = c.a1;
         k.lut_off = c.lut_off;
+    }
+    // The fused JPEG kernel (bias_int16), Fast16 with integral window starts: the f32 form where
+    // it is proven exact for every pixel value (16-bit pixels: x in [0, 65535] after the bias)
+    if (bias_int16 && fp->mode == kFusedFast16 && F.ws_int && ctx->f1_f32) {
+        F.f32 = 1;
+        for (int i = 0; i < na && F.f32; ++i)
+            F.f32 = fast16_f32_params(F.ch[i].a0, F.ch[i].wsi, 65535, &F.fa[i], &F.fb[i]) ? 1 : 0;
     }
     F.contrib = d_contrib;
     F.plan = d_plan;
@@ -1319,4 +1376,10 @@ extern "C" omr_status omr_render_projected_device(
     const bool aligned = vec_aligned(bpp, size_x, size_x) && (reinterpret_cast<uintptr_t>(d_argb_out) % 16 == 0);
     return enqueue_render(ctx, pp, pixel_type, 0, d_ptrs, size_c, 1, size_x, size_x, size_y, flip_h, flip_v,
                           d_argb_out, nullptr, aligned, L, nullptr, ptrs.data(), sizeof(void*) * ptrs.size());
+}
+
+// Test hook (not part of omr.h): the F1 f32 quantize parameters, for the host-side exhaustive
+// check in tests/test_f32_quantize.py.
+extern "C" int32_t omr_debug_fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* fb) {
+    return omr::fast16_f32_params(a0, wsi, xmax, fa, fb) ? 1 : 0;
 }
