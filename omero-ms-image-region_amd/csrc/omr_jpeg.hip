@@ -679,9 +679,9 @@ omr_status omr_encode_jpeg(omr_ctx* ctx, const uint32_t* argb, int32_t width, in
 // ImageRegionRequestHandler.java:580-582).  Here a whole batch of rendered tiles (e.g. the
 // output of omr_render_batch_*_device) is encoded by eight launches whose grids span all tiles:
 //   B1  k_jpeg_fdct_batch   one wave per MCU: colour, downsample, FDCT, quantise (zig-zag lane
-//                           order), plus each block's AC Huffman length by ballot arithmetic
+//                           order), the blocks' DCs after dummy-block propagation
 //   B2a k_jpeg_block_bits   one lane per block: total bit length (DC needs the previous block's
-//                           DC), sums per group of 256 blocks
+//                           DC; AC by a walk over the 63 coefficients), sums per 256-block group
 //   B2b k_jpeg_group_scan   one workgroup per tile: group bit offsets, tile bit length, zero
 //                           the tile's bit-stream words
 //   B3  k_jpeg_huff_thread  one lane per block: in-group scan -> bit offset, Huffman-code the 64
@@ -749,7 +749,7 @@ __constant__ uint8_t c_zigzag[64] = {
 #ifndef OMR_ABL
 #define OMR_ABL 0
 #endif
-enum : int { kAblAclen = 1, kAblColour = 2, kAblFdct = 4, kAblLane0 = 8, kAblCoefStore = 16, kAblRender = 32,
+enum : int { kAblColour = 2, kAblFdct = 4, kAblLane0 = 8, kAblCoefStore = 16, kAblRender = 32,
              kAblQuant = 64 };
 
 struct B1Args {
@@ -960,7 +960,7 @@ struct PlaneSource {
 
 // The B1 body for one pixel source (see k_jpeg_fdct_batch below).
 template <class Src>
-__device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8_t (*s_acsize)[256]) {
+__device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tile = blockIdx.y;
     const int W = A.W, H = A.H;
@@ -970,10 +970,6 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
     const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
     const uint32_t my_ = A.qt.m[0][nat], mc_ = A.qt.m[1][nat];   // host-computed (no 64-bit divide)
     const int hy = qy << 2, hc = qc << 2;
-    const uint64_t lt_mask = (1ull << lane) - 1;
-    // ZRL / EOB code lengths of the luma (0) and chroma (1) AC tables: wave-uniform scalars
-    const uint32_t zrl0 = c_huff[1].size[0xF0], zrl1 = c_huff[3].size[0xF0];
-    const uint32_t eob0 = c_huff[1].size[0x00], eob1 = c_huff[3].size[0x00];
     // The workgroup's 4 * mpw MCUs are dealt round robin: at step j its four waves transform four
     // horizontally adjacent MCUs (m = base + 4j + wave), so each row's 4 x 32 bytes of 16-bit
     // planes (or 4 x 64 bytes of ARGB) are one 128-byte line read by the four waves together.
@@ -1054,49 +1050,23 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
         const int64_t b0 = (int64_t)tile * A.nb + (int64_t)m * 6;
         int16_t* out = A.coefs + b0 * 64;
         int qv[6];
-        uint32_t aclen[6];
         int coef[6];                              // all six blocks' coefficients read back to back
 #pragma unroll
         for (int k = 0; k < 6; ++k) coef[k] = (k >= 4 && grey) ? 0 : S[k * kBS + nat_off];
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            if (k >= 4 && grey) {                 // zero chroma block: DC 0, EOB only
-                qv[k] = 0;
-                aclen[k] = lane == 0 ? eob1 : 0u;
-                continue;
-            }
-            int q = (OMR_ABL & kAblQuant) ? coef[k] : k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
+            int q = (k >= 4 && grey) ? 0                       // zero chroma block
+                  : (OMR_ABL & kAblQuant) ? coef[k] : k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
             if (k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
             }
             qv[k] = q;
-            if constexpr ((OMR_ABL & kAblAclen) != 0) { aclen[k] = (uint32_t)q & 7u; continue; }
-            // AC Huffman length, branch-free: run of zeros before this coefficient from the
-            // previous non-zero (bit 0 stands for the DC, so an empty `below` gives prev = 0).
-            const bool nzl = lane != 0 && q != 0;
-            const uint64_t nz = __ballot(nzl);
-            const int t = k < 4 ? 0 : 1;
-            const uint64_t below = (nz & lt_mask) | 1ull;
-            const int r = lane - (63 - __clzll(below)) - 1;
-            const int a = q < 0 ? -q : q;
-            const int nbits = 32 - __clz(a);
-            const uint32_t len = (uint32_t)(r >> 4) * (t ? zrl1 : zrl0) + s_acsize[t][((r & 15) << 4) | nbits] + nbits;
-            uint32_t bits = nzl ? len : 0u;
-            if (lane == 0 && (nz >> 63) == 0) bits = t ? eob1 : eob0;   // EOB after the last non-zero
-            aclen[k] = bits;
-        }
-        // A block's AC bits stay below 2^11 (63 x (16 + 10) + ZRLs + EOB), so two blocks share
-        // one 32-bit wave sum in 16-bit halves: three DPP scans instead of six.
-#pragma unroll
-        for (int k = 0; k < 6; k += 2) {
-            if constexpr ((OMR_ABL & kAblAclen) != 0) break;
-            const uint32_t s2 = wave_sum(aclen[k] | (aclen[k + 1] << 16));
-            aclen[k] = s2 & 0xFFFF;
-            aclen[k + 1] = s2 >> 16;
         }
         // jccoefct.c dummy-block DC propagation on the wave-uniform DCs (lane 0's coefficient),
-        // then each block's 64 coefficients in one store (lane 0 stores the propagated DC)
+        // then each block's 64 coefficients in one store (lane 0 stores the propagated DC).  The
+        // blocks' Huffman lengths are B2a's (one lane per block walks the stored coefficients:
+        // half the instructions of a ballot-per-coefficient length here).
         int dc[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) dc[k] = __builtin_amdgcn_readfirstlane(qv[k]);
@@ -1112,15 +1082,14 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
             if constexpr ((OMR_ABL & kAblCoefStore) != 0) abl_sink ^= v;
             else out[k * 64 + lane] = (int16_t)v;
         }
-        // the six per-block records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in the
-        // wave's run); one store per wave after the loop instead of 18 one-lane stores per MCU
+        // the six per-block DC records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in
+        // the wave's run); one store per wave after the loop instead of six one-lane stores per MCU
         if constexpr ((OMR_ABL & kAblLane0) != 0) {
-            abl_sink ^= dc[0] + dc[5] + (int)aclen[0] + (int)aclen[3];
+            abl_sink ^= dc[0] + dc[5];
         } else {
             const int slot = lane - 6 * j;
 #pragma unroll
-            for (int k = 0; k < 6; ++k)
-                rec = slot == k ? (int)((aclen[k] & 0xFFFFu) | ((uint32_t)dc[k] << 16)) : rec;
+            for (int k = 0; k < 6; ++k) rec = slot == k ? (int)((uint32_t)dc[k] << 16) : rec;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
@@ -1143,11 +1112,8 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S, uint8
 
 __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
     __shared__ int s[4][6 * kBS + 8];
-    __shared__ uint8_t s_acsize[2][256];
-    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
-    __syncthreads();
     ArgbSource src(A, blockIdx.y);
-    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
+    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
 }
 
 // F1: fused render + B1 (see PlaneSource).  The contribution tables are staged once per
@@ -1155,13 +1121,11 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
 template <int BPP, bool BE, int MODE, int NA>
 __global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F) {
     __shared__ int s[4][6 * kBS + 8];
-    __shared__ uint8_t s_acsize[2][256];
     __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
-    for (int i = threadIdx.x; i < 512; i += 256) s_acsize[i >> 8][i & 255] = c_huff[1 + 2 * (i >> 8)].size[i & 255];
     for (int i = threadIdx.x; i < NA * 256; i += 256) s_contrib[i] = F.R.contrib[i];
     __syncthreads();
     PlaneSource<BPP, BE, MODE, NA> src(F, s_contrib, blockIdx.y, A.W, A.H);
-    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], s_acsize);
+    b1_body(A, src, s[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)]);
     src.finish();
     if (__ballot(src.err)) {
         if ((threadIdx.x & 63) == 0) {
@@ -1188,31 +1152,60 @@ __device__ __forceinline__ uint32_t block_reduce_sum(uint32_t v, uint32_t* s_wav
     return total;
 }
 
-// B2a: one lane per 8x8 block: its bit length (AC part from B1, DC part needs the previous
-// block's DC in scan order); per-256-block group sums.
+// B2a: one lane per 8x8 block: its bit length, and per-256-block group sums.  The DC part needs
+// the previous block's DC in scan order (B1's records); the AC part walks the block's 63
+// zig-zag coefficients (eight 16-byte loads into registers, the walk unrolled): run length,
+// magnitude category by frexp, code length from an LDS table, ZRLs and EOB, branch-free.
 struct B2aArgs {
-    const uint32_t* blk;   // B1's per-block records (AC bits | DC << 16)
+    const int16_t* coefs;  // [tile][nb][64] zig-zag order
+    const uint32_t* blk;   // B1's per-block records (DC << 16)
     uint16_t* bits;        // [tile][nb]
     uint32_t* gsum;        // [tile][ngb]
     int32_t nb, ngb;
 };
 
+// Magnitude category (bit length of |c|, 0 for 0) of a coefficient: frexp's exponent of the exact
+// float, sign-independent (two instructions instead of abs + clz + a zero select).
+__device__ __forceinline__ int mag_bits(int c) { return __builtin_amdgcn_frexp_expf((float)c); }
+
 __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     __shared__ uint8_t s_dc[2][16];
+    __shared__ uint8_t s_acsz[2][256];   // AC code lengths, size-0 entries (EOB, ZRL, unused) 0
     __shared__ uint32_t sw[16];
     if (threadIdx.x < 32) s_dc[threadIdx.x >> 4][threadIdx.x & 15] = c_huff[2 * (threadIdx.x >> 4)].size[threadIdx.x & 15];
+    for (int i = threadIdx.x; i < 512; i += kGrp)
+        s_acsz[i >> 8][i & 255] = (i & 15) == 0 ? 0 : c_huff[1 + 2 * (i >> 8)].size[i & 255];
     __syncthreads();
     const int tile = blockIdx.y, b = blockIdx.x * kGrp + threadIdx.x;
     uint32_t bits = 0;
     if (b < A.nb) {
+        const int64_t gb = (int64_t)tile * A.nb + b;
+        const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
+        uint4 q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = src[i];
         const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
         const int pb = prev_block_in_tile(b);
         const uint32_t rb = blk[b];
-        int d = (int)(int16_t)(rb >> 16) - (pb >= 0 ? (int)(int16_t)(blk[pb] >> 16) : 0);
-        if (d < 0) d = -d;
-        const int nbits = d ? 32 - __clz(d) : 0;
-        bits = (rb & 0xFFFFu) + s_dc[(b % 6) < 4 ? 0 : 1][nbits] + nbits;
-        A.bits[(int64_t)tile * A.nb + b] = (uint16_t)bits;
+        const int d = (int)(int16_t)(rb >> 16) - (pb >= 0 ? (int)(int16_t)(blk[pb] >> 16) : 0);
+        const int nbd = mag_bits(d);
+        const int t = (b % 6) < 4 ? 0 : 1;
+        bits = s_dc[t][nbd] + nbd;
+        const uint32_t zrl = c_huff[1 + 2 * t].size[0xF0], eob = c_huff[1 + 2 * t].size[0x00];
+        const uint8_t* sz = s_acsz[t];
+        uint32_t r16 = 0;                                  // zero run before coefficient k, times 16
+#pragma unroll
+        for (int k = 1; k < 64; ++k) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
+            const int c = (k & 1) ? (int)(int16_t)(w[(k >> 1) & 3] >> 16) : (int)(int16_t)(w[(k >> 1) & 3] & 0xFFFF);
+            const int nb = mag_bits(c);
+            // c == 0: nb == 0 and the (run, 0) entry is 0, so only the ZRL term needs the select
+            const uint32_t len = sz[(r16 & 0xF0) | nb] + nb + (c ? (r16 >> 8) * zrl : 0u);
+            bits += len;
+            r16 = c ? 0u : r16 + 16;
+        }
+        if (r16) bits += eob;                              // EOB after the last non-zero
+        A.bits[gb] = (uint16_t)bits;
     }
     const uint32_t total = block_reduce_sum(bits, sw);
     if (threadIdx.x == 0) A.gsum[(int64_t)tile * A.ngb + blockIdx.x] = total;
@@ -1367,8 +1360,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
             if (k > 16 && __ballot(nzk && r > 15)) {                // r <= k - 1: no ZRL before k 17
                 if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
             }
-            const int a = c < 0 ? -c : c;
-            const int nbits = 32 - __clz(a);                       // 0 for c == 0
+            const int nbits = mag_bits(c);                         // 0 for c == 0
             const uint32_t cs = s_ac[ta][((r & 15) << 4) | nbits];
             const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
             put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
@@ -1693,7 +1685,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
     set_recips(a1.qt);
     uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
-    B2aArgs a2{a1.blk, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
+    B2aArgs a2{a1.coefs, a1.blk, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
     GroupScanArgs a2b{u32(L.gsum), nullptr, u32(L.tbits), u32(L.words), nullptr, L.ngb, L.slot_words, (int32_t)L.ngb};
     B3Args a3{a1.coefs, a1.blk, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
     B4aArgs a4{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), u32(L.ngroups), L.slot_words, L.slot_chunks,

@@ -6,7 +6,7 @@
 #   run (GPU box):      tools/ablate_jpeg.sh run
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-MASKS=${ABL_MASKS:-"0 1 2 4 8 16 32 64 127"}
+MASKS=${ABL_MASKS:-"0 2 4 8 16 32 64 127"}
 if [ "$1" = build ]; then
   cd $R/omero-ms-image-region_amd
   for m in $MASKS; do
