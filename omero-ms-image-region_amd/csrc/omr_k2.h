@@ -60,12 +60,18 @@ __device__ __forceinline__ uint32_t fast16i(int x, const K2Chan& p) {
 }
 
 // fast16i in single precision: round(a0*(x - ws)) clamped is a non-decreasing step function of
-// x with 255 steps, and so is trunc(fma(x - ws, fa, fb)) clamped; the host picks (fa, fb) so that
-// the two step at the same 255 pixel values (fast16_f32_params), i.e. agree on every x of the
-// type, or the launch keeps the f64 form.  Full-rate f32 instead of four f64 operations.
+// x with 255 steps, and so is the f32 form below; the host picks fa so that the two step at the
+// same 255 pixel values (fast16_f32_params), i.e. agree on every x of the type, or the launch
+// keeps the f64 form.  fb is the magic 1.5 * 2^23: in [2^23, 2^24) an f32 has ulp 1, so the one
+// rounding of the fma is round-to-nearest-even of the exact (x - ws) * fa, and the float's bits
+// are 0x4B400000 + that integer; an integer med3 on the bits clamps to [0, 255] (beyond
+// +-2^22 the exponent moves and the clamp still saturates the right way).  Full-rate f32 and no
+// float -> int conversion instead of four f64 operations.
+constexpr int32_t kMagicBits = 0x4B400000;            // bits of 12582912.0f = 1.5 * 2^23
 __device__ __forceinline__ uint32_t fast16f(int x, int wsi, float fa, float fb) {
-    const float y = __builtin_amdgcn_fmed3f(__builtin_fmaf((float)(x - wsi), fa, fb), 0.0f, 255.0f);
-    return (uint32_t)(int)y;                     // toward zero; y in [0, 255]
+    const float y = __builtin_fmaf((float)(x - wsi), fa, fb);
+    const int32_t b = __float_as_int(y);
+    return (uint32_t)(min(max(b, kMagicBits), kMagicBits + 255) - kMagicBits);
 }
 
 
@@ -123,8 +129,8 @@ struct FusedRender {
 };
 
 // (fa, fb) for fast16f such that fast16f(x) == fast16i(x) for every x in [0, xmax] (the pixel
-// domain, int16 biased to unsigned) given the window start wsi and slope a0; false when no
-// candidate near (a0, 0.5) steps at exactly fast16i's 255 pixel values.
+// domain, int16 biased to unsigned) given the window start wsi and slope a0; false when no f32
+// slope within a few ulps of a0 steps at exactly fast16i's 255 pixel values.
 bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* fb);
 
 // Host side (omr_render.hip).  render_fused_plan: true when the fused kernel covers these

@@ -813,8 +813,9 @@ static int host_fast16i(int64_t t, double a0) {
 
 static int host_fast16f(int64_t t, float fa, float fb) {
     const float y = std::fmaf((float)t, fa, fb);       // correctly rounded, as v_fma_f32
-    if (!(y < 256.0f)) return 255;
-    return y < 1.0f ? 0 : (int)y;
+    int32_t b;
+    std::memcpy(&b, &y, 4);
+    return std::min(std::max(b, kMagicBits), kMagicBits + 255) - kMagicBits;
 }
 
 bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* fb) {
@@ -831,7 +832,8 @@ bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* f
     }
     // both functions are non-decreasing in t, so agreeing on both sides of every step means
     // agreeing everywhere
-    auto exact = [&](float A, float B) {
+    const float B = 12582912.0f;                       // kMagicBits
+    auto exact = [&](float A) {
         for (int k = 1; k <= 255; ++k) {
             const int64_t b = bp[k];
             if (b <= thi && host_fast16f(b, A, B) < k) return false;
@@ -840,14 +842,10 @@ bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* f
         return true;
     };
     const float A0 = (float)a0;
-    for (int da = 0; da < 5; ++da) {                   // A0, +1, -1, +2, -2 ulps
+    for (int da = 0; da < 17; ++da) {                  // A0, +1, -1, ..., +8, -8 ulps
         float A = A0;
         for (int i = 0; i < (da + 1) / 2; ++i) A = std::nextafterf(A, (da & 1) ? INFINITY : 0.0f);
-        for (int db = 0; db < 9; ++db) {               // 0.5, then +-1..4 ulps
-            float B = 0.5f;
-            for (int i = 0; i < (db + 1) / 2; ++i) B = std::nextafterf(B, (db & 1) ? INFINITY : 0.0f);
-            if (A > 0 && exact(A, B)) { *fa = A; *fb = B; return true; }
-        }
+        if (A > 0 && exact(A)) { *fa = A; *fb = B; return true; }
     }
     return false;
 }

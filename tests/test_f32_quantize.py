@@ -37,12 +37,20 @@ def rule_f64(a0, wsi):
 
 
 def rule_f32(fa, fb, wsi):
-    """fast16f: fma(x - ws, fa, fb) rounded once to f32, clamped to [0, 255], truncated.
-    t * fa (<= 48 significant bits) and the sum (< 64 bits for these magnitudes) are exact in
-    x87 extended precision, so one rounding to float32 reproduces v_fma_f32."""
-    t = (X - wsi).astype(np.longdouble)
-    y = (t * np.longdouble(fa) + np.longdouble(fb)).astype(np.float32)
-    return np.clip(y, np.float32(0), np.float32(255)).astype(np.int64)
+    """fast16f: fma(x - ws, fa, 1.5 * 2^23) rounds the exact (x - ws) * fa to the nearest integer,
+    ties to even (ulp 1 in [2^23, 2^24)); the bits minus 0x4B400000 clamped to [0, 255].  Exact
+    in Python integers: fa = m * 2^e with an integer m, so (x - ws) * fa = (x - ws) * m / 2^-e."""
+    assert fb == np.float32(12582912.0)
+    m, e = np.frexp(np.float64(fa))                 # fa = m * 2^e, 0.5 <= m < 1
+    mi, s = int(m * 2 ** 24), 24 - int(e)           # fa = mi / 2^s exactly (f32: 24-bit significand)
+    t = (X - wsi) * mi
+    if s <= 0:
+        n = t << -s
+    else:
+        q, r = np.divmod(t, 1 << s)                 # floor division, 0 <= r < 2^s
+        half = 1 << (s - 1)
+        n = q + ((r > half) | ((r == half) & ((q & 1) == 1)))
+    return np.clip(n, 0, 255).astype(np.int64)
 
 
 def windows(seed, n):
@@ -57,7 +65,6 @@ def windows(seed, n):
     return out
 
 
-@pytest.mark.skipif(np.finfo(np.longdouble).nmant < 63, reason="needs x87 extended precision")
 def test_accepted_parameters_are_exact_on_every_pixel_value():
     accepted = 0
     ws_list = windows(7, 300)
