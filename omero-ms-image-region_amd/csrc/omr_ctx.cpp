@@ -165,7 +165,10 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     if (const char* v = std::getenv("OMR_K3R")) c->k3r = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_PNG_DEVICE_D3")) c->png_device_d3 = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_F1_F32")) c->f1_f32 = std::atoi(v) != 0;
-    if (const char* v = std::getenv("OMR_K2_EVAL_CPT")) c->k2_eval_cpt = std::atoi(v) == 4 ? 4 : 2;
+    if (const char* v = std::getenv("OMR_K2_EVAL_CPT")) {   // 2 / 4 plain grid stride, -1 / -2 pipelined
+        const int k = std::atoi(v);
+        c->k2_eval_cpt = (k == 4 || k == 2 || k == -1) ? k : -2;
+    }
     *out = c;
     return OMR_OK;
 }

@@ -122,7 +122,7 @@ struct Ctx {
     bool f1_f32 = true;              // F1's Fast16 quantize in f32 when proven exact (OMR_F1_F32=0: f64)
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
-    int k2_eval_cpt = 2;
+    int k2_eval_cpt = -2;            // float / 32-bit K2: -1 / -2 pipelined chunks per lane, 2 / 4 plain
     // kernel timing (omr_ctx_enable_kernel_timing)
     bool timing = false;
     struct Timed { hipEvent_t start, stop; int kind; };

@@ -346,18 +346,145 @@ __device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_con
     }
 }
 
+// One chunk of 8/16 bytes per channel (loaded, or NA == 0: loaded here channel by channel):
+// quantize + codomain + composite, then the ARGB store (flips folded into the address).
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE>
+__device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)[NA > 0 ? NA : 1], uint32_t tile,
+                                         uint32_t row, uint32_t cc, const uint32_t* s_contrib) {
+    constexpr int NL = NA > 0 ? NA : 1;
+    const int na = NA > 0 ? NA : A.n_active;
+    const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
+    const int W = A.width, H = A.height;
+    auto plane_base = [&](uint32_t t, int a) -> const uint8_t* {
+        if (A.strided) return A.sbase + (int64_t)t * A.tile_stride + (int64_t)A.ch[a].index * A.chan_stride;
+        return static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
+    };
+    const uint32_t* const s_thr = s_contrib + na * 256;
+    const uint16_t* const s_bkt = reinterpret_cast<const uint16_t*>(s_thr + na * 256);
+    const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
+    uint32_t acc[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) acc[j] = 0;
+    uint32_t err_bits = 0;
+    bool err = false;
+#pragma unroll
+    for (int a = 0; a < (NA > 0 ? NA : kMaxActive); ++a) {
+        if (NA == 0 && a >= na) break;
+        const K2Chan& p = A.ch[a];
+        Chunk<BPP, VEC>& c = ckk[NA > 0 ? a : 0];
+        if constexpr (NA == 0) {
+            load_chunk<BPP, VEC>(c, plane_base(tile, a) + in_off);
+        }
+        const uint32_t* tab = s_contrib + a * 256;
+        if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
+            if (MODE == kK2Thresh || p.mode == kModeThresh) {          // uniform: bucket, then the few thresholds in it
+                const uint32_t* T = s_thr + a * 256;
+                const uint16_t* Bk = s_bkt + a * kBuckets;
+                const uint32_t meta = T[0];
+                const uint32_t cmax = meta & 0xFFu, cnan = (meta >> 8) & 0xFFu;
+                const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
+                const uint32_t sh = bucket_shift(k1 > k0 ? k1 - k0 : 0u);
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    uint32_t raw = c.dw[j];
+                    if constexpr (BE) raw = bswap32(raw);
+                    const uint32_t key = raw_key<PT>(raw);
+                    const bool inr = key >= k0 && key < k1;
+                    const uint32_t e = Bk[min((key - k0) >> sh, (uint32_t)kBuckets - 1)];
+                    uint32_t base = inr ? (e & 0xFFu) : (key >= k1 ? cmax : 0u);
+                    uint32_t len = inr ? (e >> 8) : 0u;
+                    while (len > 0) {
+                        const uint32_t half = len >> 1;
+                        const bool le = T[base + half + 1] <= key;
+                        base = le ? base + half + 1 : base;
+                        len = le ? len - half - 1 : half;
+                    }
+                    if constexpr (PT == OMR_PIXELS_FLOAT) base = ((raw & 0x7FFFFFFFu) > 0x7F800000u) ? cnan : base;
+                    acc[j] += tab[base];
+                    if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
+                }
+                continue;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            uint32_t e;
+            if constexpr (MODE == kK2Table8) {
+                e = tab[byte_index<VEC>(c, j)];
+                err_bits |= e;
+                e &= ~kErrBit;
+            } else if constexpr (MODE == kK2Fast16 || MODE == kK2Linear16 || MODE == kK2Mixed16) {
+                const int x = pixel16<VEC, BE, SIGNED>(c, j);
+                if (p.check) err |= (x < p.gmin) | (x > p.gmax);
+                uint32_t v;
+                if constexpr (MODE == kK2Fast16) {
+                    v = fast16(x, p);
+                } else if (MODE == kK2Linear16 || p.mode == kModeLinear16) {
+                    v = linear16(x, p, cds, cds8, cde8);
+                } else {
+                    const int xi = min(max(x, p.gmin), p.gmax);
+                    v = A.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
+                }
+                e = tab[v];
+            } else if constexpr (MODE == kK2Eval) {
+                const double x = pixel_double<BPP, VEC, BE, PT>(c, j);
+                e = tab[eval_q(x, A.plan->ch[a], A.cd_start, A.cd_end)];
+            } else {
+                e = 0;   // kK2Thresh: every channel took the threshold path above
+            }
+            acc[j] += e;
+            if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
+        }
+    }
+    if ((err_bits & kErrBit) || err) {
+        atomicOr(A.flag, 1);
+        if (A.status) A.status[tile] = OMR_QUANTIZATION;
+    }
+    uint32_t px[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t c = clamp_fields(acc[j]);
+        px[j] = 0xFF000000u | ((c >> 4) & 0xFF0000u) | ((c >> 2) & 0xFF00u) | (c & 0xFFu);
+    }
+    const uint32_t orow = A.flip_v ? (uint32_t)H - 1 - row : row;
+    const uint32_t ocol = A.flip_h ? (uint32_t)W - (cc + 1) * VEC : cc * VEC;
+    OMR_GLOBAL uint32_t* o = gstore_ptr<uint32_t>(A.out + (int64_t)tile * W * H + (int64_t)orow * W + ocol);
+    if (A.flip_h) {
+#pragma unroll
+        for (int j = 0; j < VEC / 2; ++j) { const uint32_t t = px[j]; px[j] = px[VEC - 1 - j]; px[VEC - 1 - j] = t; }
+    }
+    if constexpr (VEC % 4 == 0) {
+#pragma unroll
+        for (int j = 0; j < VEC; j += 4)
+        {
+            const u32x4 v = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
+            if (OMR_K2_NT && BPP * NL >= 4 && A.nt_store) __builtin_nontemporal_store(v, (OMR_GLOBAL u32x4*)(o + j));
+            else *(OMR_GLOBAL u32x4*)(o + j) = v;
+        }
+    } else if constexpr (VEC == 2) {
+        *(OMR_GLOBAL u32x2*)(o) = u32x2{px[0], px[1]};
+    } else {
+        o[0] = px[0];
+    }
+}
+
 // The chunks of work block wb: [wb*256*CPT, (wb+1)*256*CPT), thread t the chunks
 // wb*256*CPT + k*256 + t.  Every channel load of every chunk is issued before any compute
 // (CPT*NA 16-B loads in flight per lane); plain loads (measured faster than non-temporal here,
 // tools/probe_stream.hip).  NA == 0: runtime channel count, one chunk per thread, clamp per add.
 // STAGE: load the LDS tables here, after the pixel loads are in flight (one-pass grids).
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, bool STAGE, int CPTT>
-__device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* s_contrib) {
-    constexpr int CPT = NA > 0 ? CPTT : 1;
+// The chunks of a work block in flight: positions and (NA > 0) every channel's pixels.
+template <int BPP, int VEC, int NA, int CPT>
+struct K2Batch {
+    uint32_t gk[CPT], tk[CPT], rk[CPT], ck[CPT];
+    Chunk<BPP, VEC> c[CPT][NA > 0 ? NA : 1];
+};
+
+// Positions of work block wb's chunks for this thread, then (NA > 0) every plane pointer (scalar
+// when the block sits in one tile) and every pixel load back to back: no wait between them.
+template <int BPP, int VEC, int NA, int CPT>
+__device__ __forceinline__ void k2_issue(const K2Args& A, uint32_t wb, K2Batch<BPP, VEC, NA, CPT>& B) {
     constexpr int NL = NA > 0 ? NA : 1;
-    const int na = NA > 0 ? NA : A.n_active;
-    const int cds = A.cd_start, cds8 = A.cds8, cde8 = A.cde8;
-    const int W = A.width, H = A.height;
     const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
     const uint32_t g0 = wb * (kBlock * CPT);
     uint32_t btile = 0;
@@ -366,39 +493,57 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
         if (A.strided) return A.sbase + (int64_t)t * A.tile_stride + (int64_t)A.ch[a].index * A.chan_stride;
         return static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
     };
-    const uint8_t* ubase[NL];
-    if (NA > 0 && A.tile_uniform) {
-#pragma unroll
-        for (int a = 0; a < NL; ++a) ubase[a] = plane_base(btile, a);
-    }
-    uint32_t gk[CPT], tk[CPT], rk[CPT], ck_[CPT];
-    Chunk<BPP, VEC> ck[CPT][NL];
-    const uint8_t* pb[CPT][NL];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-        gk[k] = g0 + k * kBlock + threadIdx.x;
-        const uint32_t g = min(gk[k], A.total - 1);   // tail lanes load a valid chunk, store nothing
+        B.gk[k] = g0 + k * kBlock + threadIdx.x;
+        const uint32_t g = min(B.gk[k], A.total - 1);   // tail lanes load a valid chunk, store nothing
         const uint32_t t = A.tile_uniform ? btile : fdiv(g, A.cpt);
         const uint32_t rem = g - t * cptd;
         const uint32_t r = fdiv(rem, A.cpr);
-        tk[k] = t;
-        rk[k] = r;
-        ck_[k] = rem - r * cpr;
+        B.tk[k] = t;
+        B.rk[k] = r;
+        B.ck[k] = rem - r * cpr;
     }
     if constexpr (NA > 0) {
-        // 1) every plane pointer (scalar when the block sits in one tile), 2) every pixel load
-        //    back to back: no wait between the channel loads.
+        const uint8_t* ubase[NL];
+        if (A.tile_uniform) {
+#pragma unroll
+            for (int a = 0; a < NL; ++a) ubase[a] = plane_base(btile, a);
+        }
+        const uint8_t* pb[CPT][NL];
 #pragma unroll
         for (int k = 0; k < CPT; ++k)
 #pragma unroll
-            for (int a = 0; a < NA; ++a) pb[k][a] = A.tile_uniform ? ubase[a] : plane_base(tk[k], a);
+            for (int a = 0; a < NA; ++a) pb[k][a] = A.tile_uniform ? ubase[a] : plane_base(B.tk[k], a);
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
-            const int64_t off = ((int64_t)rk[k] * A.row_stride + (int64_t)ck_[k] * VEC) * BPP;
+            const int64_t off = ((int64_t)B.rk[k] * A.row_stride + (int64_t)B.ck[k] * VEC) * BPP;
 #pragma unroll
-            for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(ck[k][a], pb[k][a] + off);
+            for (int a = 0; a < NA; ++a) load_chunk<BPP, VEC>(B.c[k][a], pb[k][a] + off);
         }
     }
+}
+
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, int CPT>
+__device__ __forceinline__ void k2_finish(const K2Args& A, K2Batch<BPP, VEC, NA, CPT>& B, const uint32_t* s_contrib) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+        if (B.gk[k] >= A.total) continue;
+        k2_chunk<BPP, VEC, BE, SIGNED, PT, NA, MODE>(A, B.c[k], B.tk[k], B.rk[k], B.ck[k], s_contrib);
+    }
+}
+
+// The chunks of work block wb: [wb*256*CPT, (wb+1)*256*CPT), thread t the chunks
+// wb*256*CPT + k*256 + t.  Every channel load of every chunk is issued before any compute
+// (CPT*NA 16-B loads in flight per lane); plain loads (measured faster than non-temporal here).
+// NA == 0: runtime channel count, one chunk per thread, clamp per add.
+// STAGE: load the LDS tables here, after the pixel loads are in flight (one-pass grids).
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, bool STAGE, int CPTT>
+__device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* s_contrib) {
+    constexpr int CPT = NA > 0 ? CPTT : 1;
+    const int na = NA > 0 ? NA : A.n_active;
+    K2Batch<BPP, VEC, NA, CPT> B;
+    k2_issue<BPP, VEC, NA, CPT>(A, wb, B);
     if constexpr (STAGE) {
         // tables -> LDS, issued after the pixel loads so their latencies overlap.  Small launches
         // (CPTT 1, integer modes) build them from the plan here instead: no K1 launch per request.
@@ -410,118 +555,30 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
         }
         __syncthreads();
     }
-    uint32_t* const s_thr = s_contrib + na * 256;
-    const uint16_t* const s_bkt = reinterpret_cast<const uint16_t*>(s_thr + na * 256);
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-        const uint32_t g = gk[k];
-        if (g >= A.total) continue;
-        const uint32_t tile = tk[k], row = rk[k], cc = ck_[k];
-        const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
-        uint32_t acc[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) acc[j] = 0;
-        uint32_t err_bits = 0;
-        bool err = false;
-#pragma unroll
-        for (int a = 0; a < (NA > 0 ? NA : kMaxActive); ++a) {
-            if (NA == 0 && a >= na) break;
-            const K2Chan& p = A.ch[a];
-            Chunk<BPP, VEC>& c = ck[k][NA > 0 ? a : 0];
-            if constexpr (NA == 0) {
-                load_chunk<BPP, VEC>(c, plane_base(tile, a) + in_off);
-            }
-            const uint32_t* tab = s_contrib + a * 256;
-            if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
-                if (MODE == kK2Thresh || p.mode == kModeThresh) {          // uniform: bucket, then the few thresholds in it
-                    const uint32_t* T = s_thr + a * 256;
-                    const uint16_t* Bk = s_bkt + a * kBuckets;
-                    const uint32_t meta = T[0];
-                    const uint32_t cmax = meta & 0xFFu, cnan = (meta >> 8) & 0xFFu;
-                    const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
-                    const uint32_t sh = bucket_shift(k1 > k0 ? k1 - k0 : 0u);
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j) {
-                        uint32_t raw = c.dw[j];
-                        if constexpr (BE) raw = bswap32(raw);
-                        const uint32_t key = raw_key<PT>(raw);
-                        const bool inr = key >= k0 && key < k1;
-                        const uint32_t e = Bk[min((key - k0) >> sh, (uint32_t)kBuckets - 1)];
-                        uint32_t base = inr ? (e & 0xFFu) : (key >= k1 ? cmax : 0u);
-                        uint32_t len = inr ? (e >> 8) : 0u;
-                        while (len > 0) {
-                            const uint32_t half = len >> 1;
-                            const bool le = T[base + half + 1] <= key;
-                            base = le ? base + half + 1 : base;
-                            len = le ? len - half - 1 : half;
-                        }
-                        if constexpr (PT == OMR_PIXELS_FLOAT) base = ((raw & 0x7FFFFFFFu) > 0x7F800000u) ? cnan : base;
-                        acc[j] += tab[base];
-                        if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
-                    }
-                    continue;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) {
-                uint32_t e;
-                if constexpr (MODE == kK2Table8) {
-                    e = tab[byte_index<VEC>(c, j)];
-                    err_bits |= e;
-                    e &= ~kErrBit;
-                } else if constexpr (MODE == kK2Fast16 || MODE == kK2Linear16 || MODE == kK2Mixed16) {
-                    const int x = pixel16<VEC, BE, SIGNED>(c, j);
-                    if (p.check) err |= (x < p.gmin) | (x > p.gmax);
-                    uint32_t v;
-                    if constexpr (MODE == kK2Fast16) {
-                        v = fast16(x, p);
-                    } else if (MODE == kK2Linear16 || p.mode == kModeLinear16) {
-                        v = linear16(x, p, cds, cds8, cde8);
-                    } else {
-                        const int xi = min(max(x, p.gmin), p.gmax);
-                        v = A.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
-                    }
-                    e = tab[v];
-                } else if constexpr (MODE == kK2Eval) {
-                    const double x = pixel_double<BPP, VEC, BE, PT>(c, j);
-                    e = tab[eval_q(x, A.plan->ch[a], A.cd_start, A.cd_end)];
-                } else {
-                    e = 0;   // kK2Thresh: every channel took the threshold path above
-                }
-                acc[j] += e;
-                if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
-            }
-        }
-        if ((err_bits & kErrBit) || err) {
-            atomicOr(A.flag, 1);
-            if (A.status) A.status[tile] = OMR_QUANTIZATION;
-        }
-        uint32_t px[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            const uint32_t c = clamp_fields(acc[j]);
-            px[j] = 0xFF000000u | ((c >> 4) & 0xFF0000u) | ((c >> 2) & 0xFF00u) | (c & 0xFFu);
-        }
-        const uint32_t orow = A.flip_v ? (uint32_t)H - 1 - row : row;
-        const uint32_t ocol = A.flip_h ? (uint32_t)W - (cc + 1) * VEC : cc * VEC;
-        OMR_GLOBAL uint32_t* o = gstore_ptr<uint32_t>(A.out + (int64_t)tile * W * H + (int64_t)orow * W + ocol);
-        if (A.flip_h) {
-#pragma unroll
-            for (int j = 0; j < VEC / 2; ++j) { const uint32_t t = px[j]; px[j] = px[VEC - 1 - j]; px[VEC - 1 - j] = t; }
-        }
-        if constexpr (VEC % 4 == 0) {
-#pragma unroll
-            for (int j = 0; j < VEC; j += 4)
-            {
-                const u32x4 v = u32x4{px[j], px[j + 1], px[j + 2], px[j + 3]};
-                if (OMR_K2_NT && BPP * NL >= 4 && A.nt_store) __builtin_nontemporal_store(v, (OMR_GLOBAL u32x4*)(o + j));
-                else *(OMR_GLOBAL u32x4*)(o + j) = v;
-            }
-        } else if constexpr (VEC == 2) {
-            *(OMR_GLOBAL u32x2*)(o) = u32x2{px[0], px[1]};
-        } else {
-            o[0] = px[0];
-        }
+    k2_finish<BPP, VEC, BE, SIGNED, PT, NA, MODE, CPT>(A, B, s_contrib);
+}
+
+// Float / 32-bit modes, software-pipelined grid stride (round 3): the pixel loads of the
+// workgroup's next work block are issued before the current block is quantized, so every lane
+// keeps NA * CPT 16-byte loads in flight through the compute (the plain grid stride above waits
+// out the HBM latency once per block, then computes with nothing in flight).
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, int CPT>
+__global__ void __launch_bounds__(kBlock) k_render_pipe(const K2Args A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
+    K2Batch<BPP, VEC, NA, CPT> b0, b1;
+    uint32_t wb = blockIdx.x;
+    if (wb < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, wb, b0);
+    k2_stage_tables<MODE, BPP>(A, s_contrib, NA);                 // behind the first loads
+    __syncthreads();
+    while (wb < A.n_work) {                                       // uniform; two blocks per trip
+        const uint32_t w1 = wb + gridDim.x;
+        if (w1 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w1, b1);
+        k2_finish<BPP, VEC, BE, SIGNED, PT, NA, MODE, CPT>(A, b0, s_contrib);
+        if (w1 >= A.n_work) break;
+        const uint32_t w2 = w1 + gridDim.x;
+        if (w2 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w2, b0);
+        k2_finish<BPP, VEC, BE, SIGNED, PT, NA, MODE, CPT>(A, b1, s_contrib);
+        wb = w2;
     }
 }
 
@@ -719,6 +776,21 @@ template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s, int cpt = kCPT) {
     const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
     if constexpr (BPP == 4 && VEC > 1 && (MODE == kK2Thresh || MODE == kK2Eval)) {
+        // software-pipelined grid stride (k_render_pipe; cpt -1: one chunk per lane and block,
+        // -2: two), the default for 1..4 channels
+        if (cpt < 0) {
+            switch (na * 2 + (cpt == -2 ? 1 : 0)) {
+            case 2: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 1, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 3: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 1, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 4: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 2, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 5: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 2, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 6: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 7: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 3, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 8: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 4, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 9: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 4, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            default: break;
+            }
+        }
         // grid-stride float / 32-bit modes, OMR_K2_EVAL_CPT=4: 4 chunks per lane (12 loads in
         // flight at 3 channels; measured slower than kCPT on C5)
         if (cpt == 4) {
@@ -956,7 +1028,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.cde8 = pp.plan.cd_end & 0xFF;
     // chunks per lane: kCPT (the float / 32-bit vector path: the context's k2_eval_cpt), 1 for
     // small launches and the runtime-channel-count kernels
-    const int cpt_thread = (na >= 1 && na <= 4 && !small) ? (bpp == 4 && aligned ? ctx->k2_eval_cpt : kCPT) : 1;
+    // (negative: the software-pipelined float kernel, k_render_pipe, at |cpt| chunks)
+    const int cpt_sel = (na >= 1 && na <= 4 && !small) ? (bpp == 4 && aligned ? ctx->k2_eval_cpt : kCPT) : 1;
+    const int cpt_thread = cpt_sel < 0 ? -cpt_sel : cpt_sel;
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.nt_store = ctx->k2_nt_store ? 1 : 0;
     a.total = (uint32_t)total;
@@ -1000,7 +1074,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         switch (bpp) {
         case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
         case 2: e = launch_render_be<2, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
-        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
+        case 4: e = launch_render_be<4, 4>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_sel); break;
         default: e = launch_render_be<8, 2>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
         }
     } else {
