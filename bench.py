@@ -306,32 +306,42 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
     return res
 
 
-VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r02", "jpeg_valu_pmc.json")
-VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2   # 1,024 SIMD-32s, a wave64 VALU op per 2 cycles
+VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03", "jpeg_valu_pmc.json")
+VALU_PEAK_ISSUE_CYCLES_PER_S = 256 * 4 * 2.4e9   # 1,024 SIMD-32s at 2.4 GHz
+# issue cycles of one wave64 VALU instruction: 2 on a SIMD-32; f64 add / mul / fma issue at half
+# the f32 rate and transcendentals (v_exp / v_log / v_sqrt / v_rcp ...) at half the issue rate
+# (MI355X_MICROARCH.md, vector-instruction issue cost), so they are charged 4
+VALU_CYCLES = 2.0
+VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                      "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32")
 
 
 def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
-    """B1 / F1 / B3 are VALU-issue-bound: achieved = VALU wave-instructions per
-    launch (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r02.sh) x MCUs
-    / the kernel's measured average duration; peak = every SIMD issuing one wave64 VALU
-    instruction per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, v_fma_f32 wave64 throughput)."""
+    """B1 / F1 / B3 are VALU-issue-bound: achieved = VALU issue cycles per launch
+    (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r03.sh, at 2 cycles,
+    plus 2 more for every f64 and transcendental instruction) x MCUs / the kernel's measured average
+    duration; peak = every SIMD issuing every cycle at 2.4 GHz."""
     case = "c1" if name.startswith("c1") else "c2"
     try:
         with open(VALU_PMC) as fh:
             pmc = json.load(fh).get(case, {})
     except (OSError, ValueError):
         return None
-    out = {"bound": "valu", "unit": "wave-instr/s", "peak": VALU_PEAK_WAVE_INSTR_PER_S,
+    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S,
            "source": os.path.relpath(VALU_PMC, os.path.dirname(os.path.abspath(__file__))) + f" [{case}]"}
     for label, key, ms in (("B1_fdct", "k_jpeg_fdct_batch", j1_ms), ("F1_render_fdct", "k_jpeg_render_fdct", f1_ms),
                            ("B3_huffman", "k_jpeg_huff_thread", j3_ms)):
         k = next((k for k in pmc if key in k), None)
         if k is None or not ms:
             continue
-        ipm = pmc[k]["SQ_INSTS_VALU_per_mcu"]
-        ach = ipm * mcus / (ms * 1e-3)
-        out[label] = {"valu_instr_per_mcu": round(ipm, 1), "achieved": round(ach, 1),
-                      "frac": round(ach / VALU_PEAK_WAVE_INSTR_PER_S, 4), "avg_launch_ms": round(ms, 5)}
+        cnt, per = pmc[k]["counters"], pmc[k]["mcus_per_launch"]
+        ipm = cnt["SQ_INSTS_VALU"] / per
+        slow = sum(cnt.get(c, 0.0) for c in VALU_SLOW_COUNTERS) / per
+        cyc = VALU_CYCLES * (ipm + slow)
+        ach = cyc * mcus / (ms * 1e-3)
+        out[label] = {"valu_instr_per_mcu": round(ipm, 1), "f64_and_transcendental_per_mcu": round(slow, 2),
+                      "issue_cycles_per_mcu": round(cyc, 1), "achieved": round(ach, 1),
+                      "frac": round(ach / VALU_PEAK_ISSUE_CYCLES_PER_S, 4), "avg_launch_ms": round(ms, 5)}
     return out
 
 
