@@ -100,6 +100,44 @@ __constant__ HuffTab c_huff[4] = {make_huff(kBitsDcL, kValDc), make_huff(kBitsAc
                                   make_huff(kBitsDcC, kValDc), make_huff(kBitsAcC, kValAcC)};
 __constant__ ZzInv c_zzinv = make_zzinv();
 
+// B2a's AC length table, built at compile time: code length of (zero run r < 64, magnitude
+// category nb) with the r >> 4 ZRL codes folded in, at r * 16 + nb; 0 for nb == 0 (a zero
+// coefficient adds nothing).  [0] luma, [1] chroma; 1 KiB each, copied to LDS with 16-B loads.
+struct AcLen {
+    uint8_t v[2][1024];
+};
+constexpr AcLen make_aclen() {
+    AcLen a{};
+    const HuffTab t[2] = {make_huff(kBitsAcL, kValAcL), make_huff(kBitsAcC, kValAcC)};
+    for (int c = 0; c < 2; ++c)
+        for (int i = 0; i < 1024; ++i) {
+            const int r = i >> 4, nb = i & 15;
+            a.v[c][i] = nb ? (uint8_t)((r >> 4) * t[c].size[0xF0] + t[c].size[((r & 15) << 4) | nb]) : 0;
+        }
+    return a;
+}
+__constant__ AcLen c_aclen = make_aclen();
+
+// B3's tables, built at compile time and copied to LDS with 16-byte loads: the AC codes packed as
+// size << 16 | code with the size-0 entries (run, 0) — EOB and ZRL come from c_huff — zeroed, so
+// a zero coefficient codes as zero bits with no select; the DC codes and sizes (12 categories).
+struct B3Tabs {
+    uint32_t ac[2][256];
+    uint32_t dc[2][16];    // size << 16 | code
+};
+constexpr B3Tabs make_b3tabs() {
+    B3Tabs b{};
+    const HuffTab ac[2] = {make_huff(kBitsAcL, kValAcL), make_huff(kBitsAcC, kValAcC)};
+    const HuffTab dc[2] = {make_huff(kBitsDcL, kValDc), make_huff(kBitsDcC, kValDc)};
+    for (int t = 0; t < 2; ++t) {
+        for (int i = 0; i < 256; ++i)
+            b.ac[t][i] = (i & 15) == 0 ? 0u : ((uint32_t)ac[t].size[i] << 16) | ac[t].code[i];
+        for (int i = 0; i < 16; ++i) b.dc[t][i] = ((uint32_t)dc[t].size[i] << 16) | dc[t].code[i];
+    }
+    return b;
+}
+__constant__ B3Tabs c_b3tabs = make_b3tabs();
+
 struct QTabs {
     uint16_t q[2][64];  // natural order
     uint32_t m[2][64];  // ceil(2^32 / (8 q)): B1's reciprocal quantiser (set_recips)
@@ -1168,22 +1206,26 @@ struct B2aArgs {
 // float, sign-independent (two instructions instead of abs + clz + a zero select).
 __device__ __forceinline__ int mag_bits(int c) { return __builtin_amdgcn_frexp_expf((float)c); }
 
+// (Staging the workgroup's 32 KiB of coefficients through LDS with coalesced loads, rows of
+// 9 x 16 B, measured 2.4x slower than each lane loading its own 128 B: 121 vs 48 us per 64 C2
+// tiles, profiles/r03/ab_jpeg_b2a_variants.txt.)
 __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     __shared__ uint8_t s_dc[2][16];
-    __shared__ uint8_t s_acsz[2][256];   // AC code lengths, size-0 entries (EOB, ZRL, unused) 0
+    // code length of (run r < 64, category nb) with the r >> 4 ZRL codes folded in, indexed by
+    // r * 16 + nb; 0 for nb == 0 (a zero coefficient adds nothing)
+    __shared__ __attribute__((aligned(16))) uint8_t s_len[2][1024];
     __shared__ uint32_t sw[16];
+    const int tile = blockIdx.y, b0 = blockIdx.x * kGrp, b = b0 + threadIdx.x;
     if (threadIdx.x < 32) s_dc[threadIdx.x >> 4][threadIdx.x & 15] = c_huff[2 * (threadIdx.x >> 4)].size[threadIdx.x & 15];
-    for (int i = threadIdx.x; i < 512; i += kGrp)
-        s_acsz[i >> 8][i & 255] = (i & 15) == 0 ? 0 : c_huff[1 + 2 * (i >> 8)].size[i & 255];
+    if (threadIdx.x < 128)
+        reinterpret_cast<uint4*>(&s_len[0][0])[threadIdx.x] = reinterpret_cast<const uint4*>(&c_aclen.v[0][0])[threadIdx.x];
     __syncthreads();
-    const int tile = blockIdx.y, b = blockIdx.x * kGrp + threadIdx.x;
     uint32_t bits = 0;
     if (b < A.nb) {
         const int64_t gb = (int64_t)tile * A.nb + b;
-        const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
         uint4 q[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = src[i];
+        for (int i = 0; i < 8; ++i) q[i] = reinterpret_cast<const uint4*>(A.coefs + gb * 64)[i];
         const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
         const int pb = prev_block_in_tile(b);
         const uint32_t rb = blk[b];
@@ -1191,20 +1233,28 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
         const int nbd = mag_bits(d);
         const int t = (b % 6) < 4 ? 0 : 1;
         bits = s_dc[t][nbd] + nbd;
-        const uint32_t zrl = c_huff[1 + 2 * t].size[0xF0], eob = c_huff[1 + 2 * t].size[0x00];
-        const uint8_t* sz = s_acsz[t];
+        const uint8_t* len = s_len[t];
         uint32_t r16 = 0;                                  // zero run before coefficient k, times 16
+        // eight coefficients at a time: their table indices first (the run chain is VALU only),
+        // then the eight LDS reads in flight together
 #pragma unroll
-        for (int k = 1; k < 64; ++k) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
-            const int c = (k & 1) ? (int)(int16_t)(w[(k >> 1) & 3] >> 16) : (int)(int16_t)(w[(k >> 1) & 3] & 0xFFFF);
-            const int nb = mag_bits(c);
-            // c == 0: nb == 0 and the (run, 0) entry is 0, so only the ZRL term needs the select
-            const uint32_t len = sz[(r16 & 0xF0) | nb] + nb + (c ? (r16 >> 8) * zrl : 0u);
-            bits += len;
-            r16 = c ? 0u : r16 + 16;
+        for (int k0 = 0; k0 < 64; k0 += 8) {
+            uint32_t idx[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = k0 + j;
+                if (k == 0) { idx[j] = 0; continue; }
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
+                const int c = (k & 1) ? (int)(int16_t)(w[(k >> 1) & 3] >> 16) : (int)(int16_t)(w[(k >> 1) & 3] & 0xFFFF);
+                const int nb = mag_bits(c);
+                idx[j] = r16 | nb;
+                bits += nb;
+                r16 = nb ? 0u : r16 + 16;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bits += (k0 + j) ? len[idx[j]] : 0u;   // zero coefficient: entry 0
         }
-        if (r16) bits += eob;                              // EOB after the last non-zero
+        if (r16) bits += c_huff[1 + 2 * t].size[0x00];     // EOB after the last non-zero
         A.bits[gb] = (uint16_t)bits;
     }
     const uint32_t total = block_reduce_sum(bits, sw);
@@ -1280,17 +1330,13 @@ struct B3Args {
 // neighbours are ORed in.
 
 __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
-    __shared__ HuffLds h;
-    // AC tables packed as size << 16 | code, with the size-0 entries (run, 0) — EOB and ZRL are
-    // taken from c_huff directly — zeroed: a zero coefficient then codes as zero bits with no
-    // select in the coefficient loop
-    __shared__ uint32_t s_ac[2][256];
+    // AC tables packed as size << 16 | code (size-0 entries zeroed: a zero coefficient codes as
+    // zero bits with no select in the coefficient loop), then the DC tables
+    __shared__ __attribute__((aligned(16))) B3Tabs s_t;
     __shared__ uint32_t s_words[kB3LdsWords];
     __shared__ uint32_t sw[16];
-    load_huff_lds(h);
-    for (int i = threadIdx.x; i < 512; i += blockDim.x)
-        s_ac[i >> 8][i & 255] = (i & 15) == 0 ? 0u
-            : ((uint32_t)c_huff[1 + 2 * (i >> 8)].size[i & 255] << 16) | c_huff[1 + 2 * (i >> 8)].code[i & 255];
+    if (threadIdx.x < (int)(sizeof(B3Tabs) / 16))
+        reinterpret_cast<uint4*>(&s_t)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_b3tabs)[threadIdx.x];
     const int tile = blockIdx.y;
     const int b = blockIdx.x * kGrp + threadIdx.x;
     const int64_t gb = (int64_t)tile * A.nb + b;
@@ -1341,12 +1387,13 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
             return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
         };
         const int kk = b % 6;
-        const int td = kk < 4 ? 0 : 2, ta = kk < 4 ? 0 : 1;
+        const int ta = kk < 4 ? 0 : 1;
         {
             int d = coef(0) - pred, d2 = d;
             if (d < 0) { d = -d; d2--; }
             const int nbits = d ? 32 - __clz(d) : 0;
-            put(((uint32_t)h.code[td][nbits] << nbits) | ((uint32_t)d2 & ((1u << nbits) - 1)), h.size[td][nbits] + nbits);
+            const uint32_t dcc = s_t.dc[ta][nbits];
+            put(((dcc & 0xFFFF) << nbits) | ((uint32_t)d2 & ((1u << nbits) - 1)), (int)(dcc >> 16) + nbits);
         }
         const uint32_t zrl = ((uint32_t)c_huff[1 + 2 * ta].size[0xF0] << 16) | c_huff[1 + 2 * ta].code[0xF0];
         const uint32_t eob = ((uint32_t)c_huff[1 + 2 * ta].size[0x00] << 16) | c_huff[1 + 2 * ta].code[0x00];
@@ -1361,7 +1408,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
                 if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
             }
             const int nbits = mag_bits(c);                         // 0 for c == 0
-            const uint32_t cs = s_ac[ta][((r & 15) << 4) | nbits];
+            const uint32_t cs = s_t.ac[ta][((r & 15) << 4) | nbits];
             const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
             put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
             r = nzk ? 0 : r + 1;
