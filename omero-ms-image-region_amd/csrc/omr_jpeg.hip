@@ -102,9 +102,12 @@ __constant__ ZzInv c_zzinv = make_zzinv();
 
 // B2a's AC length table, built at compile time: code length of (zero run r < 64, magnitude
 // category nb) with the r >> 4 ZRL codes folded in, at r * 16 + nb; 0 for nb == 0 (a zero
-// coefficient adds nothing).  [0] luma, [1] chroma; 1 KiB each, copied to LDS with 16-B loads.
+// coefficient adds nothing).  Entries with ZRL codes also carry 0x800: a block's sum is then its
+// bit count (< 2^11) plus 0x800 per ZRL-prefixed coefficient, so B2a flags B3's ZRL path for free.
+// [0] luma, [1] chroma; 2 KiB each, copied to LDS with 16-B loads.
+constexpr uint32_t kZrlFlag = 0x800;
 struct AcLen {
-    uint8_t v[2][1024];
+    uint16_t v[2][1024];
 };
 constexpr AcLen make_aclen() {
     AcLen a{};
@@ -112,7 +115,8 @@ constexpr AcLen make_aclen() {
     for (int c = 0; c < 2; ++c)
         for (int i = 0; i < 1024; ++i) {
             const int r = i >> 4, nb = i & 15;
-            a.v[c][i] = nb ? (uint8_t)((r >> 4) * t[c].size[0xF0] + t[c].size[((r & 15) << 4) | nb]) : 0;
+            a.v[c][i] = nb ? (uint16_t)((r >> 4) * t[c].size[0xF0] + t[c].size[((r & 15) << 4) | nb] +
+                                        (r >= 16 ? kZrlFlag : 0u)) : 0;
         }
     return a;
 }
@@ -1213,12 +1217,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     __shared__ uint8_t s_dc[2][16];
     // code length of (run r < 64, category nb) with the r >> 4 ZRL codes folded in, indexed by
     // r * 16 + nb; 0 for nb == 0 (a zero coefficient adds nothing)
-    __shared__ __attribute__((aligned(16))) uint8_t s_len[2][1024];
+    __shared__ __attribute__((aligned(16))) uint16_t s_len[2][1024];
     __shared__ uint32_t sw[16];
     const int tile = blockIdx.y, b0 = blockIdx.x * kGrp, b = b0 + threadIdx.x;
     if (threadIdx.x < 32) s_dc[threadIdx.x >> 4][threadIdx.x & 15] = c_huff[2 * (threadIdx.x >> 4)].size[threadIdx.x & 15];
-    if (threadIdx.x < 128)
-        reinterpret_cast<uint4*>(&s_len[0][0])[threadIdx.x] = reinterpret_cast<const uint4*>(&c_aclen.v[0][0])[threadIdx.x];
+    reinterpret_cast<uint4*>(&s_len[0][0])[threadIdx.x] = reinterpret_cast<const uint4*>(&c_aclen.v[0][0])[threadIdx.x];
     __syncthreads();
     uint32_t bits = 0;
     if (b < A.nb) {
@@ -1233,7 +1236,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
         const int nbd = mag_bits(d);
         const int t = (b % 6) < 4 ? 0 : 1;
         bits = s_dc[t][nbd] + nbd;
-        const uint8_t* len = s_len[t];
+        const uint16_t* len = s_len[t];
         uint32_t r16 = 0;                                  // zero run before coefficient k, times 16
         // eight coefficients at a time: their table indices first (the run chain is VALU only),
         // then the eight LDS reads in flight together
@@ -1255,7 +1258,8 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
             for (int j = 0; j < 8; ++j) bits += (k0 + j) ? len[idx[j]] : 0u;   // zero coefficient: entry 0
         }
         if (r16) bits += c_huff[1 + 2 * t].size[0x00];     // EOB after the last non-zero
-        A.bits[gb] = (uint16_t)bits;
+        A.bits[gb] = (uint16_t)bits;                       // bit count | 0x800 x ZRL-prefixed coefficients
+        bits &= kZrlFlag - 1;
     }
     const uint32_t total = block_reduce_sum(bits, sw);
     if (threadIdx.x == 0) A.gsum[(int64_t)tile * A.ngb + blockIdx.x] = total;
@@ -1341,7 +1345,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     const int b = blockIdx.x * kGrp + threadIdx.x;
     const int64_t gb = (int64_t)tile * A.nb + b;
     const bool live = b < A.nb;
-    const uint32_t mybits = live ? A.bits[gb] : 0u;
+    const uint32_t brec = live ? A.bits[gb] : 0u;
+    const uint32_t mybits = brec & (kZrlFlag - 1);
+    // no block of the wave has a zero run of 16+ before a non-zero (B2a's kZrlFlag multiples): the
+    // walk below drops its per-coefficient ZRL vote
+    const bool any_zrl = __ballot(brec >= kZrlFlag) != 0;
     uint32_t gtot;
     const uint32_t gbit0 = A.goff[(int64_t)tile * A.ngb + blockIdx.x];
     const uint32_t boff = gbit0 + block_exclusive_scan(mybits, sw, gtot);
@@ -1399,20 +1407,27 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         const uint32_t eob = ((uint32_t)c_huff[1 + 2 * ta].size[0x00] << 16) | c_huff[1 + 2 * ta].code[0x00];
         int r = 0;
         // Branch-free per coefficient: a zero contributes a zero-length code; runs of 16+ zeros
-        // before a non-zero (ZRL) take a wave-uniform, rarely entered branch.
+        // before a non-zero (ZRL) take a wave-uniform, rarely entered branch, checked only in
+        // waves where B2a saw one.
+        auto walk = [&](auto with_zrl) {
 #pragma unroll
-        for (int k = 1; k < 64; ++k) {
-            const int c = coef(k);
-            const bool nzk = c != 0;
-            if (k > 16 && __ballot(nzk && r > 15)) {                // r <= k - 1: no ZRL before k 17
-                if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
+            for (int k = 1; k < 64; ++k) {
+                const int c = coef(k);
+                const bool nzk = c != 0;
+                if constexpr (decltype(with_zrl)::value) {
+                    if (k > 16 && __ballot(nzk && r > 15)) {                // r <= k - 1: no ZRL before k 17
+                        if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
+                    }
+                }
+                const int nbits = mag_bits(c);                         // 0 for c == 0
+                const uint32_t cs = s_t.ac[ta][((r & 15) << 4) | nbits];
+                const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
+                put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
+                r = nzk ? 0 : r + 1;
             }
-            const int nbits = mag_bits(c);                         // 0 for c == 0
-            const uint32_t cs = s_t.ac[ta][((r & 15) << 4) | nbits];
-            const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
-            put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
-            r = nzk ? 0 : r + 1;
-        }
+        };
+        if (any_zrl) walk(std::true_type{});
+        else walk(std::false_type{});
         if (r > 0) put(eob & 0xFFFF, (int)(eob >> 16));                   // EOB
         if (nacc > 0) {                                                   // shared with the next block
             const uint32_t w = (uint32_t)(acc << (32 - nacc));
