@@ -1167,8 +1167,10 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         auto sat = [](int64_t v) { return (int32_t)std::min<int64_t>(std::max<int64_t>(v, INT32_MIN), INT32_MAX); };
         k.lo = sat((int64_t)c.lo + bias);
         k.hi = sat((int64_t)c.hi + bias);
-        k.gmin = c.gmin + bias;
-        k.gmax = c.gmax + bias;
+        // the biased LUT domain is compared with u16 pixels: clamp it to one step beyond the
+        // int16 range first, so that + 32768 cannot overflow and the compares are unchanged
+        k.gmin = bias ? (int32_t)std::min<int64_t>(std::max<int64_t>(c.gmin, -32768), 32768) + bias : c.gmin;
+        k.gmax = bias ? (int32_t)std::min<int64_t>(std::max<int64_t>(c.gmax, -32769), 32767) + bias : c.gmax;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
         F.any_check |= k.check;
         const bool wint = c.ws == std::floor(c.ws) && std::fabs(c.ws) < 1073741824.0;

@@ -171,6 +171,37 @@ def test_quantization_error_signed_lower_and_upper_bounds(ctx):
     assert files[0] == exp[0] and files[2] == exp[1]
 
 
+@pytest.mark.parametrize("gmin,gmax,bad", [(0.0, 2147483647.0, True), (-2147483648.0, 2147483647.0, False),
+                                            (-2147483648.0, -1.0, True), (40000.0, 2147483647.0, True),
+                                            (-2147483648.0, -40000.0, True)])
+def test_int16_extreme_lut_domain(ctx, gmin, gmax, bad):
+    """int16 channels whose LUT domain lies partly or wholly outside the type: the
+    fused kernel moves the domain by the int16 bias after clamping it to the type, so gmax near
+    INT32_MAX no longer wraps; the per-tile QuantizationException and every file agree with the
+    restatement (tiles 0 and 2 hold pixels below 0 / inside, tile 1 only positives)."""
+    w, h = 64, 48
+    rng = np.random.default_rng(23)
+    tiles = [[rng.integers(-3000, 3000, (h, w)).astype(np.int16) for _ in range(2)],
+             [rng.integers(1, 3000, (h, w)).astype(np.int16) for _ in range(2)],
+             [rng.integers(-3000, 3000, (h, w)).astype(np.int16) for _ in range(2)]]
+    chans = [{"input_start": f32(-500.0), "input_end": f32(2500.0), "global_min": gmin, "global_max": gmax,
+              "rgba": (255, 0, 0, 255)},
+             {"input_start": f32(0.0), "input_end": f32(1000.0), "global_min": -32768.0, "global_max": 32767.0,
+              "rgba": (0, 255, 0, 255)}]
+    files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h)
+    want = []
+    for t in tiles:
+        s_, _ = O.render(chans, t, _lib.PIXELS_INT16, w, h)
+        want.append(s_)
+    assert [int(x) != 0 for x in st.tolist()] == [x != 0 for x in want], (st.tolist(), want)
+    ok = [i for i, x in enumerate(want) if x == 0]
+    if ok:
+        exp = _expect(chans, [tiles[i] for i in ok], _lib.PIXELS_INT16, w, h)
+        assert [files[i] for i in ok] == exp
+    if not bad:
+        assert st.tolist() == [0, 0, 0]
+
+
 def test_int16_window_start_inexact_after_bias_falls_back(ctx):
     """The fused kernel reads int16 pixels biased by 32768 and moves the window start with them;
     a window start for which ws + 32768 is not exact (1e-30) takes the K2 + B1 path instead.
