@@ -271,9 +271,13 @@ __global__ void __launch_bounds__(256) k_build_thresh(const RenderPlan* __restri
     if (lane == 0) thr[a * 256 + c] = lo > khi ? 0xFFFFFFFFu : (uint32_t)lo;
 }
 
-// Buckets over the key range where a kModeThresh channel's code varies, [T[1], T[cmax]):
-// bucket b covers 2^shift keys; its entry is (#T <= its first key) | (#T inside it) << 8, so K2
-// searches only the few thresholds of its bucket (usually 0-2) instead of all 255.
+// Buckets over the key range where a kModeThresh channel's code varies, [T[1] - 1, T[cmax]]
+// (origin one key below T[1] when T[1] > 0): bucket b covers 2^shift keys from origin + b·2^shift;
+// its entry is (#T <= its first key) | (#T in the rest of it) << 8, so K2 searches only the few
+// thresholds of its bucket (usually 0-2) instead of all 255.  K2 clamps the key into
+// [origin, T[cmax]] for the bucket index only (one med3): a key below T[1] lands in bucket 0
+// (base 0, and no threshold of it is <= the key), a key at or above T[cmax] in the last one
+// (every threshold of it is <= the key), so no range test is needed.
 #ifndef OMR_K2_BUCKETS_LOG2
 #define OMR_K2_BUCKETS_LOG2 11
 #endif
@@ -303,13 +307,13 @@ __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restr
     const uint32_t* T = thr + a * 256;
     const uint32_t cmax = T[0] & 0xFFu;
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
+    const uint32_t k1 = cmax ? T[cmax] : 0u, org = cmax ? T[1] - (T[1] > 0u ? 1u : 0u) : 0u;
     uint16_t e = 0;
-    if (k1 > k0) {
-        const uint32_t sh = bucket_shift(k1 - k0);
-        const uint64_t ks = (uint64_t)k0 + ((uint64_t)b << sh);
-        if (ks < k1) {
-            const uint64_t ke = std::min<uint64_t>(ks + (1ull << sh) - 1, (uint64_t)k1 - 1);
+    if (cmax) {
+        const uint32_t sh = bucket_shift(k1 - org);
+        const uint64_t ks = (uint64_t)org + ((uint64_t)b << sh);
+        if (ks <= k1) {
+            const uint64_t ke = std::min<uint64_t>(ks + (1ull << sh) - 1, (uint64_t)k1);
             const uint32_t lo = thresh_count(T, (uint32_t)ks), hi = thresh_count(T, (uint32_t)ke);
             e = (uint16_t)(lo | ((hi - lo) << 8));
         }
@@ -382,17 +386,16 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
                 const uint16_t* Bk = s_bkt + a * kBuckets;
                 const uint32_t meta = T[0];
                 const uint32_t cmax = meta & 0xFFu, cnan = (meta >> 8) & 0xFFu;
-                const uint32_t k0 = T[1], k1 = cmax ? T[cmax] : 0u;
-                const uint32_t sh = bucket_shift(k1 > k0 ? k1 - k0 : 0u);
+                const uint32_t k1 = cmax ? T[cmax] : 0u, org = cmax ? T[1] - (T[1] > 0u ? 1u : 0u) : 0u;
+                const uint32_t sh = bucket_shift(k1 - org);
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {
                     uint32_t raw = c.dw[j];
                     if constexpr (BE) raw = bswap32(raw);
                     const uint32_t key = raw_key<PT>(raw);
-                    const bool inr = key >= k0 && key < k1;
-                    const uint32_t e = Bk[min((key - k0) >> sh, (uint32_t)kBuckets - 1)];
-                    uint32_t base = inr ? (e & 0xFFu) : (key >= k1 ? cmax : 0u);
-                    uint32_t len = inr ? (e >> 8) : 0u;
+                    const uint32_t e = Bk[(min(max(key, org), k1) - org) >> sh];
+                    uint32_t base = e & 0xFFu;
+                    uint32_t len = e >> 8;
                     while (len > 0) {
                         const uint32_t half = len >> 1;
                         const bool le = T[base + half + 1] <= key;
