@@ -1176,6 +1176,13 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.gmax = bias ? (int32_t)std::min<int64_t>(std::max<int64_t>(c.gmax, -32769), 32767) + bias : c.gmax;
         k.check = (c.gmin > tlo || c.gmax < thi) ? 1 : 0;
         F.any_check |= k.check;
+        {
+            const int64_t dl = std::max<int64_t>(k.gmin, 0), dh = std::min<int64_t>(k.gmax, 65535);
+            if (k.check && dl > dh) F.dnone = 1;
+            const uint32_t l = (uint32_t)std::min<int64_t>(dl, 65535), h = (uint32_t)std::max<int64_t>(dh, 0);
+            F.dlo2[i] = l | (l << 16);
+            F.dhi2[i] = h | (h << 16);
+        }
         const bool wint = c.ws == std::floor(c.ws) && std::fabs(c.ws) < 1073741824.0;
         F.ws_int = (i == 0 ? 1 : F.ws_int) & (wint ? 1 : 0);
         k.second = c.second;
