@@ -845,15 +845,17 @@ struct ArgbSource {
     template <int S>
     __device__ __forceinline__ void issue(int x0, int y0) {
         const int ya = min(y0, H - 1), yb = min(y0 + 1, H - 1);
+        // 32-bit byte offsets from the uniform tile base (a tile is at most 4096^2 pixels): loads
+        // with an SGPR base and a VGPR offset, no 64-bit address arithmetic per load
         if (even_w) {
             const int xl = min(x0, W - 2);                        // even, W >= 2
-            na[S] = *reinterpret_cast<const uint2*>(img + (int64_t)ya * W + xl);
-            nb[S] = *reinterpret_cast<const uint2*>(img + (int64_t)yb * W + xl);
+            na[S] = *px_at<uint2>((uint32_t)(ya * W + xl));
+            nb[S] = *px_at<uint2>((uint32_t)(yb * W + xl));
             nclamp[S] = x0 > W - 1;                                // both columns clamp to W-1
         } else {
             const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
-            na[S] = make_uint2(img[(int64_t)ya * W + xa], img[(int64_t)ya * W + xb]);
-            nb[S] = make_uint2(img[(int64_t)yb * W + xa], img[(int64_t)yb * W + xb]);
+            na[S] = make_uint2(*px_at<uint32_t>((uint32_t)(ya * W + xa)), *px_at<uint32_t>((uint32_t)(ya * W + xb)));
+            nb[S] = make_uint2(*px_at<uint32_t>((uint32_t)(yb * W + xa)), *px_at<uint32_t>((uint32_t)(yb * W + xb)));
             nclamp[S] = false;
         }
     }
@@ -862,7 +864,11 @@ struct ArgbSource {
         px[0] = rgb_of(nclamp[S] ? na[S].y : na[S].x); px[1] = rgb_of(na[S].y);
         px[2] = rgb_of(nclamp[S] ? nb[S].y : nb[S].x); px[3] = rgb_of(nb[S].y);
     }
-    __device__ __forceinline__ uint32_t at(int x, int y) const { return img[(int64_t)y * W + x]; }
+    __device__ __forceinline__ uint32_t at(int x, int y) const { return *px_at<uint32_t>((uint32_t)(y * W + x)); }
+    template <typename T>
+    __device__ __forceinline__ const T* px_at(uint32_t i) const {
+        return reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(img) + i * 4u);
+    }
 };
 
 // Fused render -> JPEG: B1 reads the raw channel planes and renders its pixels as K2 does
@@ -900,13 +906,16 @@ struct PlaneSource {
     template <int S>
     __device__ __forceinline__ void issue(int x0, int y0) {
         const int sx = F.flip_h ? W - 2 - x0 : x0;
-        const int64_t r0 = (int64_t)(F.flip_v ? H - 1 - y0 : y0) * F.row_stride + sx;
-        const int64_t r1 = (int64_t)(F.flip_v ? H - 2 - y0 : y0 + 1) * F.row_stride + sx;
+        // 32-bit byte offsets from the uniform plane base (the host keeps the plane below 4 GiB):
+        // global_load with an SGPR base and a VGPR offset, no 64-bit address arithmetic per load
+        const uint32_t rs = (uint32_t)F.row_stride;
+        const uint32_t r0 = ((uint32_t)(F.flip_v ? H - 1 - y0 : y0) * rs + (uint32_t)sx) * BPP;
+        const uint32_t r1 = ((uint32_t)(F.flip_v ? H - 2 - y0 : y0 + 1) * rs + (uint32_t)sx) * BPP;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             if constexpr (BPP == 2) {   // global, not flat, loads: see ld_global
-                raw[S][a][0] = ld_global<uint32_t>(base[a] + r0 * 2);
-                raw[S][a][1] = ld_global<uint32_t>(base[a] + r1 * 2);
+                raw[S][a][0] = ld_global<uint32_t>(base[a] + r0);
+                raw[S][a][1] = ld_global<uint32_t>(base[a] + r1);
             } else {
                 raw[S][a][0] = ld_global<uint16_t>(base[a] + r0);
                 raw[S][a][1] = ld_global<uint16_t>(base[a] + r1);
@@ -1110,7 +1119,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         for (int k = 0; k < 6; ++k) {
             const int v = lane == 0 ? dc[k] : qv[k];
             if constexpr ((OMR_ABL & kAblCoefStore) != 0) abl_sink ^= v;
-            else out[k * 64 + lane] = (int16_t)v;
+            else *reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(out) + (uint32_t)(k * 128 + lane * 2)) = (int16_t)v;
         }
         // the six per-block DC records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in
         // the wave's run); one store per wave after the loop instead of six one-lane stores per MCU
@@ -1883,7 +1892,9 @@ static omr_status render_jpeg_batch(Ctx* ctx, const omr_quantum_def* qdef, const
     const int64_t al = bpp == 2 ? 4 : 2;     // the fused loads read pixel pairs
     const bool aligned = (row_stride * bpp) % al == 0 &&
                          (!d_base || ((uintptr_t)d_base % al == 0 && tile_stride % al == 0 && chan_stride % al == 0));
-    const bool fused = plan_ok && W % 16 == 0 && H % 16 == 0 && aligned;
+    // F1 addresses a plane's pixels by 32-bit byte offsets from the plane's (uniform) base
+    const bool offs32 = (row_stride * (int64_t)(H - 1) + W) * bpp < ((int64_t)1 << 32);
+    const bool fused = plan_ok && W % 16 == 0 && H % 16 == 0 && aligned && offs32;
     const size_t rstat_bytes = align_up((size_t)n * 4, 256);
     if (fused) {
         const size_t r_bytes = align_up(render_fused_ws_bytes(fp.get()), 256);
