@@ -1203,6 +1203,12 @@ struct B2aArgs {
     int32_t nb, ngb;
 };
 
+// Block b of a 256-block group whose first block is g0: its 64 coefficients from the group's
+// uniform base plus a 32-bit byte offset (an SGPR-base load, no 64-bit address VALU).
+__device__ __forceinline__ const uint4* group_block_coefs(const int16_t* coefs, int64_t g0, int i) {
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(coefs + g0 * 64) + (uint32_t)i * 128u);
+}
+
 // Magnitude category (bit length of |c|, 0 for 0) of a coefficient: frexp's exponent of the exact
 // float, sign-independent (two instructions instead of abs + clz + a zero select).
 __device__ __forceinline__ int mag_bits(int c) { return __builtin_amdgcn_frexp_expf((float)c); }
@@ -1225,7 +1231,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
         const int64_t gb = (int64_t)tile * A.nb + b;
         uint4 q[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = reinterpret_cast<const uint4*>(A.coefs + gb * 64)[i];
+        for (int i = 0; i < 8; ++i) q[i] = group_block_coefs(A.coefs, (int64_t)tile * A.nb + b0, threadIdx.x)[i];
         const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
         const int pb = prev_block_in_tile(b);
         const uint32_t rb = blk[b];
@@ -1362,7 +1368,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         __syncthreads();
     }
     if (live) {
-        const uint4* src = reinterpret_cast<const uint4*>(A.coefs + gb * 64);
+        const uint4* src = group_block_coefs(A.coefs, (int64_t)tile * A.nb + (int64_t)blockIdx.x * kGrp, threadIdx.x);
         uint4 q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = src[i];
