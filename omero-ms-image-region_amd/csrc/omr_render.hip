@@ -775,6 +775,21 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
     return L;
 }
 
+// The pipelined float kernel holds two work blocks in registers (87 VGPRs at three channels: 5
+// waves per SIMD), so its grid-stride grid is sized by the kernel's own occupancy, queried once
+// per instantiation: a grid sized for 8 resident blocks per CU left 3 of every 8 waiting for a
+// second round.
+static thread_local int tl_cu_count = 0;
+template <auto KERN>
+static int pipe_grid(const K2Args& a, int grid, size_t lds) {
+    static const int occ = [&] {                       // one query per instantiation
+        int o = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, KERN, kBlock, lds) == hipSuccess ? o : 0;
+    }();
+    if (occ <= 0 || tl_cu_count <= 0) return grid;
+    return (int)std::min<uint64_t>(a.n_work, (uint64_t)tl_cu_count * (uint64_t)occ);
+}
+
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s, int cpt = kCPT) {
     const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
@@ -782,17 +797,24 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small
         // software-pipelined grid stride (k_render_pipe; cpt -1: one chunk per lane and block,
         // -2: two), the default for 1..4 channels
         if (cpt < 0) {
+#define OMR_PIPE(NAV, CPTV)                                                                       \
+    {                                                                                             \
+        constexpr auto kern = &k_render_pipe<BPP, VEC, BE, SIGNED, PT, NAV, MODE, CPTV>;         \
+        hipLaunchKernelGGL(kern, dim3(pipe_grid<kern>(a, grid, lds)), dim3(kBlock), lds, s, a);   \
+        return hipGetLastError();                                                                 \
+    }
             switch (na * 2 + (cpt == -2 ? 1 : 0)) {
-            case 2: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 1, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 3: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 1, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 4: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 2, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 5: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 2, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 6: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 7: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 3, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 8: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 4, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 9: hipLaunchKernelGGL((k_render_pipe<BPP, VEC, BE, SIGNED, PT, 4, MODE, 2>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 2: OMR_PIPE(1, 1)
+            case 3: OMR_PIPE(1, 2)
+            case 4: OMR_PIPE(2, 1)
+            case 5: OMR_PIPE(2, 2)
+            case 6: OMR_PIPE(3, 1)
+            case 7: OMR_PIPE(3, 2)
+            case 8: OMR_PIPE(4, 1)
+            case 9: OMR_PIPE(4, 2)
             default: break;
             }
+#undef OMR_PIPE
         }
         // grid-stride float / 32-bit modes, OMR_K2_EVAL_CPT=4: 4 chunks per lane (12 loads in
         // flight at 3 channels; measured slower than kCPT on C5)
@@ -1073,6 +1095,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     hipError_t e;
     const bool be = big_endian != 0;
     KernelTimer timer(ctx, 2);
+    tl_cu_count = ctx->cu_count;
     if (aligned) {
         switch (bpp) {
         case 1: e = launch_render_be<1, 8>(a, pixel_type, be, na, mode16, grid, small, ctx->stream, cpt_thread); break;
