@@ -1367,7 +1367,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         for (uint32_t i = threadIdx.x; i < nw; i += kGrp) s_words[i] = 0;
         __syncthreads();
     }
-    if (live) {
+    // The coder, instantiated for the LDS-staged group (the common case: a flush is one ds_or at
+    // a running LDS pointer) and for a group too long for the staging buffer (word stores, the
+    // block's shared first word ORed into HBM).
+    auto code_block = [&](auto staged_c) {
+        constexpr bool STAGED = decltype(staged_c)::value;
         const uint4* src = group_block_coefs(A.coefs, (int64_t)tile * A.nb + (int64_t)blockIdx.x * kGrp, threadIdx.x);
         uint4 q[8];
 #pragma unroll
@@ -1378,17 +1382,21 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         int nacc = (int)(boff & 31);
         uint32_t wpos = boff >> 5;
         const uint32_t w0 = wpos;
+        uint32_t* sp = &s_words[wpos - gw0];          // STAGED: the LDS word the next flush ORs into
         auto flush = [&](uint32_t w) {
-            if (staged) atomicOr(&s_words[wpos - gw0], w);
-            else if (wpos == w0) atomicOr(&words[wpos], w);   // shares bits with the previous block
-            else words[wpos] = w;
+            if constexpr (STAGED) { atomicOr(sp, w); ++sp; }
+            else {
+                if (wpos == w0) atomicOr(&words[wpos], w);   // shares bits with the previous block
+                else words[wpos] = w;
+                ++wpos;
+            }
         };
         auto put = [&](uint32_t v, int n) {          // n <= 26, v < 2^n
             acc = (acc << n) | v;
             nacc += n;
             if (nacc >= 32) {
-                flush((uint32_t)(acc >> (nacc - 32)));
-                ++wpos;
+                // bits [nacc - 32, nacc) of acc: one v_alignbit_b32 of its halves
+                flush(__builtin_amdgcn_alignbit((uint32_t)(acc >> 32), (uint32_t)acc, (uint32_t)(nacc - 32)));
                 nacc -= 32;
             }
         };
@@ -1434,9 +1442,13 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         if (r > 0) put(eob & 0xFFFF, (int)(eob >> 16));                   // EOB
         if (nacc > 0) {                                                   // shared with the next block
             const uint32_t w = (uint32_t)(acc << (32 - nacc));
-            if (staged) atomicOr(&s_words[wpos - gw0], w);
+            if constexpr (STAGED) atomicOr(sp, w);
             else atomicOr(&words[wpos], w);
         }
+    };
+    if (live) {
+        if (staged) code_block(std::true_type{});
+        else code_block(std::false_type{});
     }
     if (staged) {
         __syncthreads();
