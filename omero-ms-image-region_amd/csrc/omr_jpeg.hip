@@ -1462,6 +1462,16 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
 
 constexpr int kStuffBytes = 16;   // bytes per chunk in B4a/B6
 
+// 0x80 in every byte of w that is 0xFF, 0 elsewhere (exact: no borrow between bytes).
+__device__ __forceinline__ uint32_t ff_bytes(uint32_t w) {
+    const uint32_t t = ~w;
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
+// 0x80 in each of the first k (big-endian) bytes of a stream word, k in [0, 4].
+__device__ __forceinline__ uint32_t first_bytes_mask(int k) {
+    return k >= 4 ? 0x80808080u : k <= 0 ? 0u : 0x80808080u & ~(0xFFFFFFFFu >> (8 * k));
+}
+
 __device__ __forceinline__ uint32_t seg_byte(const uint32_t* words, uint32_t i, uint32_t nbytes, uint32_t tb) {
     uint32_t b = (words[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
     if (i == nbytes - 1 && (tb & 7)) b |= 0xFFu >> (tb & 7);   // jchuff flush: pad with 1s
@@ -1506,9 +1516,9 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_count(B4aArgs A) {
             uint32_t w[4];
             chunk_bytes(words, c, nbytes, tb, w);
             const uint32_t e = min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes);
+            // four bytes at a time: exact 0xFF-byte detection, popcount of the valid ones
 #pragma unroll
-            for (int i = 0; i < kStuffBytes; ++i)
-                n += (i < (int)e && ((w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF) == 0xFF) ? 1u : 0u;
+            for (int q = 0; q < 4; ++q) n += __popc(ff_bytes(w[q]) & first_bytes_mask((int)e - 4 * q));
             A.cnt[(int64_t)tile * A.slot_chunks + c] = (uint8_t)n;
         }
         const uint32_t total = block_reduce_sum(n, sw);
@@ -1637,6 +1647,8 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
                 atomicOr(&swords[wi + 3], (uint32_t)((((uint64_t)l3 << 32) | l2) >> (32 - sh)));
                 if (sh) atomicOr(&swords[wi + 4], l3 >> (32 - sh));
             } else {
+                // byte by byte (a word-wise split — a full word without 0xFF as one shifted pair of
+                // ORs — measured 4 % slower: the words with a 0xFF still diverge the wave)
                 for (uint32_t i = 0; i < e; ++i) {
                     const uint32_t bv = (w[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
                     atomicOr(&swords[o >> 2], bv << (8 * (o & 3)));
