@@ -463,6 +463,22 @@ omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int
                           uint8_t* out, size_t cap, size_t* out_len);
 omr_status omr_encode_png_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t width,
                                  int32_t height, uint8_t* out, size_t cap, size_t* out_len);
+/*
+ * Batched PNG (same encoder family, decoded pixels identical per tile) of n_tiles device ARGB
+ * tiles (tile i at d_argb + i*tile_stride_px; 0 = width*height): the batch form of the
+ * per-request ImageIO.write(image, "png", ...) calls (ImageRegionRequestHandler.java:597-599).
+ * Complete PNG files in d_out (capacity out_cap bytes): file i at d_out + d_offsets[i] (16-byte
+ * aligned slots, in tile order), d_lengths[i] bytes; 0 and d_status[i] = OMR_BUFFER_TOO_SMALL when
+ * it did not fit (d_offsets / d_lengths / d_status optional).  Every stage is one launch over all
+ * tiles; no host sync (asynchronous on the context stream).  width, height <= 4096.
+ */
+omr_status omr_encode_png_batch_device(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px,
+                                       int32_t n_tiles, int32_t width, int32_t height, uint8_t* d_out,
+                                       size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                       int32_t* d_status);
+/* Output capacity that always holds n batched PNG files of width x height (channels 3: RGB
+ * tiles, 1: masks), 16-byte slots included. */
+size_t omr_png_batch_max_bytes(int32_t width, int32_t height, int32_t channels, int32_t n);
 
 /*
  * TIFF of the 24-bit RGB view (TIFFImageWriter branch, ImageRegionRequestHandler.java:584-596):
@@ -489,6 +505,26 @@ omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n
                                      int32_t width, int32_t height, const uint8_t rgba[4],
                                      int32_t flip_h, int32_t flip_v,
                                      uint8_t* out, size_t cap, size_t* out_len);
+/*
+ * N render_shape_mask requests in one call (the per-worker renderShapeMask calls of
+ * ShapeMaskVerticle.java:121-149 coalesced): the masks may differ in size, colour and flips, and
+ * are encoded by the batched PNG pipeline (one launch per stage for all of them).  Host in/out,
+ * synchronous.  File i lands at out + offsets[i] (16-byte aligned slots), lengths[i] bytes;
+ * status[i] is OMR_OK, OMR_NOT_FOUND for every case the single call answers with 404 (the same
+ * checks and the same packed-buffer flip), or OMR_BUFFER_TOO_SMALL when cap ran out
+ * (omr_png_batch_max_bytes(w, h, 1, 1) per mask always suffices).  Returns OMR_OK when the call
+ * ran; per-mask outcomes are in status.
+ */
+typedef struct omr_mask_job {
+    const uint8_t* bits;        /* MSB-first mask bits (byte[] of the Mask) */
+    size_t n_bytes;
+    int32_t width, height;
+    uint8_t rgba[4];            /* fill colour (omr_shape_mask_fill_color) */
+    int32_t flip_h, flip_v;
+} omr_mask_job;
+omr_status omr_render_shape_mask_png_batch(omr_ctx* ctx, const omr_mask_job* jobs, int32_t n,
+                                           uint8_t* out, size_t cap, uint64_t* offsets,
+                                           uint32_t* lengths, int32_t* status);
 
 /* ---- host-side request helpers (no device work) ---------------------------------- */
 /* ImageRegionRequestHandler.splitHTMLColor (:865-890), bug-compatible; OMR_INVALID_ARGUMENT = null. */

@@ -82,9 +82,18 @@ static jctx* get_ctx(JNIEnv* env, jlong h) {
     return J && J->ctx ? J : NULL;
 }
 
-/* Pinned staging of at least `bytes` (grow-only). */
+/* Pinned staging of at least `bytes`.  The context keeps one grow-only buffer up to
+ * STAGE_KEEP_MAX bytes (a few tiles); a larger request (a full-plane render, an 8 GiB worst-case
+ * encode) gets a temporary pinned buffer that unstage() frees after the call, so one big request
+ * does not stay pinned for the rest of a worker context's life. */
+#define STAGE_KEEP_MAX ((size_t)64 << 20)
 static uint8_t* stage(JNIEnv* env, jctx* J, size_t bytes) {
     if (bytes == 0) bytes = 1;
+    if (bytes > STAGE_KEEP_MAX) {
+        uint8_t* tmp = (uint8_t*)omr_pinned_alloc(J->ctx, bytes);
+        if (!tmp) throw_omr(env, OMR_OOM, "pinned staging");
+        return tmp;
+    }
     if (bytes > J->pin_cap) {
         if (J->pin) omr_pinned_free(J->ctx, J->pin);
         J->pin_cap = 0;
@@ -97,6 +106,15 @@ static uint8_t* stage(JNIEnv* env, jctx* J, size_t bytes) {
     }
     return J->pin;
 }
+
+/* Release what stage() returned: a temporary buffer is freed, the kept one stays. */
+static void unstage(jctx* J, uint8_t* p) {
+    if (p && p != J->pin) omr_pinned_free(J->ctx, p);
+}
+
+/* 16-byte alignment of each slice of the staging buffer (planes, ARGB output, encoded bytes):
+ * the library's copies and the int views stay aligned whatever the plane size. */
+static size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 /* Length of a Java array that must hold at least `need` elements (INVALID_ARGUMENT otherwise). */
 static int check_len(JNIEnv* env, jarray a, int64_t need, const char* what) {
@@ -243,7 +261,7 @@ JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNat
             return;
         }
     }
-    const size_t out_off = (size_t)plane_bytes * (size_t)n_active;
+    const size_t slot = align16((size_t)plane_bytes), out_off = slot * (size_t)n_active;
     uint8_t* pin = stage(env, J, out_off + (size_t)npx * 4);
     if (!pin) { free(s); return; }
     const void* planes[MAX_CH] = {0};
@@ -251,25 +269,27 @@ JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNat
     for (jsize c = 0; c < s->n; ++c) {                  /* copy each active plane, drop its local ref */
         if (!s->cb[c].active) continue;
         jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, jplanes, c);
-        if ((*env)->ExceptionCheck(env)) { free(s); return; }
+        if ((*env)->ExceptionCheck(env)) { free(s); unstage(J, pin); return; }
         if (!a || (int64_t)(*env)->GetArrayLength(env, a) < plane_bytes) {   /* changed since the check */
             if (a) (*env)->DeleteLocalRef(env, a);
             free(s);
+            unstage(J, pin);
             throw_omr(env, OMR_INVALID_ARGUMENT, "plane array changed during the call");
             return;
         }
         (*env)->GetByteArrayRegion(env, a, 0, (jsize)plane_bytes, (jbyte*)(pin + off));
         (*env)->DeleteLocalRef(env, a);
-        if ((*env)->ExceptionCheck(env)) { free(s); return; }
+        if ((*env)->ExceptionCheck(env)) { free(s); unstage(J, pin); return; }
         planes[c] = pin + off;
-        off += (size_t)plane_bytes;
+        off += slot;
     }
     const omr_quantum_def q = {0, 255, 255, model};      /* createRenderingDef, :273-277 */
     const omr_status st = omr_render_packed_int(J->ctx, &q, s->cb, s->n, planes, 0, pixelType, bigEndian, w, ht,
                                                 flipH, flipV, (uint32_t*)(pin + out_off));
     free(s);
-    if (st) { throw_ctx(env, J->ctx, st); return; }
-    (*env)->SetIntArrayRegion(env, jout, 0, (jsize)npx, (const jint*)(pin + out_off));
+    if (!st) (*env)->SetIntArrayRegion(env, jout, 0, (jsize)npx, (const jint*)(pin + out_off));
+    else throw_ctx(env, J->ctx, st);
+    unstage(J, pin);
 }
 
 /* ---- ProjectionService.projectStack ----------------------------------------------------------- */
@@ -287,14 +307,16 @@ JNIEXPORT void JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNat
     if (!check_len(env, jstack, stack, "stack shorter than sizeX*sizeY*sizeZ pixels") ||
         !check_len(env, jout, plane, "plane output shorter than sizeX*sizeY pixels"))
         return;
-    uint8_t* pin = stage(env, J, (size_t)stack + (size_t)plane);
+    const size_t out_off = align16((size_t)stack);
+    uint8_t* pin = stage(env, J, out_off + (size_t)plane);
     if (!pin) return;
     (*env)->GetByteArrayRegion(env, jstack, 0, (jsize)stack, (jbyte*)pin);
-    if ((*env)->ExceptionCheck(env)) return;
+    if ((*env)->ExceptionCheck(env)) { unstage(J, pin); return; }
     const omr_status st = omr_project_stack(J->ctx, pin, pixelType, beIn, sx, sy, sz, alg, start, end, stepping,
-                                            pin + stack, beOut);
-    if (st) { throw_ctx(env, J->ctx, st); return; }
-    (*env)->SetByteArrayRegion(env, jout, 0, (jsize)plane, (const jbyte*)(pin + stack));
+                                            pin + out_off, beOut);
+    if (!st) (*env)->SetByteArrayRegion(env, jout, 0, (jsize)plane, (const jbyte*)(pin + out_off));
+    else throw_ctx(env, J->ctx, st);
+    unstage(J, pin);
 }
 
 /* ---- encoders: ARGB int[] -> file bytes ------------------------------------------------------- */
@@ -321,21 +343,22 @@ static jbyteArray encode(JNIEnv* env, jlong h, jintArray jargb, jint w, jint ht,
     if (!check_len(env, jargb, npx, "ARGB array shorter than width*height")) return NULL;
     const size_t cap = kind == 0 ? omr_jpeg_max_bytes(w, ht) : kind == 1 ? omr_png_max_bytes(w, ht, 3)
                                                                            : omr_tiff_max_bytes(w, ht);
-    uint8_t* pin = stage(env, J, (size_t)npx * 4 + cap);
+    const size_t buf_off = align16((size_t)npx * 4);
+    uint8_t* pin = stage(env, J, buf_off + cap);
     if (!pin) return NULL;
     (*env)->GetIntArrayRegion(env, jargb, 0, (jsize)npx, (jint*)pin);
-    if ((*env)->ExceptionCheck(env)) return NULL;
-    uint8_t* buf = pin + (size_t)npx * 4;
+    if ((*env)->ExceptionCheck(env)) { unstage(J, pin); return NULL; }
+    uint8_t* buf = pin + buf_off;
     size_t len = 0;
     const uint32_t* argb = (const uint32_t*)pin;
     const omr_status st = kind == 0 ? omr_encode_jpeg(J->ctx, argb, w, ht, quality, buf, cap, &len)
                         : kind == 1 ? omr_encode_png(J->ctx, argb, w, ht, buf, cap, &len)
                                     : omr_encode_tiff(J->ctx, argb, w, ht, buf, cap, &len);
-    if (st) {
-        throw_ctx(env, J->ctx, st);
-        return NULL;
-    }
-    return new_bytes(env, buf, len);
+    jbyteArray res = NULL;
+    if (st) throw_ctx(env, J->ctx, st);
+    else res = new_bytes(env, buf, len);
+    unstage(J, pin);
+    return res;
 }
 
 JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_encodeJpeg(
@@ -364,22 +387,30 @@ JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_
     (*env)->GetByteArrayRegion(env, jrgba, 0, 4, (jbyte*)rgba);
     if ((*env)->ExceptionCheck(env)) return NULL;
     const jsize nbits = jbits ? (*env)->GetArrayLength(env, jbits) : 0;   /* null mask: the library's 404 */
-    const size_t cap = omr_png_max_bytes(w, ht, 1);
-    uint8_t* pin = stage(env, J, (size_t)nbits + cap);
-    if (!pin) return NULL;
-    if (nbits) {
-        (*env)->GetByteArrayRegion(env, jbits, 0, nbits, (jbyte*)pin);
-        if ((*env)->ExceptionCheck(env)) return NULL;
-    }
-    size_t len = 0;
-    uint8_t* buf = pin + nbits;
-    const omr_status st = omr_render_shape_mask_png(J->ctx, jbits ? pin : NULL, (size_t)nbits, w, ht, rgba, flipH,
-                                                    flipV, buf, cap, &len);
-    if (st) {
-        throw_ctx(env, J->ctx, st);
+    /* The library's own checks, before anything is pinned: every one of them is an exception inside
+     * renderShapeMask, which ShapeMaskVerticle.java:119-128 answers with 404 (OMR_NOT_FOUND). */
+    const int64_t npx = (int64_t)w * ht;
+    if (w <= 0 || ht <= 0 || npx > INT32_MAX || !jbits || (int64_t)nbits * 8 < npx) {
+        throw_omr(env, OMR_NOT_FOUND, w <= 0 || ht <= 0 ? "Attempted to flip image with 0 size"
+                                      : npx > INT32_MAX ? "width*height overflows a Java int"
+                                      : !jbits          ? "NullPointerException: null mask bytes"
+                                                        : "mask shorter than width*height bits");
         return NULL;
     }
-    return new_bytes(env, buf, len);
+    const size_t cap = omr_png_max_bytes(w, ht, 1), buf_off = align16((size_t)nbits);
+    uint8_t* pin = stage(env, J, buf_off + cap);
+    if (!pin) return NULL;
+    (*env)->GetByteArrayRegion(env, jbits, 0, nbits, (jbyte*)pin);
+    if ((*env)->ExceptionCheck(env)) { unstage(J, pin); return NULL; }
+    size_t len = 0;
+    uint8_t* buf = pin + buf_off;
+    const omr_status st = omr_render_shape_mask_png(J->ctx, pin, (size_t)nbits, w, ht, rgba, flipH, flipV, buf, cap,
+                                                    &len);
+    jbyteArray res = NULL;
+    if (st) throw_ctx(env, J->ctx, st);
+    else res = new_bytes(env, buf, len);
+    unstage(J, pin);
+    return res;
 }
 
 /* ---- ROMIO pixel buffer + request batcher + node pool ----------------------------------------- */

@@ -119,6 +119,9 @@ struct Ctx {
     // PNG D3 (Huffman tables) on the device (env OMR_PNG_DEVICE_D3=1): no mid-encode host round
     // trip, but the single-workgroup build measured slower than the host's
     bool png_device_d3 = false;
+    // x^(8*256*j) mod P (CRC-32) for the batched PNG's segment combine: [0, 4096) j = lo, then
+    // [4096, 6144) j = hi * 4096; built on the device on first use (omr_png.hip)
+    uint32_t* d_crc_pow = nullptr;
     bool f1_f32 = true;              // F1's Fast16 quantize in f32 when proven exact (OMR_F1_F32=0: f64)
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)

@@ -355,14 +355,13 @@ __device__ __forceinline__ uint32_t paeth(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // LDS: the raw bytes of this row and the row above (2 * (rowlen - 1) bytes, dynamic); every
-// filter residual is then computed from LDS.
-__global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
+// filter residual is then computed from LDS.  One workgroup, row y of image A: the filter byte +
+// filtered row at flt + y * rowlen, the row's Adler partials at rs[0..1].
+__device__ void png_filter_row(const PngArgs& A, int bpp, int y, uint8_t* __restrict__ flt,
+                               unsigned long long* __restrict__ rs, uint8_t* s_rows) {
     __shared__ uint32_t s_sum[5][4];
     __shared__ int s_f;
-    const PngArgs& A = D.P;
-    const int y = blockIdx.x;
-    const int rb = (int)A.rowlen - 1, bpp = D.bpp;
+    const int rb = (int)A.rowlen - 1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint8_t* cur = s_rows;
     uint8_t* prev = s_rows + rb;
@@ -419,7 +418,7 @@ __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
     const int64_t row0 = (int64_t)y * A.rowlen;
     unsigned long long s1 = 0, s2 = 0;
     if (threadIdx.x == 0) {
-        D.flt[row0] = (uint8_t)f;
+        flt[row0] = (uint8_t)f;
         s1 += (unsigned long long)f;
         s2 += (unsigned long long)(A.raw - row0) * (unsigned long long)f;
     }
@@ -428,7 +427,7 @@ __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
         filt(i, fv);
         const uint32_t v = fv[f];
         const int64_t idx = row0 + 1 + i;
-        D.flt[idx] = (uint8_t)v;
+        flt[idx] = (uint8_t)v;
         s1 += v;
         s2 += (unsigned long long)(A.raw - idx) * v;
     }
@@ -440,9 +439,14 @@ __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
     if (lane == 0) { s_ad[0][wv] = s1; s_ad[1][wv] = s2; }
     __syncthreads();
     if (threadIdx.x == 0) {      // per-row Adler partials; summed by k_png_adler_rows
-        D.row_sums[2 * y] = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
-        D.row_sums[2 * y + 1] = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
+        rs[0] = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
+        rs[1] = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
     }
+}
+
+__global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
+    png_filter_row(D.P, D.bpp, blockIdx.x, D.flt, D.row_sums + 2 * blockIdx.x, s_rows);
 }
 
 // Sum of the per-row Adler partials into A.sums (one workgroup; dynamic stream only).
@@ -466,30 +470,33 @@ __global__ void __launch_bounds__(256) k_png_adler_rows(DflArgs D) {
 constexpr int kParseLanes = 128;            // segments (lanes) per parse workgroup
 constexpr int kMaxBack = 31 * 1024;         // LDS look-back window (bytes)
 
-// One lane per kSeg-byte segment; the workgroup first stages its 32 KiB of filtered stream plus
+// One lane per kSeg-byte segment; the workgroup first stages its 4 KiB of filtered stream plus
 // the look-back window (one image row, <= 31 KiB) in LDS, so the greedy parse's byte compares
-// are LDS reads instead of dependent global loads.
-__global__ void __launch_bounds__(kParseLanes) k_png_lz_parse(DflArgs D, int32_t back) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
+// are LDS reads instead of dependent global loads.  Parse block `blk` of one image: flt is the
+// image's filtered stream (16-byte aligned), tokens / ntok its segments' token slots and counts,
+// lhist / dhist its symbol histograms.
+__device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw, int64_t rowlen, int bpp,
+                                   int64_t nseg, int64_t blk, int32_t back, uint32_t* __restrict__ tokens,
+                                   uint16_t* __restrict__ ntok, uint32_t* __restrict__ lhist,
+                                   uint32_t* __restrict__ dhist, uint8_t* s_win) {
     __shared__ uint32_t lh[286], dh[30];
     for (int i = threadIdx.x; i < 286; i += kParseLanes) lh[i] = 0;
     if (threadIdx.x < 30) dh[threadIdx.x] = 0;
-    const int64_t bbeg = (int64_t)blockIdx.x * kParseLanes * kSeg;
-    const int64_t bend = min(D.P.raw, bbeg + (int64_t)kParseLanes * kSeg);
+    const int64_t bbeg = blk * kParseLanes * kSeg;
+    const int64_t bend = min(raw, bbeg + (int64_t)kParseLanes * kSeg);
     const int64_t wbeg = max((int64_t)0, bbeg - back);          // back is a multiple of 16
     const int64_t n16 = (bend - wbeg) / 16;
-    const uint4* g16 = reinterpret_cast<const uint4*>(D.flt + wbeg);
+    const uint4* g16 = reinterpret_cast<const uint4*>(flt + wbeg);
     for (int64_t i = threadIdx.x; i < n16; i += kParseLanes) reinterpret_cast<uint4*>(s_win)[i] = g16[i];
-    for (int64_t i = wbeg + n16 * 16 + threadIdx.x; i < bend; i += kParseLanes) s_win[i - wbeg] = D.flt[i];
+    for (int64_t i = wbeg + n16 * 16 + threadIdx.x; i < bend; i += kParseLanes) s_win[i - wbeg] = flt[i];
     __syncthreads();
-    const int64_t s = (int64_t)blockIdx.x * kParseLanes + threadIdx.x;
-    if (s < D.nseg) {
+    const int64_t s = blk * kParseLanes + threadIdx.x;
+    if (s < nseg) {
         const uint8_t* f = s_win - wbeg;            // f[p] for p in [wbeg, bend)
-        const int64_t beg = s * kSeg, end = min(D.P.raw, beg + kSeg);
-        const int64_t rowlen = D.P.rowlen;
-        const int64_t cand[4] = {1, D.bpp, 2 * D.bpp, rowlen};
-        const int nc = D.bpp == 1 ? 2 : 3;
-        uint32_t* tok = D.tokens + beg;
+        const int64_t beg = s * kSeg, end = min(raw, beg + kSeg);
+        const int64_t cand[4] = {1, bpp, 2 * bpp, rowlen};
+        const int nc = bpp == 1 ? 2 : 3;
+        uint32_t* tok = tokens + beg;
         int nt = 0;
         int64_t p = beg;
         while (p < end) {
@@ -517,12 +524,18 @@ __global__ void __launch_bounds__(kParseLanes) k_png_lz_parse(DflArgs D, int32_t
                 ++p;
             }
         }
-        D.ntok[s] = (uint16_t)nt;
+        ntok[s] = (uint16_t)nt;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 286; i += kParseLanes)
-        if (lh[i]) atomicAdd(&D.lhist[i], lh[i]);
-    if (threadIdx.x < 30 && dh[threadIdx.x]) atomicAdd(&D.dhist[threadIdx.x], dh[threadIdx.x]);
+        if (lh[i]) atomicAdd(&lhist[i], lh[i]);
+    if (threadIdx.x < 30 && dh[threadIdx.x]) atomicAdd(&dhist[threadIdx.x], dh[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(kParseLanes) k_png_lz_parse(DflArgs D, int32_t back) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
+    png_lz_parse_block(D.flt, D.P.raw, D.P.rowlen, D.bpp, D.nseg, blockIdx.x, back, D.tokens, D.ntok, D.lhist,
+                       D.dhist, s_win);
 }
 
 // ---- D3 on the device: the code is a function of two small histograms (286 + 30 counts); one
@@ -702,7 +715,7 @@ __device__ void huff_canon_dev(HuffWork& W, int n, uint16_t* code) {
 }
 
 // D3: one workgroup.  hist = [286 literal/length][30 distance] counts from D2.
-__global__ void __launch_bounds__(kHuffThreads) k_png_tables(const uint32_t* __restrict__ hist, DflTables* __restrict__ T) {
+__device__ void png_build_tables(const uint32_t* __restrict__ hist, DflTables* __restrict__ T) {
     __shared__ HuffWork W;
     __shared__ DflTables t;
     __shared__ uint8_t seq[286 + 30];
@@ -789,6 +802,10 @@ __global__ void __launch_bounds__(kHuffThreads) k_png_tables(const uint32_t* __r
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&t);
     uint32_t* dst = reinterpret_cast<uint32_t*>(T);
     for (int i = tid; i < (int)(sizeof(DflTables) / 4); i += kHuffThreads) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(kHuffThreads) k_png_tables(const uint32_t* __restrict__ hist, DflTables* __restrict__ T) {
+    png_build_tables(hist, T);
 }
 
 // ---- D3 on the host (the default): the same construction in C++ between D2 and D4 (one
@@ -1231,6 +1248,699 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
 
 static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H).total; }
 
+// =====================================================================================
+// Batched PNG (round 4): N images — rendered RGB tiles of one size, or shape masks of any size —
+// through one launch per stage, every grid spanning all images, and the N files packed in device
+// memory with per-image status (the batch form of the per-request ImageIO.write calls,
+// ImageRegionRequestHandler.java:597-599, and of every mask, ShapeMaskRequestHandler.java:185-203):
+//   P1 k_pngb_filter   one workgroup per image row (D1)
+//   P2 k_pngb_parse    one lane per 32-byte segment, 128 per workgroup (D2); per-image histograms
+//   P3 k_pngb_tables   one workgroup per image: length-limited Huffman code + block header (D3
+//                      on the device: no host round trip; N workgroups run side by side)
+//   P4 k_pngb_bits     one lane per segment: its bits, the in-group exclusive scan, group sums
+//   P5 k_pngb_scan     one workgroup per image: group bit offsets, stream length, stored vs
+//                      dynamic, Adler-32 from the row partials, boundary words zeroed, header +
+//                      EOB ORed in
+//   P6 k_pngb_offsets  one workgroup: files' offsets in the output (16-byte aligned), status
+//   P7 k_pngb_write    one workgroup per 256 segments: codes assembled in LDS, interior words
+//                      stored, the two boundary words ORed
+//   P8 k_pngb_emit     16 output bytes per lane: prefix chunks, IDAT header, zlib stream (deflate
+//                      words funnel-shifted, or stored blocks of the filtered stream), Adler,
+//                      IEND — aligned 16-byte stores
+//   P9 k_pngb_crc      one lane per 256-byte segment counted from the end of the CRC range:
+//                      segment CRC x x^(8*256*j) from a power table, XOR-combined per image
+//   P10 k_pngb_finish  one lane per image: the CRC bytes
+// =====================================================================================
+constexpr int kPngbGroup = 256;                 // segments per P4/P7 group
+constexpr int kPngbGroupWords = kPngbGroup * kSeg * 16 / 32 + 2;   // <= 16 bits per stream byte
+constexpr int kPngbEmitBytes = 16 * 256;        // output bytes per P8 workgroup
+constexpr int kPngbCrcBytes = 256 * 256;        // CRC range bytes per P9 workgroup
+constexpr int kPngbMaxSide = 4096;
+constexpr int kCrcPowLo = 4096, kCrcPowHi = 2048;
+
+struct PngImg {
+    const uint32_t* argb;      // kRgb: pixels, row stride W
+    const uint8_t* bits;       // kIdx1 / kIdx8: MSB-first mask bits
+    int32_t kind, W, H, flip_h, flip_v, bpp;
+    int32_t row0, pblk0, grp0, pre_len;         // first global row / parse block / group; prefix bytes
+    int32_t back, pad;                          // parse look-back (bytes, multiple of 16)
+    int64_t rowlen, raw, nseg, nblk;            // row bytes + 1, filtered stream bytes, segments, stored blocks
+    int64_t flt, seg0, words;                   // filtered stream offset (bytes), first segment, first word
+    int64_t eblk0, cblk0;                       // first P8 / P9 workgroup
+    uint8_t pre[72];                            // signature, IHDR (+ PLTE, tRNS)
+};
+
+struct PngMeta {
+    int64_t zlen, file_len, off;               // zlib stream bytes; file bytes; offset in the output (-1: none)
+    uint32_t adler, crc, hbits, tot_bits;       // Adler-32, CRC-32 (XOR-accumulated), header bits, codes' bits
+    int32_t stored, status, pad0, pad1;
+};
+
+struct PngBatch {
+    const PngImg* img;
+    int32_t n, uniform;                         // uniform: every image has the same geometry
+    int32_t rows_per, pblk_per, grp_per, eblk_per, cblk_per;   // per-image counts when uniform
+    int32_t total_grp, pad;
+    const int32_t* row0;                        // [n] first global row etc. (binary search when not uniform)
+    const int32_t* pblk0;
+    const int32_t* grp0;
+    const int32_t* eblk0;
+    const int32_t* cblk0;
+    uint8_t* flt;
+    uint32_t* tokens;                           // [segments][kSeg]
+    uint16_t* ntok;                             // [segments]
+    uint32_t* segb;                             // [segments] bit offset within the group
+    uint32_t* gsum;                             // [groups] bits of the group
+    uint32_t* goff;                             // [groups] bit offset of the group in its stream
+    uint32_t* hist;                             // [n][316]
+    DflTables* tab;                             // [n]
+    PngMeta* meta;                              // [n]
+    unsigned long long* row_sums;               // [rows][2]
+    uint32_t* words;                            // deflate streams
+    uint8_t* out;
+    uint64_t out_cap;
+    uint64_t* d_offsets;
+    uint32_t* d_lengths;
+    int32_t* d_status;
+    const uint32_t* crc_pow;                    // [kCrcPowLo + kCrcPowHi]
+};
+
+// Image owning global item `x` of a stage whose per-image first items are `first` (sorted).
+__device__ __forceinline__ int pngb_image(const PngBatch& B, const int32_t* first, int32_t per, int64_t x) {
+    if (B.uniform) return (int)(x / per);
+    int lo = 0, hi = B.n - 1;
+    while (lo < hi) {                           // last image whose first item <= x
+        const int mid = (lo + hi + 1) >> 1;
+        if (first[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ PngArgs pngb_args(const PngImg& I) {
+    PngArgs A{};
+    A.argb = I.argb;
+    A.bits = I.bits;
+    A.kind = I.kind;
+    A.W = I.W;
+    A.H = I.H;
+    A.flip_h = I.flip_h;
+    A.flip_v = I.flip_v;
+    A.rowlen = I.rowlen;
+    A.raw = I.raw;
+    A.nblk = I.nblk;
+    return A;
+}
+
+// x^(8*256*j) mod P: [0, 4096) for j, [4096, 6144) for j * 4096 (one lane per entry).
+__global__ void __launch_bounds__(256) k_png_crc_pow(uint32_t* __restrict__ pw) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kCrcPowLo + kCrcPowHi) return;
+    const uint64_t j = i < kCrcPowLo ? (uint64_t)i : (uint64_t)(i - kCrcPowLo) * kCrcPowLo;
+    pw[i] = x2nmodp(j * 256, 3);
+}
+
+__global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
+    const int i = pngb_image(B, B.row0, B.rows_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const int y = (int)blockIdx.x - (B.uniform ? i * B.rows_per : I.row0);
+    png_filter_row(pngb_args(I), I.bpp, y, B.flt + I.flt, B.row_sums + 2 * (int64_t)blockIdx.x, s_rows);
+}
+
+__global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
+    const int i = pngb_image(B, B.pblk0, B.pblk_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
+    uint32_t* h = B.hist + (size_t)i * 316;
+    png_lz_parse_block(B.flt + I.flt, I.raw, I.rowlen, I.bpp, I.nseg, blk, I.back, B.tokens + I.seg0 * kSeg,
+                       B.ntok + I.seg0, h, h + 286, s_win);
+}
+
+__global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
+    png_build_tables(B.hist + (size_t)blockIdx.x * 316, B.tab + blockIdx.x);
+}
+
+__device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t w = lane < nw ? s_wave[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;
+    }
+    __syncthreads();
+    const uint32_t off = wid ? s_wave[wid - 1] : 0;
+    total = s_wave[nw - 1];
+    __syncthreads();
+    return off + x - v;
+}
+
+// P4: one lane per segment (256 per workgroup = one group, never straddling images).
+__global__ void __launch_bounds__(kPngbGroup) k_pngb_bits(PngBatch B) {
+    __shared__ uint8_t llen[286], dlen[30];
+    __shared__ uint32_t s_wave[kPngbGroup / 64];
+    const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const int64_t gl = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.grp_per : I.grp0);
+    const DflTables* T = B.tab + i;
+    for (int k = threadIdx.x; k < 286; k += kPngbGroup) llen[k] = T->llen[k];
+    if (threadIdx.x < 30) dlen[threadIdx.x] = T->dlen[threadIdx.x];
+    __syncthreads();
+    const int64_t ls = gl * kPngbGroup + threadIdx.x;     // segment within the image
+    uint32_t b = 0;
+    if (ls < I.nseg) {
+        const int64_t s = I.seg0 + ls;
+        const uint32_t* tok = B.tokens + s * kSeg;
+        const int nt = B.ntok[s];
+        for (int k = 0; k < nt; ++k) b += token_bits(tok[k], llen, dlen);
+    }
+    uint32_t total;
+    const uint32_t ex = pngb_block_excl_scan(b, s_wave, total);
+    if (ls < I.nseg) B.segb[I.seg0 + ls] = ex;
+    if (threadIdx.x == 0) B.gsum[blockIdx.x] = total;
+}
+
+// P5: one workgroup per image.
+__global__ void __launch_bounds__(256) k_pngb_scan(PngBatch B) {
+    __shared__ uint32_t s_wave[4];
+    __shared__ unsigned long long s_ad[2][4];
+    __shared__ uint32_t s_carry;
+    const int i = blockIdx.x;
+    const PngImg& I = B.img[i];
+    const DflTables* T = B.tab + i;
+    const int ng = (int)((I.nseg + kPngbGroup - 1) / kPngbGroup);
+    const uint32_t hb = T->hdr[95];
+    if (threadIdx.x == 0) s_carry = hb;
+    __syncthreads();
+    for (int g0 = 0; g0 < ng; g0 += 256) {              // group offsets: header bits + exclusive scan
+        const int g = g0 + threadIdx.x;
+        const uint32_t v = g < ng ? B.gsum[I.grp0 + g] : 0u;
+        uint32_t tot;
+        const uint32_t ex = pngb_block_excl_scan(v, s_wave, tot);
+        const uint32_t base = s_carry;
+        if (g < ng) B.goff[I.grp0 + g] = base + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = base + tot;
+        __syncthreads();
+    }
+    const uint32_t eob = s_carry;                      // header + codes
+    const uint32_t eob_n = T->llen[256];
+    const int64_t dbytes = ((int64_t)eob + eob_n + 7) / 8;
+    const int64_t zdyn = 2 + dbytes + 4, zstored = 2 + 5 * I.nblk + I.raw + 4;
+    const bool stored = zdyn >= zstored;
+    // Adler-32 of the filtered stream from the row partials (the same bytes either way)
+    unsigned long long s1 = 0, s2 = 0;
+    for (int y = threadIdx.x; y < I.H; y += 256) {
+        s1 += B.row_sums[2 * ((int64_t)I.row0 + y)];
+        s2 += B.row_sums[2 * ((int64_t)I.row0 + y) + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_down(s1, o, 64);
+        s2 += __shfl_down(s2, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) { s_ad[0][threadIdx.x >> 6] = s1; s_ad[1][threadIdx.x >> 6] = s2; }
+    uint32_t* w = B.words + I.words;
+    if (!stored) {                                     // zero the words the groups OR into
+        for (int g = threadIdx.x; g < ng; g += 256) {
+            const uint32_t o = B.goff[I.grp0 + g], n = B.gsum[I.grp0 + g];
+            w[o >> 5] = 0;
+            if (n) w[(o + n - 1) >> 5] = 0;
+        }
+        for (uint32_t k = threadIdx.x; k <= (hb >> 5); k += 256) w[k] = 0;
+        if (threadIdx.x == 0) {
+            w[eob >> 5] = 0;
+            w[(eob + eob_n - 1) >> 5] = 0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!stored) {
+            for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&w[k], T->hdr[k]);
+            const uint32_t v = T->lcode[256], sh = eob & 31;
+            atomicOr(&w[eob >> 5], v << sh);
+            if (sh + eob_n > 32) atomicOr(&w[(eob >> 5) + 1], v >> (32 - sh));
+        }
+        const unsigned long long a1 = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
+        const unsigned long long a2 = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
+        const uint64_t a = (1 + a1) % 65521, b = ((uint64_t)I.raw % 65521 + a2 % 65521) % 65521;
+        PngMeta& M = B.meta[i];
+        M.zlen = stored ? zstored : zdyn;
+        M.file_len = I.pre_len + 8 + M.zlen + 4 + 12;
+        M.off = -1;
+        M.adler = (uint32_t)((b << 16) | a);
+        M.crc = 0;
+        M.hbits = hb;
+        M.tot_bits = eob - hb;
+        M.stored = stored ? 1 : 0;
+        M.status = OMR_OK;
+    }
+}
+
+// P6: one workgroup: each file's offset (16-byte aligned slots, in image order) and status.
+__global__ void __launch_bounds__(1024) k_pngb_offsets(PngBatch B) {
+    __shared__ unsigned long long s_wave[16];
+    __shared__ unsigned long long s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int i0 = 0; i0 < B.n; i0 += 1024) {
+        const int i = i0 + threadIdx.x;
+        const unsigned long long v = i < B.n ? ((unsigned long long)B.meta[i].file_len + 15ull) & ~15ull : 0ull;
+        unsigned long long x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_wave[wid] = x;
+        __syncthreads();
+        if (wid == 0) {
+            unsigned long long t = lane < 16 ? s_wave[lane] : 0ull;
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {
+                const unsigned long long y = __shfl_up(t, o, 64);
+                if (lane >= o) t += y;
+            }
+            if (lane < 16) s_wave[lane] = t;
+        }
+        __syncthreads();
+        const unsigned long long base = s_carry, ex = base + (wid ? s_wave[wid - 1] : 0ull) + x - v;
+        if (i < B.n) {
+            PngMeta& M = B.meta[i];
+            const bool fits = ex + v <= B.out_cap;       // the whole 16-byte slot (P8 stores 16 B)
+            M.off = fits ? (int64_t)ex : -1;
+            M.status = fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
+            if (B.d_offsets) B.d_offsets[i] = fits ? ex : 0ull;
+            if (B.d_lengths) B.d_lengths[i] = fits ? (uint32_t)M.file_len : 0u;
+            if (B.d_status) B.d_status[i] = M.status;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = base + s_wave[15];
+        __syncthreads();
+    }
+}
+
+// P7: one workgroup per group of 256 segments: the group's codes are one contiguous run of the
+// stream, assembled in LDS (ds_or: neighbouring lanes share boundary words) and copied out; the
+// run's first and last words are ORed into memory (shared with the neighbouring groups, the
+// header or the EOB, zeroed by P5), interior words stored.
+__global__ void __launch_bounds__(kPngbGroup) k_pngb_write(PngBatch B) {
+    __shared__ uint8_t llen[286], dlen[30];
+    __shared__ uint16_t lcode[286], dcode[30];
+    __shared__ uint32_t sw[kPngbGroupWords];
+    const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    if (B.meta[i].stored) return;
+    const int64_t gl = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.grp_per : I.grp0);
+    const DflTables* T = B.tab + i;
+    for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = T->llen[k]; lcode[k] = T->lcode[k]; }
+    if (threadIdx.x < 30) { dlen[threadIdx.x] = T->dlen[threadIdx.x]; dcode[threadIdx.x] = T->dcode[threadIdx.x]; }
+    for (int k = threadIdx.x; k < kPngbGroupWords; k += kPngbGroup) sw[k] = 0;
+    __syncthreads();
+    const uint32_t gbase = B.goff[blockIdx.x], gbits = B.gsum[blockIdx.x];
+    const int64_t ls = gl * kPngbGroup + threadIdx.x;
+    if (ls < I.nseg) {
+        const int64_t s = I.seg0 + ls;
+        const uint32_t* tok = B.tokens + s * kSeg;
+        const int nt = B.ntok[s];
+        const uint32_t pos = (gbase & 31) + B.segb[s];     // bit position in sw
+        uint64_t acc = 0;
+        int nacc = (int)(pos & 31);
+        uint32_t wpos = pos >> 5;
+        auto put = [&](uint32_t v, int n) {                // LSB-first into a 64-bit accumulator
+            acc |= (uint64_t)(v & ((1u << n) - 1)) << nacc;
+            nacc += n;
+            if (nacc >= 32) {
+                atomicOr(&sw[wpos], (uint32_t)acc);
+                ++wpos;
+                acc >>= 32;
+                nacc -= 32;
+            }
+        };
+        for (int k = 0; k < nt; ++k) {
+            const uint32_t t = tok[k];
+            if (!(t & 0x80000000u)) {
+                put(lcode[t], llen[t]);
+            } else {
+                const uint32_t l = (t & 0xFF) + 3, d = ((t >> 8) & 0x7FFF) + 1;
+                const int lsym = c_dfl.len_sym[l], ds = dist_sym(d);
+                put(lcode[lsym], llen[lsym]);
+                if (c_dfl.len_xbits[lsym - 257]) put(l - c_dfl.len_base[lsym - 257], c_dfl.len_xbits[lsym - 257]);
+                put(dcode[ds], dlen[ds]);
+                if (c_dfl.dist_xbits[ds]) put(d - c_dfl.dist_base[ds], c_dfl.dist_xbits[ds]);
+            }
+        }
+        if (nacc > 0) atomicOr(&sw[wpos], (uint32_t)acc);
+    }
+    __syncthreads();
+    if (!gbits) return;
+    uint32_t* w = B.words + I.words;
+    const uint32_t w0 = gbase >> 5, w1 = (gbase + gbits - 1) >> 5;
+    for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup) {
+        const uint32_t v = sw[k - w0];
+        if (k == w0 || k == w1) atomicOr(&w[k], v);
+        else w[k] = v;
+    }
+}
+
+__constant__ uint8_t c_iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+
+// Byte k of image I's file (P8's general path).
+__device__ uint32_t pngb_file_byte(const PngBatch& B, const PngImg& I, const PngMeta& M, int64_t k) {
+    const int64_t P = I.pre_len;
+    if (k < P) return I.pre[k];
+    k -= P;
+    if (k < 4) return (uint32_t)(M.zlen >> (24 - 8 * k)) & 0xFF;
+    if (k < 8) return (uint32_t)"IDAT"[k - 4];
+    k -= 8;
+    if (k < M.zlen) {
+        if (k == 0) return 0x78;                       // CMF/FLG: deflate, 32K window, check bits
+        if (k == 1) return 0x01;
+        if (k >= M.zlen - 4) return (M.adler >> (8 * (M.zlen - 1 - k))) & 0xFF;
+        const int64_t d = k - 2;
+        if (!M.stored) return reinterpret_cast<const uint8_t*>(B.words + I.words)[d];
+        const int64_t b = d / (kStored + 5), o = d - b * (kStored + 5);
+        if (o >= 5) return B.flt[I.flt + b * kStored + (o - 5)];
+        const uint32_t len = (uint32_t)min((int64_t)kStored, I.raw - b * kStored);
+        switch (o) {
+        case 0: return b == I.nblk - 1 ? 1u : 0u;       // BFINAL, BTYPE=00
+        case 1: return len & 0xFF;
+        case 2: return (len >> 8) & 0xFF;
+        case 3: return (~len) & 0xFF;
+        default: return ((~len) >> 8) & 0xFF;
+        }
+    }
+    k -= M.zlen;
+    if (k < 4) return 0;                               // CRC: P10
+    k -= 4;
+    return k < 12 ? c_iend[k] : 0u;
+}
+
+// P8: 16 bytes of one file per lane, one aligned 16-byte store.
+__global__ void __launch_bounds__(256) k_pngb_emit(PngBatch B) {
+    const int i = pngb_image(B, B.eblk0, B.eblk_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const PngMeta& M = B.meta[i];
+    const int64_t lb = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.eblk_per : I.eblk0);
+    const int64_t k0 = (lb * 256 + threadIdx.x) * 16;
+    if (M.off < 0 || k0 >= M.file_len) return;
+    uint32_t o[4];
+    const int64_t d0 = k0 - I.pre_len - 10;            // deflate byte of k0 (dynamic stream)
+    if (!M.stored && d0 >= 0 && k0 + 16 <= I.pre_len + 8 + M.zlen - 4) {
+        const uint32_t* w = B.words + I.words + (d0 >> 2);
+        const int sh = (int)(d0 & 3) * 8;
+        uint32_t x[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) x[j] = w[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = sh ? (x[j] >> sh) | (x[j + 1] << (32 - sh)) : x[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int64_t k = k0 + 4 * j + b;
+                if (k < M.file_len) v |= pngb_file_byte(B, I, M, k) << (8 * b);
+            }
+            o[j] = v;
+        }
+    }
+    *reinterpret_cast<uint4*>(B.out + M.off + k0) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {   // unaligned 32-bit load
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const int sh = (int)(a & 3) * 8;
+    const uint32_t w0 = q[0];
+    return sh ? (w0 >> sh) | (q[1] << (32 - sh)) : w0;
+}
+
+// P9: CRC-32 of 'IDAT' + zlib stream (4 + zlen bytes) in the output.  Lane j (per image) owns the
+// 256 bytes ending 256*j bytes before the end: its CRC times x^(8*256*j) (two table products)
+// is its share of the whole CRC (the init / final XOR terms telescope), XOR-combined per image.
+__global__ void __launch_bounds__(256) k_pngb_crc(PngBatch B) {
+    __shared__ uint32_t t[8][256];
+    __shared__ uint32_t s_x[4];
+    for (int k = threadIdx.x; k < 8 * 256; k += 256) t[k >> 8][k & 255] = c_crc8.t[k >> 8][k & 255];
+    __syncthreads();
+    const int i = pngb_image(B, B.cblk0, B.cblk_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const PngMeta& M = B.meta[i];
+    if (M.off < 0) return;
+    const int64_t lb = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.cblk_per : I.cblk0);
+    const int64_t j = lb * 256 + threadIdx.x;
+    const int64_t n = 4 + M.zlen, hi = n - 256 * j, lo = max((int64_t)0, hi - 256);
+    uint32_t v = 0;
+    if (hi > 0) {
+        const uint8_t* d = B.out + M.off + I.pre_len + 4;
+        uint32_t r = 0xFFFFFFFFu;
+        int64_t q = lo;
+        for (; q + 8 <= hi; q += 8) {
+            const uint32_t w0 = load_u32_any(d + q) ^ r, w1 = load_u32_any(d + q + 4);
+            r = t[7][w0 & 0xFF] ^ t[6][(w0 >> 8) & 0xFF] ^ t[5][(w0 >> 16) & 0xFF] ^ t[4][w0 >> 24] ^
+                t[3][w1 & 0xFF] ^ t[2][(w1 >> 8) & 0xFF] ^ t[1][(w1 >> 16) & 0xFF] ^ t[0][w1 >> 24];
+        }
+        for (; q < hi; ++q) r = t[0][(r ^ d[q]) & 0xFF] ^ (r >> 8);
+        v = ~r;
+        if (j) {
+            v = multmodp(B.crc_pow[j & (kCrcPowLo - 1)], v);
+            if (j >= kCrcPowLo) v = multmodp(B.crc_pow[kCrcPowLo + (j / kCrcPowLo)], v);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) s_x[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t x = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
+        if (x) atomicXor(&B.meta[i].crc, x);
+    }
+}
+
+// P10: the CRC bytes after the zlib stream.
+__global__ void __launch_bounds__(256) k_pngb_finish(PngBatch B) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= B.n) return;
+    const PngMeta& M = B.meta[i];
+    if (M.off < 0) return;
+    uint8_t* c = B.out + M.off + B.img[i].pre_len + 8 + M.zlen;
+    const uint32_t crc = M.crc;
+    c[0] = crc >> 24; c[1] = crc >> 16; c[2] = crc >> 8; c[3] = crc;
+}
+
+// One image of a batch as the host describes it.
+struct PngImgHost {
+    const uint32_t* argb;
+    const uint8_t* bits;
+    int kind, W, H, flip_h, flip_v;
+    uint8_t rgba[4];
+};
+
+static int png_prefix(int kind, int W, int H, const uint8_t* rgba, uint8_t* pre) {
+    std::vector<uint8_t> v;
+    const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+    v.insert(v.end(), sig, sig + 8);
+    uint8_t ihdr[13];
+    ihdr[0] = W >> 24; ihdr[1] = W >> 16; ihdr[2] = W >> 8; ihdr[3] = W;
+    ihdr[4] = H >> 24; ihdr[5] = H >> 16; ihdr[6] = H >> 8; ihdr[7] = H;
+    ihdr[8] = kind == kIdx1 ? 1 : 8;
+    ihdr[9] = kind == kRgb ? 2 : 3;   // truecolour / indexed
+    ihdr[10] = ihdr[11] = ihdr[12] = 0;
+    put_chunk(v, "IHDR", ihdr, 13);
+    if (kind != kRgb) {
+        const uint8_t plte[6] = {0, 0, 0, rgba[0], rgba[1], rgba[2]};
+        put_chunk(v, "PLTE", plte, 6);
+        const uint8_t trns[2] = {0, rgba[3]};
+        put_chunk(v, "tRNS", trns, 2);
+    }
+    std::memcpy(pre, v.data(), v.size());
+    return (int)v.size();
+}
+
+static omr_status ensure_crc_pow(Ctx* ctx) {
+    if (ctx->d_crc_pow) return OMR_OK;
+    OMR_HIP(ctx, hipMalloc(&ctx->d_crc_pow, sizeof(uint32_t) * (kCrcPowLo + kCrcPowHi)));
+    hipLaunchKernelGGL(k_png_crc_pow, dim3((kCrcPowLo + kCrcPowHi + 255) / 256), dim3(256), 0, ctx->stream,
+                       ctx->d_crc_pow);
+    OMR_HIP(ctx, hipGetLastError());
+    return OMR_OK;
+}
+
+// Geometry, grids and scratch layout of one batch (no pointers yet): plan_png_batch, then the
+// caller sizes the workspace, then launch_png_batch.
+struct PngBatchPlan {
+    std::vector<PngImg> I;
+    std::vector<int32_t> firsts;
+    int64_t rows = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, flt = 0, words = 0;
+    size_t rows_lds = 16, parse_lds = 16;
+    bool uniform = true;
+    size_t o_img, o_first, o_flt, o_tok, o_ntok, o_segb, o_gsum, o_goff, o_hist, o_tab, o_meta, o_rows, o_words;
+    size_t scratch = 0;
+};
+
+static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatchPlan& L) {
+    L.I.assign(n, PngImg{});
+    L.firsts.assign(5 * (size_t)n, 0);
+    for (int i = 0; i < n; ++i) {
+        const PngImgHost& h = im[i];
+        const PngPlan P = png_plan(h.kind, h.W, h.H);
+        PngImg& d = L.I[i];
+        d.kind = h.kind;
+        d.W = h.W;
+        d.H = h.H;
+        d.flip_h = h.flip_h;
+        d.flip_v = h.flip_v;
+        d.bpp = h.kind == kRgb ? 3 : 1;
+        d.rowlen = P.rowlen;
+        d.raw = P.raw;
+        d.nblk = P.nblk;
+        d.nseg = (P.raw + kSeg - 1) / kSeg;
+        d.back = (int32_t)align_up((size_t)std::min<int64_t>(std::max<int64_t>(P.rowlen, 2 * d.bpp), kMaxBack), 16);
+        d.pre_len = png_prefix(h.kind, h.W, h.H, h.rgba, d.pre);
+        const int64_t npb = (d.nseg + kParseLanes - 1) / kParseLanes, ng = (d.nseg + kPngbGroup - 1) / kPngbGroup;
+        const int64_t max_file = d.pre_len + 8 + P.zlen + 4 + 12;
+        const int64_t ne = (max_file + kPngbEmitBytes - 1) / kPngbEmitBytes;
+        const int64_t nc = (4 + P.zlen + kPngbCrcBytes - 1) / kPngbCrcBytes;
+        if (L.rows + h.H > INT32_MAX || L.pblk + npb > INT32_MAX || L.grp + ng > INT32_MAX ||
+            L.eblk + ne > INT32_MAX || L.cblk + nc > INT32_MAX)
+            return fail(ctx, OMR_INVALID_ARGUMENT, "PNG batch too large");
+        d.row0 = (int32_t)L.rows;
+        d.pblk0 = (int32_t)L.pblk;
+        d.grp0 = (int32_t)L.grp;
+        d.eblk0 = L.eblk;
+        d.cblk0 = L.cblk;
+        d.seg0 = L.segs;
+        d.flt = L.flt;
+        d.words = L.words;
+        L.firsts[i] = d.row0;
+        L.firsts[n + i] = d.pblk0;
+        L.firsts[2 * (size_t)n + i] = d.grp0;
+        L.firsts[3 * (size_t)n + i] = (int32_t)d.eblk0;
+        L.firsts[4 * (size_t)n + i] = (int32_t)d.cblk0;
+        L.rows += h.H;
+        L.pblk += npb;
+        L.grp += ng;
+        L.eblk += ne;
+        L.cblk += nc;
+        L.segs += d.nseg;
+        L.flt += (int64_t)align_up((size_t)P.raw, 16);
+        L.words += (int64_t)align_up((size_t)(P.raw / 2 + 128), 4);     // <= 16 bits per byte + header
+        L.rows_lds = std::max(L.rows_lds, align_up(2 * (size_t)(P.rowlen - 1), 16));
+        L.parse_lds = std::max(L.parse_lds, (size_t)d.back + (size_t)kParseLanes * kSeg);
+        if (i && (h.kind != im[0].kind || h.W != im[0].W || h.H != im[0].H)) L.uniform = false;
+    }
+    size_t o = 0;
+    auto take = [&](size_t b) { const size_t r = o; o = align_up(o + b, 256); return r; };
+    L.o_img = take(sizeof(PngImg) * n);
+    L.o_first = take(sizeof(int32_t) * 5 * n);
+    L.o_flt = take((size_t)L.flt);
+    L.o_tok = take((size_t)L.segs * kSeg * 4);
+    L.o_ntok = take((size_t)L.segs * 2);
+    L.o_segb = take((size_t)L.segs * 4);
+    L.o_gsum = take((size_t)L.grp * 4);
+    L.o_goff = take((size_t)L.grp * 4);
+    L.o_hist = take((size_t)n * 316 * 4);
+    L.o_tab = take(sizeof(DflTables) * n);
+    L.o_meta = take(sizeof(PngMeta) * n);
+    L.o_rows = take((size_t)L.rows * 16);
+    L.o_words = take((size_t)L.words * 4 + 64);
+    L.scratch = o;
+    return OMR_OK;
+}
+
+// Encode images[0..n) into d_out (asynchronous on the context stream).  Scratch: the workspace
+// from ws_off on, already sized to ws_off + L.scratch (it must not hold the inputs).
+static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* im, int n, size_t ws_off,
+                                   uint8_t* d_out, size_t out_cap, uint64_t* d_offsets, uint32_t* d_lengths,
+                                   int32_t* d_status) {
+    if (n <= 0) return OMR_OK;
+    omr_status st = ensure_crc_pow(ctx);
+    if (st) return st;
+    for (int i = 0; i < n; ++i) {
+        L.I[i].argb = im[i].argb;
+        L.I[i].bits = im[i].bits;
+    }
+    std::vector<PngImg>& I = L.I;
+    std::vector<int32_t>& firsts = L.firsts;
+    const int64_t rows = L.rows, pblk = L.pblk, grp = L.grp, eblk = L.eblk, cblk = L.cblk;
+    const size_t rows_lds = L.rows_lds, parse_lds = L.parse_lds;
+    const bool uniform = L.uniform;
+    auto at = [&](size_t rel) { return ws_off + rel; };
+    const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt), o_tok = at(L.o_tok),
+                 o_ntok = at(L.o_ntok), o_segb = at(L.o_segb), o_gsum = at(L.o_gsum), o_goff = at(L.o_goff),
+                 o_hist = at(L.o_hist), o_tab = at(L.o_tab), o_meta = at(L.o_meta), o_rows = at(L.o_rows),
+                 o_words = at(L.o_words);
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    PngBatch Bt{};
+    Bt.img = reinterpret_cast<const PngImg*>(ws + o_img);
+    Bt.n = n;
+    Bt.uniform = uniform ? 1 : 0;
+    Bt.rows_per = im[0].H;
+    Bt.pblk_per = n > 1 ? I[1].pblk0 : (int32_t)pblk;
+    Bt.grp_per = n > 1 ? I[1].grp0 : (int32_t)grp;
+    Bt.eblk_per = n > 1 ? (int32_t)I[1].eblk0 : (int32_t)eblk;
+    Bt.cblk_per = n > 1 ? (int32_t)I[1].cblk0 : (int32_t)cblk;
+    Bt.total_grp = (int32_t)grp;
+    const int32_t* fd = reinterpret_cast<const int32_t*>(ws + o_first);
+    Bt.row0 = fd;
+    Bt.pblk0 = fd + n;
+    Bt.grp0 = fd + 2 * (size_t)n;
+    Bt.eblk0 = fd + 3 * (size_t)n;
+    Bt.cblk0 = fd + 4 * (size_t)n;
+    Bt.flt = ws + o_flt;
+    Bt.tokens = reinterpret_cast<uint32_t*>(ws + o_tok);
+    Bt.ntok = reinterpret_cast<uint16_t*>(ws + o_ntok);
+    Bt.segb = reinterpret_cast<uint32_t*>(ws + o_segb);
+    Bt.gsum = reinterpret_cast<uint32_t*>(ws + o_gsum);
+    Bt.goff = reinterpret_cast<uint32_t*>(ws + o_goff);
+    Bt.hist = reinterpret_cast<uint32_t*>(ws + o_hist);
+    Bt.tab = reinterpret_cast<DflTables*>(ws + o_tab);
+    Bt.meta = reinterpret_cast<PngMeta*>(ws + o_meta);
+    Bt.row_sums = reinterpret_cast<unsigned long long*>(ws + o_rows);
+    Bt.words = reinterpret_cast<uint32_t*>(ws + o_words);
+    Bt.out = d_out;
+    Bt.out_cap = out_cap;
+    Bt.d_offsets = d_offsets;
+    Bt.d_lengths = d_lengths;
+    Bt.d_status = d_status;
+    Bt.crc_pow = ctx->d_crc_pow;
+    st = stage_h2d2(ctx, ws + o_img, I.data(), sizeof(PngImg) * n, ws + o_first, firsts.data(),
+                    sizeof(int32_t) * 5 * n);
+    if (st) return st;
+    OMR_HIP(ctx, hipMemsetAsync(ws + o_hist, 0, (size_t)n * 316 * 4, ctx->stream));
+    if (rows_lds > (size_t)60 * 1024)
+        OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_filter),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds + 1024));
+    if (parse_lds > (size_t)60 * 1024)
+        OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_parse),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds + 2048));
+    hipStream_t s = ctx->stream;
+    hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)rows), dim3(256), rows_lds, s, Bt);
+    hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
+    hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_bits, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_scan, dim3((unsigned)n), dim3(256), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_offsets, dim3(1), dim3(1024), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_write, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_emit, dim3((unsigned)eblk), dim3(256), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_crc, dim3((unsigned)cblk), dim3(256), 0, s, Bt);
+    hipLaunchKernelGGL(k_pngb_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Bt);
+    OMR_HIP(ctx, hipGetLastError());
+    return OMR_OK;
+}
+
 }  // namespace omr
 
 using namespace omr;
@@ -1264,6 +1974,147 @@ omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int
     uint32_t* d = static_cast<uint32_t*>(ctx->ws);
     OMR_HIP(ctx, hipMemcpyAsync(d, argb, (size_t)width * height * 4, hipMemcpyHostToDevice, ctx->stream));
     return encode_png_ws(ctx, kRgb, d, nullptr, width, height, 0, 0, nullptr, img, out, cap, out_len);
+}
+
+omr_status omr_encode_png_batch_device(omr_ctx* ctx, const uint32_t* d_argb, int64_t tile_stride_px, int32_t n_tiles,
+                                       int32_t width, int32_t height, uint8_t* d_out, size_t out_cap,
+                                       uint64_t* d_offsets, uint32_t* d_lengths, int32_t* d_status) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (n_tiles < 0 || width <= 0 || height <= 0 || width > kPngbMaxSide || height > kPngbMaxSide)
+        return fail(ctx, OMR_INVALID_ARGUMENT, "bad PNG batch size (tiles up to 4096 x 4096)");
+    if (n_tiles == 0) return OMR_OK;
+    if (!d_argb || !d_out) return fail(ctx, OMR_INVALID_ARGUMENT, "null PNG batch buffer");
+    const int64_t px = (int64_t)width * height, stride = tile_stride_px ? tile_stride_px : px;
+    if (stride < px) return fail(ctx, OMR_INVALID_ARGUMENT, "tile stride below width*height");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    std::vector<PngImgHost> im(n_tiles);
+    for (int i = 0; i < n_tiles; ++i) im[i] = {d_argb + stride * i, nullptr, kRgb, width, height, 0, 0, {0, 0, 0, 0}};
+    PngBatchPlan L;
+    omr_status st = plan_png_batch(ctx, im.data(), n_tiles, L);
+    if (st) return st;
+    st = ensure_workspace(ctx, L.scratch);
+    if (st) return st;
+    return launch_png_batch(ctx, L, im.data(), n_tiles, 0, d_out, out_cap, d_offsets, d_lengths, d_status);
+}
+
+size_t omr_png_batch_max_bytes(int32_t width, int32_t height, int32_t channels, int32_t n) {
+    if (n <= 0) return 0;
+    return (size_t)n * align_up(omr_png_max_bytes(width, height, channels), 16);
+}
+
+omr_status omr_render_shape_mask_png_batch(omr_ctx* ctx, const omr_mask_job* jobs, int32_t n, uint8_t* out,
+                                           size_t cap, uint64_t* offsets, uint32_t* lengths, int32_t* status) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    if (n < 0 || (n && (!jobs || !offsets || !lengths || !status)))
+        return fail(ctx, OMR_INVALID_ARGUMENT, "bad mask batch arguments");
+    if (n == 0) return OMR_OK;
+    if (!out && cap) return fail(ctx, OMR_INVALID_ARGUMENT, "null output buffer");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    // Per mask: the single call's checks (each one the reference's 404, ShapeMaskVerticle.java:119-128)
+    // and its packed-buffer flip (w % 8 == 0 with a flip, :175-181); masks whose stream would not fit
+    // the batch's 32-bit bit offsets go through the single-mask path after the batch.
+    std::vector<PngImgHost> im;
+    std::vector<int> idx, big;
+    std::vector<std::vector<uint8_t>> flipped(n);
+    std::vector<size_t> boff;
+    size_t bits_total = 0;
+    for (int i = 0; i < n; ++i) {
+        const omr_mask_job& j = jobs[i];
+        offsets[i] = 0;
+        lengths[i] = 0;
+        status[i] = OMR_OK;
+        const int64_t npx = (int64_t)j.width * j.height;
+        if (j.width <= 0 || j.height <= 0 || npx > INT32_MAX || !j.bits || (int64_t)j.n_bytes * 8 < npx) {
+            status[i] = OMR_NOT_FOUND;
+            continue;
+        }
+        const uint8_t* bits = j.bits;
+        int fh = j.flip_h ? 1 : 0, fv = j.flip_v ? 1 : 0;
+        if (j.width % 8 == 0 && (fh || fv) && !(ctx->sem & OMR_SEM_MASK_PIXEL_FLIP)) {
+            if ((int64_t)j.n_bytes < npx) {        // ArrayIndexOutOfBoundsException in the packed flip
+                status[i] = OMR_NOT_FOUND;
+                continue;
+            }
+            std::vector<uint8_t>& f = flipped[i];
+            f.assign(j.n_bytes, 0);
+            for (int64_t y = 0; y < j.height; ++y) {
+                const int64_t drow = (fv ? j.height - 1 - y : y) * j.width;
+                for (int64_t x = 0; x < j.width; ++x) f[drow + (fh ? j.width - 1 - x : x)] = j.bits[y * j.width + x];
+            }
+            bits = f.data();
+            fh = fv = 0;
+        }
+        const int kind = j.width % 8 == 0 ? kIdx1 : kIdx8;
+        const PngPlan P = png_plan(kind, j.width, j.height);
+        if (P.raw > ((int64_t)1 << 27)) {                // > 2^31 bits worst case: single path
+            big.push_back(i);
+            continue;
+        }
+        PngImgHost h{nullptr, bits, kind, j.width, j.height, fh, fv, {j.rgba[0], j.rgba[1], j.rgba[2], j.rgba[3]}};
+        im.push_back(h);
+        idx.push_back(i);
+        boff.push_back(bits_total);
+        bits_total += align_up((size_t)((npx + 7) / 8), 16);
+    }
+    const int m = (int)im.size();
+    size_t used = 0;
+    if (m) {
+        PngBatchPlan L;
+        omr_status st = plan_png_batch(ctx, im.data(), m, L);
+        if (st) return st;
+        size_t dcap = 0;
+        for (int k = 0; k < m; ++k) dcap += align_up(omr_png_max_bytes(im[k].W, im[k].H, 1), 16);
+        dcap = std::min(dcap, cap & ~(size_t)15);      // whole 16-byte slots inside the caller's buffer
+        const size_t o_bits = 0, o_out = align_up(bits_total, 256), o_meta = o_out + align_up(dcap, 256);
+        const size_t o_scr = o_meta + align_up((size_t)m * 16, 256);
+        st = ensure_workspace(ctx, o_scr + L.scratch);
+        if (st) return st;
+        st = ensure_host_out(ctx, std::max(bits_total, (size_t)m * 16));
+        if (st) return st;
+        uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+        for (int k = 0; k < m; ++k) {
+            const size_t nb = (size_t)(((int64_t)im[k].W * im[k].H + 7) / 8);
+            std::memcpy(ctx->h_out + boff[k], im[k].bits, nb);
+            im[k].bits = ws + o_bits + boff[k];
+        }
+        OMR_HIP(ctx, hipMemcpyAsync(ws + o_bits, ctx->h_out, bits_total, hipMemcpyHostToDevice, ctx->stream));
+        uint64_t* d_off = reinterpret_cast<uint64_t*>(ws + o_meta);
+        uint32_t* d_len = reinterpret_cast<uint32_t*>(d_off + m);
+        int32_t* d_st = reinterpret_cast<int32_t*>(d_len + m);
+        st = launch_png_batch(ctx, L, im.data(), m, o_scr, ws + o_out, dcap, d_off, d_len, d_st);
+        if (st) return st;
+        OMR_HIP(ctx, hipMemcpyAsync(ctx->h_out, d_off, (size_t)m * 16, hipMemcpyDeviceToHost, ctx->stream));
+        OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        const uint64_t* h_off = reinterpret_cast<const uint64_t*>(ctx->h_out);
+        const uint32_t* h_len = reinterpret_cast<const uint32_t*>(h_off + m);
+        const int32_t* h_st = reinterpret_cast<const int32_t*>(h_len + m);
+        for (int k = 0; k < m; ++k) {
+            const int i = idx[k];
+            status[i] = h_st[k];
+            if (h_st[k] == OMR_OK) {
+                offsets[i] = h_off[k];
+                lengths[i] = h_len[k];
+                used = std::max<size_t>(used, align_up(h_off[k] + h_len[k], 16));
+            }
+        }
+        if (used) OMR_HIP(ctx, hipMemcpy(out, ws + o_out, used, hipMemcpyDeviceToHost));
+    }
+    for (int i : big) {                                 // rare: huge masks one at a time, appended
+        size_t len = 0;
+        const omr_mask_job& j = jobs[i];
+        const omr_status st = omr_render_shape_mask_png(ctx, j.bits, j.n_bytes, j.width, j.height, j.rgba, j.flip_h,
+                                                        j.flip_v, used < cap ? out + used : nullptr,
+                                                        used < cap ? cap - used : 0, &len);
+        status[i] = st;
+        if (st == OMR_OK) {
+            offsets[i] = used;
+            lengths[i] = (uint32_t)len;
+            used = align_up(used + len, 16);
+        } else if (st != OMR_BUFFER_TOO_SMALL && st != OMR_NOT_FOUND) {
+            return st;
+        }
+    }
+    return OMR_OK;
 }
 
 omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n_bytes, int32_t width,

@@ -20,6 +20,7 @@
 #include "omr_k2.h"
 
 #include <memory>
+#include <mutex>
 
 namespace omr {
 
@@ -271,23 +272,39 @@ __global__ void __launch_bounds__(256) k_build_thresh(const RenderPlan* __restri
     if (lane == 0) thr[a * 256 + c] = lo > khi ? 0xFFFFFFFFu : (uint32_t)lo;
 }
 
-// Buckets over the key range where a kModeThresh channel's code varies, [T[1] - 1, T[cmax]]
-// (origin one key below T[1] when T[1] > 0): bucket b covers 2^shift keys from origin + b·2^shift;
-// its entry is (#T <= its first key) | (#T in the rest of it) << 8, so K2 searches only the few
-// thresholds of its bucket (usually 0-2) instead of all 255.  K2 clamps the key into
-// [origin, T[cmax]] for the bucket index only (one med3): a key below T[1] lands in bucket 0
-// (base 0, and no threshold of it is <= the key), a key at or above T[cmax] in the last one
-// (every threshold of it is <= the key), so no range test is needed.
+// Buckets over the key range where a kModeThresh channel's code varies: bucket b covers 2^shift
+// keys from origin + b·2^shift; its entry is (#T <= its first key) | (#T in the rest of it) << 8,
+// so K2 searches only the few thresholds of its bucket (usually 0-2) instead of all 255.  The
+// origin sits one whole bucket below T[1] (round 3), so bucket 0 holds no threshold, and the
+// table runs on past T[cmax] to its full extent `hi`: K2 clamps the key into [origin, hi] for the
+// bucket index only (one med3), and a key below T[1] (bucket 0) or past T[cmax]'s bucket finds
+// len 0 -- no search.  Before, both clamped ends shared a bucket with a threshold, and every
+// pixel outside the window (half the plane for a window that starts above the data's median)
+// ran one search step.  The (origin, hi, shift) of each channel follow its buckets in the table.
 #ifndef OMR_K2_BUCKETS_LOG2
 #define OMR_K2_BUCKETS_LOG2 11
 #endif
 constexpr int kBucketsLog2 = OMR_K2_BUCKETS_LOG2, kBuckets = 1 << kBucketsLog2;
-// channels whose threshold + bucket tables fit K2's 48 KiB LDS budget (8 at 2048 buckets)
+// channels whose threshold + bucket tables fit K2's 48 KiB LDS budget (8 at 2048 buckets; the
+// 16-byte bucket maps ride on top)
 constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 2u * kBuckets));
 
-__device__ __forceinline__ uint32_t bucket_shift(uint32_t span) {
+// Bucket map of a channel with thresholds T[1] = t1 .. T[cmax] = k1: the smallest shift with
+// (k1 - t1) >> shift <= kBuckets - 2, origin = t1 - 2^shift (0 when t1 < 2^shift), hi = the last
+// key of bucket kBuckets - 1 (saturated at 2^32 - 1).
+struct BucketMap { uint32_t org, hi, sh, pad; };
+__device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1) {
+    const uint32_t span = k1 - t1;
     const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
-    return bits > (uint32_t)kBucketsLog2 ? bits - kBucketsLog2 : 0u;
+    uint32_t sh = bits > (uint32_t)kBucketsLog2 ? bits - kBucketsLog2 : 0u;
+    if ((span >> sh) > (uint32_t)kBuckets - 2u) ++sh;
+    BucketMap m;
+    m.sh = sh;
+    m.org = t1 >= (1u << sh) ? t1 - (1u << sh) : 0u;
+    const uint64_t end = (uint64_t)m.org + ((uint64_t)kBuckets << sh) - 1u;
+    m.hi = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end;
+    m.pad = 0;
+    return m;
 }
 
 // #{c in 1..255 : T[c] <= key} over the sorted thresholds.
@@ -298,7 +315,7 @@ __device__ __forceinline__ uint32_t thresh_count(const uint32_t* __restrict__ T,
     return pos;
 }
 
-// grid: (kBuckets/256, n_active) x 256 threads.
+// grid: (kBuckets/256, n_active) x 256 threads; the maps follow the n_active bucket tables.
 __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restrict__ plan,
                                                        const uint32_t* __restrict__ thr,
                                                        uint16_t* __restrict__ bkt) {
@@ -307,16 +324,16 @@ __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restr
     const uint32_t* T = thr + a * 256;
     const uint32_t cmax = T[0] & 0xFFu;
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t k1 = cmax ? T[cmax] : 0u, org = cmax ? T[1] - (T[1] > 0u ? 1u : 0u) : 0u;
+    const uint32_t k1 = cmax ? T[cmax] : 0u;
+    const BucketMap m = bucket_map(cmax ? T[1] : 0u, k1);
+    if (b == 0) reinterpret_cast<BucketMap*>(bkt + gridDim.y * kBuckets)[a] = m;
     uint16_t e = 0;
     if (cmax) {
-        const uint32_t sh = bucket_shift(k1 - org);
-        const uint64_t ks = (uint64_t)org + ((uint64_t)b << sh);
-        if (ks <= k1) {
-            const uint64_t ke = std::min<uint64_t>(ks + (1ull << sh) - 1, (uint64_t)k1);
-            const uint32_t lo = thresh_count(T, (uint32_t)ks), hi = thresh_count(T, (uint32_t)ke);
-            e = (uint16_t)(lo | ((hi - lo) << 8));
-        }
+        const uint64_t ks = (uint64_t)m.org + ((uint64_t)b << m.sh);
+        const uint64_t ke = ks + (1ull << m.sh) - 1;
+        const uint32_t lo = thresh_count(T, (uint32_t)std::min<uint64_t>(ks, k1));
+        const uint32_t hi = thresh_count(T, (uint32_t)std::min<uint64_t>(ke, k1));
+        e = (uint16_t)(lo | ((hi - lo) << 8));
     }
     bkt[a * kBuckets + b] = e;
 }
@@ -329,7 +346,7 @@ constexpr int kCPT = OMR_K2_CPT;   // chunks per thread of the fixed-channel-cou
 // LDS of one K2 block: contrib [na][256] u32, then (kModeThresh) thresholds [na][256] u32 and
 // buckets [na][kBuckets] u16.
 __host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh) {
-    return (size_t)na * (1024 + (thresh ? 1024 + 2 * kBuckets : 0));
+    return (size_t)na * (1024 + (thresh ? 1024 + 2 * kBuckets + sizeof(BucketMap) : 0));
 }
 
 template <int MODE, int BPP>
@@ -344,7 +361,7 @@ __device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_con
                 *reinterpret_cast<uint4*>(s_thr + i) = *reinterpret_cast<const uint4*>(A.thresh + i);
             uint32_t* s_b = s_thr + na * 256;
             const uint32_t* g_b = reinterpret_cast<const uint32_t*>(A.buckets);
-            for (int i = threadIdx.x * 4; i < na * kBuckets / 2; i += kBlock * 4)
+            for (int i = threadIdx.x * 4; i < na * (kBuckets / 2 + 4); i += kBlock * 4)   // + the maps
                 *reinterpret_cast<uint4*>(s_b + i) = *reinterpret_cast<const uint4*>(g_b + i);
         }
     }
@@ -384,16 +401,15 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
             if (MODE == kK2Thresh || p.mode == kModeThresh) {          // uniform: bucket, then the few thresholds in it
                 const uint32_t* T = s_thr + a * 256;
                 const uint16_t* Bk = s_bkt + a * kBuckets;
-                const uint32_t meta = T[0];
-                const uint32_t cmax = meta & 0xFFu, cnan = (meta >> 8) & 0xFFu;
-                const uint32_t k1 = cmax ? T[cmax] : 0u, org = cmax ? T[1] - (T[1] > 0u ? 1u : 0u) : 0u;
-                const uint32_t sh = bucket_shift(k1 - org);
+                const uint32_t cnan = (T[0] >> 8) & 0xFFu;
+                const BucketMap& M = reinterpret_cast<const BucketMap*>(s_bkt + na * kBuckets)[a];
+                const uint32_t org = M.org, hi = M.hi, sh = M.sh;
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {
                     uint32_t raw = c.dw[j];
                     if constexpr (BE) raw = bswap32(raw);
                     const uint32_t key = raw_key<PT>(raw);
-                    const uint32_t e = Bk[(min(max(key, org), k1) - org) >> sh];
+                    const uint32_t e = Bk[(min(max(key, org), hi) - org) >> sh];
                     uint32_t base = e & 0xFFu;
                     uint32_t len = e >> 8;
                     while (len > 0) {
@@ -769,7 +785,7 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
     L.contrib_off = align_up(sizeof(RenderPlan), 256);
     L.thresh_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
     L.bucket_off = L.thresh_off + align_up((size_t)kMaxActive * 256 * 4, 256);
-    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * kBuckets * 2, 256);
+    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * (kBuckets * 2 + sizeof(BucketMap)), 256);
     L.extra_off = L.lut_off + align_up(pp.lut_bytes, 256);
     L.total = L.extra_off + extra;
     return L;
@@ -782,11 +798,26 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
 static thread_local int tl_cu_count = 0;
 template <auto KERN>
 static int pipe_grid(const K2Args& a, int grid, size_t lds) {
-    static const int occ = [&] {                       // one query per instantiation
-        int o = 0;
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, KERN, kBlock, lds) == hipSuccess ? o : 0;
-    }();
-    if (occ <= 0 || tl_cu_count <= 0) return grid;
+    // occupancy per (device, LDS bytes) of this instantiation: the LDS footprint differs between
+    // launches (threshold tables or not), and a pool's batchers launch it on several devices
+    struct Entry { int dev; size_t lds; int occ; };
+    static std::mutex mu;
+    static Entry cache[16];
+    static int n_cache = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || tl_cu_count <= 0) return grid;
+    int occ = -1;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (int i = 0; i < n_cache; ++i)
+            if (cache[i].dev == dev && cache[i].lds == lds) { occ = cache[i].occ; break; }
+        if (occ < 0) {
+            int o = 0;
+            occ = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, KERN, kBlock, lds) == hipSuccess ? o : 0;
+            if (n_cache < 16) cache[n_cache++] = {dev, lds, occ};
+        }
+    }
+    if (occ <= 0) return grid;
     return (int)std::min<uint64_t>(a.n_work, (uint64_t)tl_cu_count * (uint64_t)occ);
 }
 
@@ -921,8 +952,10 @@ bool fast16_f32_params(double a0, int64_t wsi, int32_t xmax, float* fa, float* f
     const int64_t tlo = -wsi, thi = (int64_t)xmax - wsi;
     int64_t bp[256];
     for (int k = 1; k <= 255; ++k) {
-        int64_t t = (int64_t)std::ceil((k - 0.5) / a0);
-        t = std::max<int64_t>(tlo, std::min<int64_t>(thi + 1, t));
+        // clamp in double before the conversion: a tiny a0 (a very wide window) puts the quotient
+        // past 2^63, where the int64 conversion is undefined
+        const double q = std::ceil((k - 0.5) / a0);
+        int64_t t = (int64_t)std::max<double>((double)tlo, std::min<double>((double)(thi + 1), q));
         while (t > tlo && host_fast16i(t - 1, a0) >= k) --t;
         while (t <= thi && host_fast16i(t, a0) < k) ++t;
         bp[k] = t;                                     // thi + 1: level k is never reached

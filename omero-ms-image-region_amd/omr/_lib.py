@@ -85,6 +85,12 @@ class TileJob(ctypes.Structure):
 FORMAT_JPEG, FORMAT_PNG, FORMAT_ARGB, FORMAT_TIFF = 0, 1, 2, 3
 
 
+class MaskJob(ctypes.Structure):
+    _fields_ = [("bits", ctypes.c_void_p), ("n_bytes", ctypes.c_size_t), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("rgba", ctypes.c_uint8 * 4), ("flip_h", ctypes.c_int32),
+                ("flip_v", ctypes.c_int32)]
+
+
 class Region(ctypes.Structure):
     _fields_ = [("x", ctypes.c_int32), ("y", ctypes.c_int32),
                 ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
@@ -198,6 +204,9 @@ _SIGS = {
     "omr_encode_png_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_render_shape_mask_png": (_i32, [_vp, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp, _sz,
                                          ctypes.POINTER(_sz)]),
+    "omr_encode_png_batch_device": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp]),
+    "omr_png_batch_max_bytes": (_sz, [_i32, _i32, _i32, _i32]),
+    "omr_render_shape_mask_png_batch": (_i32, [_vp, ctypes.POINTER(MaskJob), _i32, _vp, _sz, _vp, _vp, _vp]),
     "omr_split_html_color": (_i32, [ctypes.c_char_p, ctypes.POINTER(_i32)]),
     "omr_shape_mask_fill_color": (_i32, [_i32, _i32, ctypes.c_char_p, _vp]),
     "omr_get_region_def": (_i32, [_i32, ctypes.POINTER(Region), _i32, ctypes.POINTER(_i32), _i32,

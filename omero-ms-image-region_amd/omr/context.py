@@ -335,6 +335,35 @@ class Context:
         return self._encode(lib.omr_encode_png_device, d_argb, width, height,
                             cap=lib.omr_png_max_bytes(width, height, 3))
 
+    def encode_png_batch_device(self, d_argb, n_tiles, width, height, d_out, d_offsets=None, d_lengths=None,
+                                d_status=None, tile_stride=0):
+        """Batched PNG of n_tiles device ARGB tiles into d_out (device bytes); asynchronous."""
+        check(lib.omr_encode_png_batch_device(self.h, _ptr(d_argb), tile_stride, n_tiles, width, height,
+                                              _ptr(d_out), d_out.numel() * d_out.element_size(), _ptr(d_offsets),
+                                              _ptr(d_lengths), _ptr(d_status)), self.h)
+
+    def render_shape_mask_png_batch(self, masks, cap=None):
+        """masks: [(bits, width, height, rgba, flip_h, flip_v)] -> [(status, png bytes)] (host in/out)."""
+        n = len(masks)
+        keep = [np.frombuffer(bytes(m[0]), dtype=np.uint8).copy() if m[0] is not None else None for m in masks]
+        jobs = (_lib.MaskJob * max(n, 1))()
+        for i, (m, b) in enumerate(zip(masks, keep)):
+            jobs[i].bits = b.ctypes.data if b is not None and b.size else None
+            jobs[i].n_bytes = 0 if b is None else b.size
+            jobs[i].width, jobs[i].height = int(m[1]), int(m[2])
+            jobs[i].rgba[:] = [int(v) for v in m[3]]
+            jobs[i].flip_h, jobs[i].flip_v = int(bool(m[4])), int(bool(m[5]))
+        if cap is None:
+            cap = sum(lib.omr_png_batch_max_bytes(max(1, int(m[1])), max(1, int(m[2])), 1, 1) for m in masks)
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        offs = np.zeros(max(n, 1), np.uint64)
+        lens = np.zeros(max(n, 1), np.uint32)
+        stat = np.zeros(max(n, 1), np.int32)
+        check(lib.omr_render_shape_mask_png_batch(self.h, jobs, n, out.ctypes.data, cap, offs.ctypes.data,
+                                                  lens.ctypes.data, stat.ctypes.data), self.h)
+        return [(int(stat[i]), out[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes() if stat[i] == 0 else b"")
+                for i in range(n)]
+
     def encode_tiff(self, argb, width, height):
         argb = np.ascontiguousarray(argb, dtype=np.uint32)
         return self._encode(lib.omr_encode_tiff, argb, width, height,

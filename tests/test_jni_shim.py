@@ -153,6 +153,16 @@ def test_shape_mask_validation(fake):
     _raises(IA, "renderShapeMaskPng", 0, bits, 8, 8, M.jbytes(bytes(4)), 0, 0)
     _raises(IA, "renderShapeMaskPng", fake, bits, 8, 8, None, 0, 0)               # null colour
     _raises(IA, "renderShapeMaskPng", fake, bits, 8, 8, M.jbytes(bytes(3)), 0, 0)  # 3-byte colour
+    # The library's 404 cases are caught before any staging is pinned (the fake context has no
+    # library state behind it, so reaching omr_pinned_alloc would fail differently): huge sizes,
+    # w*h past a Java int, a mask shorter than w*h bits, a null mask, a zero size.
+    NF, col = _lib.NOT_FOUND, M.jbytes(bytes(4))
+    _raises(NF, "renderShapeMaskPng", fake, bits, 1 << 30, 1 << 30, col, 0, 0)
+    _raises(NF, "renderShapeMaskPng", fake, bits, 65536, 32768, col, 0, 0)        # 2^31 pixels
+    _raises(NF, "renderShapeMaskPng", fake, bits, 9, 8, col, 0, 0)                # 72 bits > 64
+    _raises(NF, "renderShapeMaskPng", fake, None, 8, 8, col, 0, 0)
+    _raises(NF, "renderShapeMaskPng", fake, bits, 0, 8, col, 0, 0)
+    _raises(NF, "renderShapeMaskPng", fake, bits, 8, -1, col, 1, 1)
 
 
 def test_batcher_and_pool_validation(fake):

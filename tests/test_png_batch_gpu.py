@@ -1,0 +1,247 @@
+"""Batched PNG (omr_encode_png_batch_device) and the shape-mask batch (omr_render_shape_mask_png_batch)
+on the GPU.
+
+The parity bar of PNG is decoded pixels: every file decodes (PIL) to the
+tile's RGB / the mask's palette image, every chunk CRC and the zlib Adler-32 check (PIL and zlib
+verify them).  Where the batch chose the dynamic-Huffman stream the file is also byte-identical to
+the single-tile encoder's (same filters, parse and code), so the batch is pinned to the path the
+round-1..3 PNG tests already cover; noise takes stored blocks (of the filtered rows) in the batch.
+Masks are checked against the CPU restatement's unpack/flip (oracle mask_indices), including the
+reference's 404 cases and its packed-buffer flip (ShapeMaskRequestHandler.java:165-207).
+"""
+import io
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from omr import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def decode(b):
+    from PIL import Image
+    return Image.open(io.BytesIO(b))
+
+
+def rgb_of(argb):
+    return np.stack([(argb >> 16) & 0xFF, (argb >> 8) & 0xFF, argb & 0xFF], -1).astype(np.uint8)
+
+
+def chunks(png):
+    assert png[:8] == b"\x89PNG\r\n\x1a\n"
+    i, out = 8, []
+    while i < len(png):
+        ln, = struct.unpack(">I", png[i:i + 4])
+        typ, data = png[i + 4:i + 8], png[i + 8:i + 8 + ln]
+        crc, = struct.unpack(">I", png[i + 8 + ln:i + 12 + ln])
+        assert zlib.crc32(png[i + 4:i + 8 + ln]) == crc, typ
+        out.append((typ, data))
+        i += 12 + ln
+    assert i == len(png) and out[-1][0] == b"IEND"
+    return out
+
+
+def idat_is_stored(png):
+    z = b"".join(d for t, d in chunks(png) if t == b"IDAT")
+    return (z[2] >> 1) & 3 == 0
+
+
+def tiles(kind, n, w, h, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        if kind == "noise":
+            a = rng.integers(0, 2**32, (h, w), dtype=np.uint64).astype(np.uint32)
+        elif kind == "flat":
+            a = np.full((h, w), 0xFF000000 | (i * 0x010203), np.uint32)
+        else:                                   # image-like: gradients, blocks, a little noise
+            yy, xx = np.mgrid[0:h, 0:w]
+            a = ((xx * 255 // max(w - 1, 1)) << 16 | (yy * 255 // max(h - 1, 1)) << 8 | ((xx + yy + i) % 256))
+            a = a.astype(np.uint32) | 0xFF000000
+            a[h // 4:h // 2, w // 5:w // 2] = 0xFF102030 + i
+            a ^= rng.integers(0, 3, (h, w), dtype=np.uint32)
+        out.append(a)
+    return np.stack(out)
+
+
+def encode_batch(ctx, argb, cap=None, stride=0):
+    import torch
+    n, h, w = argb.shape
+    d = torch.from_numpy(argb.view(np.int32).copy()).to("cuda")
+    if cap is None:
+        cap = _lib.lib.omr_png_batch_max_bytes(w, h, 3, n)
+    out = torch.empty(max(cap, 1), dtype=torch.uint8, device="cuda")
+    offs = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+    lens = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    stat = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ctx.encode_png_batch_device(d, n, w, h, out[:cap] if cap else out[:0], offs, lens, stat, tile_stride=stride)
+    torch.cuda.synchronize()
+    o, l, s, b = offs.cpu().numpy(), lens.cpu().numpy(), stat.cpu().numpy(), out.cpu().numpy()
+    return [(int(s[i]), int(o[i]), b[int(o[i]):int(o[i]) + int(l[i])].tobytes()) for i in range(n)]
+
+
+@pytest.mark.parametrize("kind,n,w,h", [("image", 1, 1024, 1024), ("image", 16, 256, 256), ("image", 3, 37, 53),
+                                        ("flat", 5, 64, 8), ("image", 7, 1, 1), ("noise", 4, 300, 230),
+                                        ("image", 2, 4096, 17)])
+def test_png_batch_decodes_and_matches_single(ctx, kind, n, w, h):
+    argb = tiles(kind, n, w, h, n * w + h)
+    res = encode_batch(ctx, argb)
+    for i, (st, off, png) in enumerate(res):
+        assert st == 0 and off % 16 == 0
+        chunks(png)
+        np.testing.assert_array_equal(np.asarray(decode(png)), rgb_of(argb[i]))
+        if kind == "noise":
+            assert idat_is_stored(png)
+        if not idat_is_stored(png):
+            assert png == ctx.encode_png(argb[i], w, h), f"tile {i}: dynamic stream differs from the single path"
+    offs = [r[1] for r in res]
+    assert offs == sorted(offs) and len(set(offs)) == n
+
+
+def test_png_batch_mixed_content_and_stride(ctx):
+    """Flat, image-like and noise tiles in one launch (each picks dynamic or stored on its own), and
+    a tile stride larger than the tile."""
+    import torch
+    w, h = 128, 96
+    argb = np.concatenate([tiles("flat", 2, w, h, 1), tiles("noise", 2, w, h, 2), tiles("image", 2, w, h, 3)])
+    n = len(argb)
+    pad = np.zeros((n, h + 3, w), np.uint32)
+    pad[:, :h] = argb
+    res = encode_batch(ctx, argb)
+    for i, (st, _, png) in enumerate(res):
+        assert st == 0
+        np.testing.assert_array_equal(np.asarray(decode(png)), rgb_of(argb[i]))
+    # strided: tile i at i * (h + 3) * w pixels
+    d = torch.from_numpy(pad.view(np.int32).reshape(-1)).to("cuda")
+    cap = _lib.lib.omr_png_batch_max_bytes(w, h, 3, n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(n, dtype=torch.int64, device="cuda")
+    lens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ctx.encode_png_batch_device(d, n, w, h, out, offs, lens, None, tile_stride=(h + 3) * w)
+    b, o, ln = out.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy()
+    for i in range(n):
+        assert b[o[i]:o[i] + ln[i]].tobytes() == res[i][2]
+
+
+def test_png_batch_output_too_small(ctx):
+    """Files that do not fit report OMR_BUFFER_TOO_SMALL with length 0; the ones before still land."""
+    argb = tiles("image", 4, 64, 64, 9)
+    full = encode_batch(ctx, argb)
+    need = full[1][1] + (len(full[1][2]) + 15) // 16 * 16   # room for exactly the first two 16-byte slots
+    res = encode_batch(ctx, argb, cap=need)
+    assert [r[0] for r in res] == [0, 0, _lib.BUFFER_TOO_SMALL, _lib.BUFFER_TOO_SMALL]
+    assert res[0][2] == full[0][2] and res[1][2] == full[1][2]
+    assert res[2][2] == b"" and res[3][2] == b""
+
+
+def test_png_batch_rendered_c2_tiles(ctx):
+    """The bench's workload: C2 tiles rendered on the GPU, batch-encoded, decoded == the oracle's ARGB."""
+    import torch
+    from omr.context import make_qdef
+    from omr.synthetic import c2_channels, tile_u16
+    n, t = 6, 256
+    chans = c2_channels(4)
+    planes = [[p.astype(">u2") for p in tile_u16(k, 4, t, t)] for k in range(n)]
+    base = torch.from_numpy(np.stack([np.stack(p) for p in planes]).view(np.uint8).reshape(-1).copy()).to("cuda")
+    argb = torch.empty((n, t, t), dtype=torch.int32, device="cuda")
+    plane = t * t * 2
+    ctx.render_batch_strided_device(make_qdef("rgb"), chans, base, 4 * plane, plane, n, _lib.PIXELS_UINT16, t, t,
+                                    argb, big_endian=True)
+    cap = _lib.lib.omr_png_batch_max_bytes(t, t, 3, n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    offs = torch.zeros(n, dtype=torch.int64, device="cuda")
+    lens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stat = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    ctx.encode_png_batch_device(argb, n, t, t, out, offs, lens, stat)
+    b, o, ln, s = out.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy(), stat.cpu().numpy()
+    for k in range(n):
+        assert s[k] == 0
+        st, exp = O.render(chans, planes[k], _lib.PIXELS_UINT16, t, t, big_endian=True)
+        assert st == 0
+        np.testing.assert_array_equal(np.asarray(decode(b[o[k]:o[k] + ln[k]].tobytes())), rgb_of(exp))
+
+
+def test_png_batch_errors(ctx):
+    import torch
+    d = torch.zeros(16, dtype=torch.int32, device="cuda")
+    out = torch.empty(4096, dtype=torch.uint8, device="cuda")
+    for w, h in [(0, 4), (4, 0), (4097, 1), (1, 4097)]:
+        with pytest.raises(_lib.OmrError):
+            ctx.encode_png_batch_device(d, 1, w, h, out)
+    ctx.encode_png_batch_device(d, 0, 4, 4, out)                      # nothing to do
+
+
+def mask_rgba(png):
+    return np.asarray(decode(png).convert("RGBA"))
+
+
+def expect_mask(bits, w, h, fh, fv, rgba):
+    st, idx = O.mask_indices(bits, w, h, fh, fv)
+    assert st == 0
+    exp = np.zeros((h, w, 4), np.uint8)
+    exp[idx == 1] = rgba
+    return exp
+
+
+@pytest.fixture
+def pixel_flip(ctx):
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+    with O.semantics(_lib.SEM_MASK_PIXEL_FLIP):
+        yield ctx
+    ctx.set_semantics(0)
+
+
+def test_mask_batch_mixed_sizes_colours_flips(pixel_flip):
+    ctx = pixel_flip
+    rng = np.random.default_rng(77)
+    masks = []
+    for k, (w, h) in enumerate([(8, 2), (4, 4), (64, 33), (37, 21), (1024, 1024), (1, 1), (333, 77), (16, 1)]):
+        bits = rng.integers(0, 256, (w * h + 7) // 8, dtype=np.uint8).tobytes()
+        rgba = tuple(int(v) for v in rng.integers(0, 256, 4))
+        masks.append((bits, w, h, rgba, bool(k & 1), bool(k & 2)))
+    res = ctx.render_shape_mask_png_batch(masks)
+    for (bits, w, h, rgba, fh, fv), (st, png) in zip(masks, res):
+        assert st == 0
+        chunks(png)
+        assert decode(png).size == (w, h)
+        np.testing.assert_array_equal(mask_rgba(png), expect_mask(bits, w, h, fh, fv, rgba))
+        assert png == ctx.render_shape_mask_png(bits, w, h, rgba, fh, fv) or idat_is_stored(png)
+
+
+def test_mask_batch_404_cases_and_packed_flip(ctx):
+    """Each mask fails alone, with the single call's outcome: short masks, zero sizes, a null mask
+    and (default semantics) the packed-buffer flip of a w % 8 == 0 mask: 404 when the buffer holds
+    fewer than w*h bytes, else the byte-flipped buffer rendered as packed bits."""
+    w, h = 16, 4
+    good = bytes(range(8))
+    big = bytes((i * 37) & 0xFF for i in range(w * h))        # w*h bytes: the packed flip succeeds
+    col = (255, 0, 0, 255)
+    masks = [(good, w, h, col, False, False), (bytes(2), w, h, col, False, False), (good, 0, h, col, False, False),
+             (None, w, h, col, False, False), (good, w, h, col, True, False), (big, w, h, col, True, True),
+             (good, 9, 3, col, True, False)]
+    res = ctx.render_shape_mask_png_batch(masks)
+    st = [r[0] for r in res]
+    assert st == [0, _lib.NOT_FOUND, _lib.NOT_FOUND, _lib.NOT_FOUND, _lib.NOT_FOUND, 0, 0], st
+    for m, (s, png) in zip(masks, res):
+        if m[0] is None:
+            continue
+        if s:
+            with pytest.raises(_lib.OmrError) as e:
+                ctx.render_shape_mask_png(*m)
+            assert e.value.status == s
+        else:
+            np.testing.assert_array_equal(mask_rgba(png), mask_rgba(ctx.render_shape_mask_png(*m)))
+
+
+def test_mask_batch_capacity(pixel_flip):
+    ctx = pixel_flip
+    masks = [(bytes([0x5A] * 128), 32, 32, (1, 2, 3, 4), False, False) for _ in range(3)]
+    full = ctx.render_shape_mask_png_batch(masks)
+    one = len(full[0][1])
+    res = ctx.render_shape_mask_png_batch(masks, cap=2 * ((one + 15) // 16 * 16) + 15)
+    assert [r[0] for r in res] == [0, 0, _lib.BUFFER_TOO_SMALL]
+    assert res[0][1] == full[0][1] and res[1][1] == full[1][1]

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""C2 -> JPEG (or, with JPEG_PROBE_CASE=c1, C1: 1-channel uint8 greyscale) on 64 tiles, unfused
+"""C2 -> JPEG (or, with JPEG_PROBE_CASE=c1, C1: 1-channel uint8 greyscale) on 64 tiles (JPEG_PROBE_TILES), unfused
 (K1+K2 then B1..B6) and fused (F1..B6), a few calls each: the program the JPEG PMC passes
 (tools/profile_jpeg_r02.sh) profile."""
 import os
@@ -17,7 +17,7 @@ def main():
     from omr.context import make_bindings, make_qdef
     from omr.synthetic import c2_channels
     import bench
-    B, T = 64, 1024
+    B, T = int(os.environ.get("JPEG_PROBE_TILES", "64")), 1024
     dev = torch.device("cuda", 0)
     ctx = omr.Context(0, torch_order=False)   # explicit syncs below, as the bench
     if os.environ.get("JPEG_PROBE_CASE", "c2") == "c1":

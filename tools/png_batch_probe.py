@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Batched PNG probe: C2 tiles rendered on the GPU, then omr_encode_png_batch_device at 64 and 256
+tiles per call (and the single-tile path for comparison); per-call ms, tiles/s, mean file size.
+One JSON line.  PNG_PROBE_SIZES=64,256 overrides the batch sizes."""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "omero-ms-image-region_amd"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    import torch
+    import omr
+    from omr import _lib
+    from omr.context import make_bindings, make_qdef
+    from omr.synthetic import c2_channels
+    import bench
+    T = 1024
+    sizes = [int(x) for x in os.environ.get("PNG_PROBE_SIZES", "64,256").split(",")]
+    B = max(sizes)
+    dev = torch.device("cuda", 0)
+    ctx = omr.Context(0, torch_order=False)
+    data, uniq, table = bench.build_batch(torch, B, 8, dev)
+    q, ch = make_qdef("rgb"), c2_channels(4)
+    binds = make_bindings(ch)
+    argb = torch.empty((B, T, T), dtype=torch.int32, device=dev)
+    pb = T * T * 2
+    torch.cuda.synchronize()
+    ctx.render_batch_strided_device(q, ch, data, 4 * pb, pb, B, _lib.PIXELS_UINT16, T, T, argb, big_endian=True,
+                                    bindings=binds)
+    ctx.synchronize()
+    cap = _lib.lib.omr_png_batch_max_bytes(T, T, 3, B)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    offs = torch.empty(B, dtype=torch.int64, device=dev)
+    lens = torch.empty(B, dtype=torch.int32, device=dev)
+    stat = torch.empty(B, dtype=torch.int32, device=dev)
+    res = {}
+    for n in sizes:
+        def step():
+            ctx.encode_png_batch_device(argb, n, T, T, out, offs, lens, stat)
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
+            step()
+            ctx.synchronize()
+        iters = max(3, int(2048 / n))
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            step()
+        ctx.synchronize()
+        el = time.perf_counter() - t0
+        ln = lens[:n].cpu().numpy()
+        res[f"batch{n}"] = {"ms_per_call": round(1e3 * el / iters, 4), "tiles_per_s": round(n * iters / el, 1),
+                            "mean_file_bytes": int(ln.mean()), "status_ok": int((stat[:n] == 0).sum().item())}
+    # single-tile path (host D3, one sync per tile)
+    t0 = time.perf_counter()
+    k = 32
+    for i in range(k):
+        ctx.encode_png_device(argb[i], T, T)
+    el = time.perf_counter() - t0
+    res["single"] = {"ms_per_tile": round(1e3 * el / k, 4), "tiles_per_s": round(k / el, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
