@@ -422,6 +422,29 @@ def _timed(torch, ctx, step, steps, warmup):
 C3_WINDOWS, C3_WINDOW_S = 7, 0.05
 
 
+def _gated_burst_ms(torch, ctx, launch, n, gate_ms=30.0):
+    """Average device time of `launch` over n back-to-back calls: the context stream is held by a
+    spin kernel (torch.cuda._sleep) while the host queues all n, so no launch waits on the host and
+    two events around the whole burst time only the kernels.  Per-launch HIP events on a ~17 us
+    kernel read 1-3 us long (their own dispatch and completion signalling); around a
+    burst of n launches that cost is paid once.  Returns None when torch has no _sleep."""
+    sleep = getattr(torch.cuda, "_sleep", None)
+    if sleep is None:
+        return None
+    s = ctx._ext_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    launch()                                                  # warm (tables, code objects)
+    ctx.synchronize()
+    with torch.cuda.stream(s):
+        sleep(int(gate_ms * 1e-3 * 2.4e9))                    # >= gate_ms at <= 2.4 GHz
+        e0.record(s)
+    for _ in range(n):
+        launch()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
 def _windows(sync, step, n_windows, window_s):
     """Throughput of `step` over n_windows back-to-back windows of at least window_s each (steps
     issued back to back, one `sync` closing each window): the median window rate, and every
@@ -513,6 +536,18 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
         two = _windows(sync2, step2, C3_WINDOWS, C3_WINDOW_S)
         assert torch.equal(outs[0], outs[1]), "two-stream C3 renders differ"
         k3 = avg.get(3, float("nan"))
+        k3_events = k3
+        burst = None
+        if os.environ.get("OMR_K3R", "0") in ("", "0"):
+            # the glue's K3 (all three stacks in one launch), 200 launches back to back behind a gate
+            outs3 = [torch.empty((S, S), dtype=torch.int16, device=dev) for _ in range(C)]
+
+            def k3_launch():
+                ctx.project_stacks_device(stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, outs3,
+                                          big_endian_in=True)
+            burst = _gated_burst_ms(torch, ctx, k3_launch, 200)
+            if burst is not None:
+                k3 = burst
         used_z = Z if alg == _lib.PROJECTION_MAX else Z - 1
         if os.environ.get("OMR_K3R", "0") not in ("", "0"):
             # K3R (project + render fused): every used plane of the 3 stacks in, the ARGB plane out
@@ -522,7 +557,8 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
         else:
             # K3 (all active channels in one launch): used planes in, one projected plane out each
             alg_bytes = C * (used_z * S * S * 2 + S * S * 2)
-            kms = {"K3_project": round(k3, 5), "K2_render": round(avg.get(2, float("nan")), 5)}
+            kms = {"K3_project": round(k3, 5), "K3_project_per_launch_events": round(k3_events, 5),
+                   "K2_render": round(avg.get(2, float("nan")), 5)}
             kname = f"k_project<u16,BE,{name}> (K3)"
         r = {"requests_per_s": one["median_per_s"], "ms_per_request": round(1e3 / one["median_per_s"], 4),
              "requests_per_s_two_streams": two["median_per_s"],
@@ -533,7 +569,9 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
              "roofline": {"bound": "hbm", "kernel": kname,
                           "achieved": round(alg_bytes / (k3 * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                           "unit": "GB/s", "frac": round(alg_bytes / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                          "algorithmic_bytes_per_launch": alg_bytes}}
+                          "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k3, 5),
+                          "timing": "gated burst: 200 K3 launches queued behind a spin kernel, two events "
+                                    "around the burst" if burst is not None else "per-launch HIP events"}}
         if with_cpu:
             try:
                 oracle_lib = _oracle()
@@ -649,7 +687,45 @@ def png_section(torch, ctx, data):
         if i >= 3:
             lat.append(time.perf_counter() - t0)
     res = {"p50_ms": round(1e3 * float(np.median(lat)), 4), "png_bytes": len(png),
-           "raw_bytes": (3 * TILE + 1) * TILE, "ratio": round(len(png) / ((3 * TILE + 1) * TILE), 4)}
+           "raw_bytes": (3 * TILE + 1) * TILE, "ratio": round(len(png) / ((3 * TILE + 1) * TILE), 4),
+           "single_tile_per_s": round(1.0 / float(np.median(lat)), 1)}
+    # Batched (omr_encode_png_batch_device): the rendered C2 batch (all distinct tiles of `data`)
+    # encoded at 64 and 256 tiles per call, one launch per stage, files packed in HBM.
+    B = data.shape[0]
+    argb = torch.empty((B, TILE, TILE), dtype=torch.int32, device=data.device)
+    pb = TILE * TILE * 2
+    ctx.render_batch_strided_device(make_qdef("rgb"), c2_channels(CHANNELS), data, CHANNELS * pb, pb, B,
+                                    _lib.PIXELS_UINT16, TILE, TILE, argb, big_endian=True)
+    cap = _lib.lib.omr_png_batch_max_bytes(TILE, TILE, 3, B)
+    d_out = torch.empty(cap, dtype=torch.uint8, device=data.device)
+    offs = torch.empty(B, dtype=torch.int64, device=data.device)
+    lens = torch.empty(B, dtype=torch.int32, device=data.device)
+    stat = torch.empty(B, dtype=torch.int32, device=data.device)
+    ctx.synchronize()
+    batched = {}
+    for n in (64, 256):
+        if n > B:
+            continue
+        def step():
+            ctx.encode_png_batch_device(argb, n, TILE, TILE, d_out, offs, lens, stat)
+        t_end = time.perf_counter() + SECTION_PREWARM_S
+        while time.perf_counter() < t_end:
+            step()
+            ctx.synchronize()
+        reps = max(4, 1024 // n)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step()
+        ctx.synchronize()
+        el = time.perf_counter() - t0
+        ln = lens[:n].cpu().numpy()
+        assert int((stat[:n] != 0).sum().item()) == 0, "PNG batch status"
+        batched[f"tiles_per_call_{n}"] = {"tiles_per_s": round(n * reps / el, 1),
+                                          "ms_per_call": round(1e3 * el / reps, 4),
+                                          "mean_png_bytes": int(ln.mean())}
+    res["batched"] = batched
+    if "tiles_per_call_256" in batched:
+        res["batched_vs_single"] = round(batched["tiles_per_call_256"]["tiles_per_s"] / res["single_tile_per_s"], 2)
     try:
         from PIL import Image
         a = out.cpu().numpy().view(np.uint32)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define OMR_ABI_VERSION 1
+#define OMR_ABI_VERSION 2   /* 2 (round 4): omr_tile_job gained the projection fields */
 
 typedef int32_t omr_status;
 enum {
@@ -227,7 +227,15 @@ omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* p
  * ImageRegionCtx.cacheKey (ImageRegionCtx.java:165-177).  A batcher owns one GPU context and a
  * dispatcher thread: submitted jobs are grouped by image + rendering settings + tile size + flip +
  * format, each group is rendered by one omr_render_pixel_buffer_tiles call and encoded by one
- * batched JPEG launch, and identical tiles in flight together are rendered once.
+ * batched JPEG / PNG launch, and identical tiles in flight together are rendered once.
+ * Projection requests (p=intmax|intmean|intsum, :506-558) are jobs with has_projection set: the
+ * active channels' Z-stacks at t go to HBM by DMA, K3 + K2 (or K3R) project and render the full
+ * plane, and the group's planes are encoded in one batch; jobs with the same image, settings,
+ * projection and t are rendered once.  Shape masks (render_shape_mask,
+ * ShapeMaskRequestHandler.java:165-207, one per worker at ShapeMaskVerticle.java:121-149) are
+ * jobs of their own (omr_batcher_submit_mask): every mask of a dispatch round is encoded by one
+ * omr_render_shape_mask_png_batch call.  A failing job (OMR_QUANTIZATION, the quirk-3 OMR_INTERNAL
+ * of the projection glue, a mask's 404) fails alone.
  * submit/wait are thread-safe; the pixel buffer must outlive its jobs.
  */
 enum { OMR_FORMAT_JPEG = 0, OMR_FORMAT_PNG = 1, OMR_FORMAT_ARGB = 2 /* packed int[] */,
@@ -241,16 +249,26 @@ typedef struct omr_tile_job {
     int32_t flip_h, flip_v;
     int32_t format;                                /* OMR_FORMAT_*; others -> OMR_NOT_FOUND (404) */
     float quality;                                 /* JPEG */
+    /* p=intmax|intmean|intsum[|start:end] (ImageRegionCtx.projection, ImageRegionRequestHandler.java
+     * :506-558): with has_projection != 0 every active channel is projected (OMR_PROJECTION_*) over
+     * z in [projection_start, projection_end] at t -- a negative bound takes the reference's default,
+     * 0 / sizeZ - 1 (:510-515) -- and the full projected plane is rendered: z, x, y, width and height
+     * are ignored, as the glue replaces the plane definition (:550-552).  Zero-initialised: none. */
+    int32_t has_projection, projection, projection_start, projection_end;
 } omr_tile_job;
+struct omr_mask_job;   /* shape-mask job, declared with omr_render_shape_mask_png_batch below */
 typedef struct omr_batcher omr_batcher;
 omr_status omr_batcher_create(int32_t device_ordinal, int32_t max_batch, int32_t max_wait_us,
                               omr_batcher** out);
 void       omr_batcher_destroy(omr_batcher* b);
 omr_status omr_batcher_submit(omr_batcher* b, const omr_tile_job* job, uint64_t* ticket);
+/* A render_shape_mask job (the mask bytes are copied at submit); its result is the PNG file. */
+omr_status omr_batcher_submit_mask(omr_batcher* b, const struct omr_mask_job* job, uint64_t* ticket);
 /* Blocks until the job is done; copies its encoded bytes.  OMR_BUFFER_TOO_SMALL sets *len and
  * keeps the result for a retry with a larger buffer. */
 omr_status omr_batcher_wait(omr_batcher* b, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
-/* jobs submitted, dispatch rounds, tiles rendered, duplicate tiles served from a sibling job */
+/* jobs submitted, dispatch rounds, tiles rendered (distinct renders: tiles, projected planes and
+ * masks), duplicate jobs served from a sibling job's result */
 omr_status omr_batcher_stats(omr_batcher* b, uint64_t stats_out[4]);
 /* OMR_SEM_* flags for jobs submitted after this call (each job keeps the flags it was submitted
  * under; jobs with different flags never share a render). */
@@ -272,6 +290,7 @@ omr_status omr_pool_create(const int32_t* devices, int32_t n_devices, int32_t ma
 void       omr_pool_destroy(omr_pool* p);
 int32_t    omr_pool_size(const omr_pool* p);
 omr_status omr_pool_submit(omr_pool* p, const omr_tile_job* job, uint64_t* ticket);
+omr_status omr_pool_submit_mask(omr_pool* p, const struct omr_mask_job* job, uint64_t* ticket);
 /* omr_batcher_wait of the batcher holding the ticket. */
 omr_status omr_pool_wait(omr_pool* p, uint64_t ticket, uint8_t* out, size_t cap, size_t* len);
 /* Index into devices[] of the batcher a ticket went to (-1: not a ticket of this pool). */
@@ -362,6 +381,17 @@ omr_status omr_project_stack_device(omr_ctx* ctx, const void* d_stack, int32_t p
                                     int32_t big_endian_in, int32_t size_x, int32_t size_y,
                                     int32_t size_z, int32_t algorithm, int32_t start, int32_t end,
                                     int32_t stepping, void* d_plane_out, int32_t big_endian_out);
+/*
+ * n_stacks same-geometry stacks (e.g. every active channel of one p= request, the glue's
+ * projectStack loop at ImageRegionRequestHandler.java:516-533) projected in one launch.
+ * d_stacks / d_planes_out: HOST arrays of n_stacks device pointers; n_stacks <= 32.
+ * Asynchronous on the context stream.
+ */
+omr_status omr_project_stacks_device(omr_ctx* ctx, const void* const* d_stacks, int32_t n_stacks,
+                                     int32_t pixel_type, int32_t big_endian_in, int32_t size_x,
+                                     int32_t size_y, int32_t size_z, int32_t algorithm, int32_t start,
+                                     int32_t end, int32_t stepping, void* const* d_planes_out,
+                                     int32_t big_endian_out);
 /*
  * Projection glue + render (ImageRegionRequestHandler.java:506-559): project every active
  * channel's stack (d_stacks[c], NULL for inactive) and render the full projected plane.

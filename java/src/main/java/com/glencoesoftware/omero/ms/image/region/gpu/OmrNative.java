@@ -22,6 +22,7 @@ public final class OmrNative implements AutoCloseable {
             FAMILY_EXPONENTIAL = 3;
     public static final int MODEL_GREYSCALE = 0, MODEL_RGB = 1;
     public static final int FORMAT_JPEG = 0, FORMAT_PNG = 1, FORMAT_ARGB = 2, FORMAT_TIFF = 3;
+    public static final int PROJECTION_MAX = 0, PROJECTION_MEAN = 1, PROJECTION_SUM = 2;
     /** OMR_SEM_* switches of the un-vendored upstream semantics. */
     public static final int SEM_WINDOW_INT_BOUNDS = 1, SEM_ALPHA_SEPARATE = 2, SEM_GREYSCALE_LUT = 4,
             SEM_JPEG_CHROMA_DIV2 = 8, SEM_PROJECTION_ALL_ACTIVE = 16, SEM_LOG_UNGUARDED = 32,
@@ -103,6 +104,17 @@ public final class OmrNative implements AutoCloseable {
     public static native long batcherSubmit(long batcher, long pixelBuffer, int model, double[] settings,
                                             byte[][] luts, int z, int t, int x, int y, int width, int height,
                                             boolean flipH, boolean flipV, int format, float quality);
+    /**
+     * A p=intmax|intmean|intsum request (ImageRegionRequestHandler.java:506-558): every active channel
+     * projected (PROJECTION_*) over z in [start, end] at t (negative: 0 / sizeZ - 1), the full plane
+     * rendered and encoded.
+     */
+    public static native long batcherSubmitProjected(long batcher, long pixelBuffer, int model, double[] settings,
+                                                     byte[][] luts, int t, int algorithm, int start, int end,
+                                                     boolean flipH, boolean flipV, int format, float quality);
+    /** render_shape_mask (ShapeMaskRequestHandler.java:165-207); wait returns the PNG (404 cases throw). */
+    public static native long batcherSubmitMask(long batcher, byte[] bits, int width, int height, byte[] rgba,
+                                                boolean flipH, boolean flipV);
     /** Blocks until the job is done; the encoded tile (JPEG / PNG / TIFF) or the packed ARGB bytes. */
     public static native byte[] batcherWait(long batcher, long ticket);
     /** OMR_SEM_* flags for jobs submitted after this call. */
@@ -116,5 +128,10 @@ public final class OmrNative implements AutoCloseable {
     public static native long poolSubmit(long pool, long pixelBuffer, int model, double[] settings,
                                          byte[][] luts, int z, int t, int x, int y, int width, int height,
                                          boolean flipH, boolean flipV, int format, float quality);
+    public static native long poolSubmitProjected(long pool, long pixelBuffer, int model, double[] settings,
+                                                  byte[][] luts, int t, int algorithm, int start, int end,
+                                                  boolean flipH, boolean flipV, int format, float quality);
+    public static native long poolSubmitMask(long pool, byte[] bits, int width, int height, byte[] rgba,
+                                             boolean flipH, boolean flipV);
     public static native byte[] poolWait(long pool, long ticket);
 }

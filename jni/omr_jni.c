@@ -15,6 +15,8 @@
  *   encodePng/Tiff      ImageIO.write / TIFFImageWriter         ImageRegionRequestHandler.java:583-600
  *   renderShapeMaskPng  renderShapeMask(Color, byte[], w, h)    ShapeMaskRequestHandler.java:165-207
  *   batcher* / pool*    one Renderer per request on each worker ImageRegionMicroserviceVerticle.java:149-165
+ *   *SubmitProjected    the projection glue of render           ImageRegionRequestHandler.java:506-558
+ *   *SubmitMask         renderShapeMask per worker              ShapeMaskVerticle.java:121-149
  *
  * Rules kept here:
  *  - every array length is checked (64-bit arithmetic) before any pixel byte moves; a short or
@@ -467,8 +469,22 @@ static jlong submit(JNIEnv* env, void* q, submit_fn fn, jlong jpb, jint model, j
     if (!s) { throw_omr(env, OMR_OOM, "settings"); return 0; }
     if (!load_settings(env, jch, jluts, s)) { free(s); return 0; }
     const omr_quantum_def qd = {0, 255, 255, model};
-    omr_tile_job job = {(const omr_pixel_buffer*)(intptr_t)jpb, &qd, s->cb, s->n, z, t, x, y, w, h, flipH, flipV,
-                        format, quality};
+    omr_tile_job job;
+    memset(&job, 0, sizeof(job));                        /* no projection */
+    job.pb = (const omr_pixel_buffer*)(intptr_t)jpb;
+    job.qdef = &qd;
+    job.channels = s->cb;
+    job.size_c = s->n;
+    job.z = z;
+    job.t = t;
+    job.x = x;
+    job.y = y;
+    job.width = w;
+    job.height = h;
+    job.flip_h = flipH;
+    job.flip_v = flipV;
+    job.format = format;
+    job.quality = quality;
     uint64_t ticket = 0;
     const omr_status st = fn(q, &job, &ticket);          /* copies the settings and LUTs */
     free(s);
@@ -497,6 +513,84 @@ static jbyteArray wait_result(JNIEnv* env, void* q, wait_fn fn, jlong ticket) {
     return res;
 }
 
+/* p=intmax|intmean|intsum at t (ImageRegionRequestHandler.java:506-558): the full plane; start / end
+ * < 0 take the reference's defaults (0 / sizeZ - 1). */
+static jlong submit_projected(JNIEnv* env, void* q, submit_fn fn, jlong jpb, jint model, jdoubleArray jch,
+                              jobjectArray jluts, jint t, jint alg, jint start, jint end, jboolean flipH,
+                              jboolean flipV, jint format, jfloat quality) {
+    if (!q || !jpb) {
+        throw_omr(env, OMR_INVALID_ARGUMENT, "null batcher or pixel buffer");
+        return 0;
+    }
+    settings* s = (settings*)malloc(sizeof(settings));
+    if (!s) { throw_omr(env, OMR_OOM, "settings"); return 0; }
+    if (!load_settings(env, jch, jluts, s)) { free(s); return 0; }
+    const omr_quantum_def qd = {0, 255, 255, model};
+    omr_tile_job job;
+    memset(&job, 0, sizeof(job));
+    job.pb = (const omr_pixel_buffer*)(intptr_t)jpb;
+    job.qdef = &qd;
+    job.channels = s->cb;
+    job.size_c = s->n;
+    job.t = t;
+    job.flip_h = flipH;
+    job.flip_v = flipV;
+    job.format = format;
+    job.quality = quality;
+    job.has_projection = 1;
+    job.projection = alg;
+    job.projection_start = start;
+    job.projection_end = end;
+    uint64_t ticket = 0;
+    const omr_status st = fn(q, &job, &ticket);
+    free(s);
+    if (st) throw_omr(env, st, st == OMR_NOT_FOUND ? "unknown format" : "submit failed");
+    return (jlong)ticket;
+}
+
+typedef omr_status (*submit_mask_fn)(void*, const omr_mask_job*, uint64_t*);
+
+/* render_shape_mask (ShapeMaskRequestHandler.java:165-207) as a queued job: the mask bytes are
+ * copied by the library at submit; every 404 case of the reference fails the job at wait. */
+static jlong submit_mask(JNIEnv* env, void* q, submit_mask_fn fn, jbyteArray jbits, jint w, jint ht,
+                         jbyteArray jrgba, jboolean flipH, jboolean flipV) {
+    if (!q) {
+        throw_omr(env, OMR_INVALID_ARGUMENT, "null batcher");
+        return 0;
+    }
+    if (!check_len(env, jrgba, 4, "fill colour must be 4 bytes (RGBA)")) return 0;
+    omr_mask_job job;
+    memset(&job, 0, sizeof(job));
+    (*env)->GetByteArrayRegion(env, jrgba, 0, 4, (jbyte*)job.rgba);
+    if ((*env)->ExceptionCheck(env)) return 0;
+    const jsize nbits = jbits ? (*env)->GetArrayLength(env, jbits) : 0;
+    uint8_t* bits = NULL;
+    if (jbits) {                                         /* null stays null: the job's 404 */
+        bits = (uint8_t*)malloc(nbits ? (size_t)nbits : 1);
+        if (!bits) { throw_omr(env, OMR_OOM, "mask copy"); return 0; }
+        if (nbits) (*env)->GetByteArrayRegion(env, jbits, 0, nbits, (jbyte*)bits);
+        if ((*env)->ExceptionCheck(env)) { free(bits); return 0; }
+    }
+    job.bits = bits;
+    job.n_bytes = (size_t)nbits;
+    job.width = w;
+    job.height = ht;
+    job.flip_h = flipH;
+    job.flip_v = flipV;
+    uint64_t ticket = 0;
+    const omr_status st = fn(q, &job, &ticket);          /* copies the mask */
+    free(bits);
+    if (st) throw_omr(env, st, "submit failed");
+    return (jlong)ticket;
+}
+
+static omr_status batcher_submit_mask(void* q, const omr_mask_job* j, uint64_t* t) {
+    return omr_batcher_submit_mask((omr_batcher*)q, j, t);
+}
+static omr_status pool_submit_mask(void* q, const omr_mask_job* j, uint64_t* t) {
+    return omr_pool_submit_mask((omr_pool*)q, j, t);
+}
+
 static omr_status batcher_submit(void* q, const omr_tile_job* j, uint64_t* t) {
     return omr_batcher_submit((omr_batcher*)q, j, t);
 }
@@ -515,6 +609,19 @@ JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNa
         jint t, jint x, jint y, jint w, jint h, jboolean flipH, jboolean flipV, jint format, jfloat quality) {
     return submit(env, (void*)(intptr_t)jb, batcher_submit, jpb, model, jch, jluts, z, t, x, y, w, h, flipH, flipV,
                   format, quality);
+}
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_batcherSubmitProjected(
+        JNIEnv* env, jclass cls, jlong jb, jlong jpb, jint model, jdoubleArray jch, jobjectArray jluts, jint t,
+        jint alg, jint start, jint end, jboolean flipH, jboolean flipV, jint format, jfloat quality) {
+    return submit_projected(env, (void*)(intptr_t)jb, batcher_submit, jpb, model, jch, jluts, t, alg, start, end,
+                            flipH, flipV, format, quality);
+}
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_batcherSubmitMask(
+        JNIEnv* env, jclass cls, jlong jb, jbyteArray jbits, jint w, jint ht, jbyteArray jrgba, jboolean flipH,
+        jboolean flipV) {
+    return submit_mask(env, (void*)(intptr_t)jb, batcher_submit_mask, jbits, w, ht, jrgba, flipH, flipV);
 }
 
 JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_batcherWait(
@@ -557,6 +664,19 @@ JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNa
         jint t, jint x, jint y, jint w, jint h, jboolean flipH, jboolean flipV, jint format, jfloat quality) {
     return submit(env, (void*)(intptr_t)jp, pool_submit, jpb, model, jch, jluts, z, t, x, y, w, h, flipH, flipV,
                   format, quality);
+}
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_poolSubmitProjected(
+        JNIEnv* env, jclass cls, jlong jp, jlong jpb, jint model, jdoubleArray jch, jobjectArray jluts, jint t,
+        jint alg, jint start, jint end, jboolean flipH, jboolean flipV, jint format, jfloat quality) {
+    return submit_projected(env, (void*)(intptr_t)jp, pool_submit, jpb, model, jch, jluts, t, alg, start, end,
+                            flipH, flipV, format, quality);
+}
+
+JNIEXPORT jlong JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_poolSubmitMask(
+        JNIEnv* env, jclass cls, jlong jp, jbyteArray jbits, jint w, jint ht, jbyteArray jrgba, jboolean flipH,
+        jboolean flipV) {
+    return submit_mask(env, (void*)(intptr_t)jp, pool_submit_mask, jbits, w, ht, jrgba, flipH, flipV);
 }
 
 JNIEXPORT jbyteArray JNICALL Java_com_glencoesoftware_omero_ms_image_region_gpu_OmrNative_poolWait(

@@ -23,15 +23,20 @@
 
 namespace omr {
 
+enum JobKind : int { kJobTile = 0, kJobProjection = 1, kJobMask = 2 };
+
 struct Job {
     uint64_t ticket = 0;
+    int kind = kJobTile;
     const omr_pixel_buffer* pb = nullptr;
     omr_quantum_def qdef{};
     std::vector<omr_channel_binding> ch;
     std::vector<std::vector<uint8_t>> luts;     // owned copies of the .lut tables
     omr_tile_job spec{};
+    omr_mask_job mask{};                         // kJobMask: bits point into mask_bits
+    std::vector<uint8_t> mask_bits;
     uint32_t sem = 0;                            // OMR_SEM_* of the batcher when the job was submitted
-    std::string group_key;                       // image + settings + semantics + size + flip + format
+    std::string group_key;                       // kind + image + settings + semantics + size + flip + format
     std::chrono::steady_clock::time_point t_submit;
 };
 
@@ -61,8 +66,10 @@ struct omr_batcher {
     // device buffers of the dispatcher (grown on demand)
     uint32_t* d_argb = nullptr;
     size_t argb_cap = 0;
-    uint8_t* d_jpeg = nullptr;
+    uint8_t* d_jpeg = nullptr;                   // encoded files of a group (JPEG / PNG batch output)
     size_t jpeg_cap = 0;
+    uint8_t* d_stack = nullptr;                  // projection jobs: the active channels' Z-stacks
+    size_t stack_cap = 0;
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
     int32_t* d_stat = nullptr;
@@ -76,6 +83,11 @@ static void append(std::string& k, const void* p, size_t n) { k.append(static_ca
 
 static std::string settings_key(const Job& j) {
     std::string k;
+    if (j.kind == kJobMask) {                    // every mask of a round shares one batch call
+        append(k, &j.kind, sizeof(j.kind));
+        append(k, &j.sem, sizeof(j.sem));
+        return k;
+    }
     append(k, &j.pb, sizeof(j.pb));
     append(k, &j.qdef, sizeof(j.qdef));
     for (size_t c = 0; c < j.ch.size(); ++c) {
@@ -96,7 +108,14 @@ static std::string settings_key(const Job& j) {
     }
     const omr_tile_job& s = j.spec;
     const int32_t geo[5] = {s.width, s.height, s.flip_h, s.flip_v, s.format};
-    append(k, geo, sizeof(geo));
+    append(k, &j.kind, sizeof(j.kind));
+    if (j.kind == kJobProjection) {             // the full plane: only the projection matters
+        const int32_t pr[5] = {s.flip_h, s.flip_v, s.format, s.projection, s.projection_start};
+        append(k, pr, sizeof(pr));
+        append(k, &s.projection_end, sizeof(s.projection_end));
+    } else {
+        append(k, geo, sizeof(geo));
+    }
     append(k, &j.sem, sizeof(j.sem));
     append(k, &s.quality, sizeof(s.quality));
     return k;
@@ -138,6 +157,64 @@ static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
     }
     return OMR_OK;
 }
+// Encode n device ARGB images of W x H (B->d_argb, tile i at i*W*H) in `format` into out[i] (skipping
+// entries that already carry an error): JPEG and PNG in one batched launch each (sides up to
+// 4096; larger planes, e.g. a projected full plane, one at a time), TIFF by the host writer, ARGB
+// as the packed int[] itself.
+static omr_status encode_group(omr_batcher* B, int n, int W, int H, int format, float quality,
+                               std::vector<Result>& out) {
+    omr_ctx* c = B->ctx;
+    const size_t px = (size_t)W * H;
+    const bool batched = W <= 4096 && H <= 4096;
+    if ((format == OMR_FORMAT_JPEG || format == OMR_FORMAT_PNG) && batched) {
+        const size_t cap = format == OMR_FORMAT_JPEG ? (size_t)n * (px * 4 + 65536)
+                                                     : omr_png_batch_max_bytes(W, H, 3, n);
+        omr_status st = grow_dev(B, 0, cap, n);
+        if (st) return st;
+        st = format == OMR_FORMAT_JPEG
+                 ? omr_encode_jpeg_batch_device(c, B->d_argb, 0, n, W, H, quality, B->d_jpeg, cap, B->d_offs,
+                                                B->d_lens, B->d_stat)
+                 : omr_encode_png_batch_device(c, B->d_argb, 0, n, W, H, B->d_jpeg, cap, B->d_offs, B->d_lens,
+                                               B->d_stat);
+        if (st) return st;
+        std::vector<uint64_t> offs(n);
+        std::vector<uint32_t> lens(n);
+        OMR_HIP(c, hipMemcpyAsync(offs.data(), B->d_offs, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipMemcpyAsync(lens.data(), B->d_lens, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        uint64_t used = 0;
+        for (int i = 0; i < n; ++i) {
+            if (!lens[i]) return fail(c, OMR_INTERNAL, "encode batch buffer too small");
+            used = std::max<uint64_t>(used, offs[i] + lens[i]);
+        }
+        std::vector<uint8_t> all(used);
+        OMR_HIP(c, hipMemcpy(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i)
+            if (!out[i].st) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
+    } else if (format == OMR_FORMAT_JPEG || format == OMR_FORMAT_PNG || format == OMR_FORMAT_TIFF) {
+        const size_t cap = format == OMR_FORMAT_JPEG ? omr_jpeg_max_bytes(W, H)
+                         : format == OMR_FORMAT_PNG  ? omr_png_max_bytes(W, H, 3)
+                                                     : omr_tiff_max_bytes(W, H);   // TIFFImageWriter (:583-596)
+        std::vector<uint8_t> buf(cap);
+        for (int i = 0; i < n; ++i) {
+            if (out[i].st) continue;
+            size_t len = 0;
+            const uint32_t* a = B->d_argb + px * i;
+            const omr_status st = format == OMR_FORMAT_JPEG ? omr_encode_jpeg_device(c, a, W, H, quality, buf.data(), cap, &len)
+                                : format == OMR_FORMAT_PNG  ? omr_encode_png_device(c, a, W, H, buf.data(), cap, &len)
+                                                            : omr_encode_tiff_device(c, a, W, H, buf.data(), cap, &len);
+            if (st) return st;
+            out[i].bytes.assign(buf.begin(), buf.begin() + len);
+        }
+    } else {                                               // OMR_FORMAT_ARGB: the packed int[] itself
+        std::vector<uint8_t> all(px * 4 * n);
+        OMR_HIP(c, hipMemcpy(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost));
+        for (int i = 0; i < n; ++i)
+            if (!out[i].st) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
+    }
+    return OMR_OK;
+}
+
 // Render + encode one group (same image, settings, size, flip, format).  jobs[u] are the
 // distinct tiles; out[u] receives each one's bytes, or OMR_QUANTIZATION for a tile with a pixel
 // outside the LUT domain — only that tile fails, as only that request's Renderer would throw
@@ -151,8 +228,7 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
     const size_t px = (size_t)W * H;
     std::vector<omr_tile_request> reqs(n);
     for (int i = 0; i < n; ++i) reqs[i] = {jobs[i]->spec.z, jobs[i]->spec.t, jobs[i]->spec.x, jobs[i]->spec.y};
-    const size_t jcap = (size_t)n * (px * 4 + 65536);
-    omr_status st = grow_dev(B, px * 4 * n, j0.spec.format == OMR_FORMAT_JPEG ? jcap : 0, n);
+    omr_status st = grow_dev(B, px * 4 * n, 0, n);
     if (st) return st;
     st = render_pixel_buffer_tiles(c, j0.pb, &j0.qdef, j0.ch.data(), (int32_t)j0.ch.size(), reqs.data(), n, W, H,
                                    j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1, B->d_rstat);
@@ -166,47 +242,84 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
             out[i].st = rstat[i];
             out[i].err = "pixel value outside the quantization LUT domain";
         }
-    if (j0.spec.format == OMR_FORMAT_JPEG) {
-        st = omr_encode_jpeg_batch_device(c, B->d_argb, 0, n, W, H, j0.spec.quality, B->d_jpeg, jcap, B->d_offs,
-                                          B->d_lens, B->d_stat);
-        if (st) return st;
-        std::vector<uint64_t> offs(n);
-        std::vector<uint32_t> lens(n);
-        OMR_HIP(c, hipMemcpyAsync(offs.data(), B->d_offs, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        OMR_HIP(c, hipMemcpyAsync(lens.data(), B->d_lens, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-        OMR_HIP(c, hipStreamSynchronize(c->stream));
-        uint64_t used = 0;
-        for (int i = 0; i < n; ++i) {
-            if (!lens[i]) return fail(c, OMR_INTERNAL, "JPEG batch buffer too small");
-            used = std::max<uint64_t>(used, offs[i] + lens[i]);
+    return encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, out);
+}
+
+// Projection jobs of one group (same image, settings, projection, flips, format): for each
+// distinct t the active channels' Z-stacks go to HBM (DMA from the registered ROMIO mapping),
+// omr_render_projected_device projects and renders the full plane (the glue,
+// ImageRegionRequestHandler.java:506-559), and the group's planes are encoded in one batch.
+// A request whose render fails (OMR_QUANTIZATION, the quirk-3 OMR_INTERNAL, a bad z range) fails
+// alone.
+static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
+    omr_ctx* c = B->ctx;
+    const Job& j0 = *jobs[0];
+    c->sem = j0.sem;
+    int32_t dims[6];
+    pixel_buffer_dims(j0.pb, dims);
+    const int W = dims[0], H = dims[1], Z = dims[2], SC = dims[3], PT = dims[5];
+    const int n = (int)jobs.size();
+    const size_t px = (size_t)W * H;
+    if ((int)j0.ch.size() != SC) return fail(c, OMR_INVALID_ARGUMENT, "channel bindings do not match sizeC");
+    std::vector<int> act;
+    for (int ch = 0; ch < SC; ++ch)
+        if (j0.ch[ch].active) act.push_back(ch);
+    const size_t stack_bytes = align_up(px * (size_t)bytes_per_pixel(PT) * Z, 256);
+    omr_status st = grow_dev(B, px * 4 * n, 0, n);
+    if (st) return st;
+    if (stack_bytes * std::max<size_t>(1, act.size()) > B->stack_cap) {
+        B->stack_cap = 0;
+        if ((st = regrow(c, B->d_stack, stack_bytes * std::max<size_t>(1, act.size())))) return st;
+        B->stack_cap = stack_bytes * std::max<size_t>(1, act.size());
+    }
+    out.assign(n, Result{});
+    const int start = j0.spec.projection_start >= 0 ? j0.spec.projection_start : 0;   // :510-515
+    const int end = j0.spec.projection_end >= 0 ? j0.spec.projection_end : Z - 1;
+    std::vector<const void*> stacks(SC, nullptr);
+    for (int i = 0; i < n; ++i) {
+        const int t = jobs[i]->spec.t;
+        for (size_t a = 0; a < act.size() && !st; ++a) {
+            stacks[act[a]] = B->d_stack + stack_bytes * a;
+            st = pixel_buffer_upload_stack(c, j0.pb, act[a], t, B->d_stack + stack_bytes * a);
         }
-        std::vector<uint8_t> all(used);
-        OMR_HIP(c, hipMemcpy(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost));
-        for (int i = 0; i < n; ++i)
-            if (!out[i].st) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
-    } else if (j0.spec.format == OMR_FORMAT_PNG) {
-        std::vector<uint8_t> buf(omr_png_max_bytes(W, H, 3));
-        for (int i = 0; i < n; ++i) {
-            if (out[i].st) continue;
-            size_t len = 0;
-            st = omr_encode_png_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
-            if (st) return st;
-            out[i].bytes.assign(buf.begin(), buf.begin() + len);
+        if (!st)
+            st = omr_render_projected_device(c, &j0.qdef, j0.ch.data(), SC, stacks.data(), PT, 1, W, H, Z,
+                                             j0.spec.projection, start, end, 1, j0.spec.flip_h, j0.spec.flip_v,
+                                             B->d_argb + px * i);
+        if (!st) st = omr_ctx_synchronize(c);              // this request's QuantizationException, if any
+        if (st) {
+            if (st == OMR_DEVICE || st == OMR_OOM) return st;
+            out[i].st = st;
+            out[i].err = c->last_error;
+            st = OMR_OK;
         }
-    } else if (j0.spec.format == OMR_FORMAT_TIFF) {        // TIFFImageWriter branch (:583-596)
-        std::vector<uint8_t> buf(omr_tiff_max_bytes(W, H));
-        for (int i = 0; i < n; ++i) {
-            if (out[i].st) continue;
-            size_t len = 0;
-            st = omr_encode_tiff_device(c, B->d_argb + px * i, W, H, buf.data(), buf.size(), &len);
-            if (st) return st;
-            out[i].bytes.assign(buf.begin(), buf.begin() + len);
-        }
-    } else {                                               // OMR_FORMAT_ARGB: the packed int[] itself
-        std::vector<uint8_t> all(px * 4 * n);
-        OMR_HIP(c, hipMemcpy(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost));
-        for (int i = 0; i < n; ++i)
-            if (!out[i].st) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
+    }
+    return encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, out);
+}
+
+// Every mask job of a dispatch round with the same semantics: one omr_render_shape_mask_png_batch.
+static omr_status run_mask_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
+    omr_ctx* c = B->ctx;
+    c->sem = jobs[0]->sem;
+    const int n = (int)jobs.size();
+    std::vector<omr_mask_job> mj(n);
+    size_t cap = 0;
+    for (int i = 0; i < n; ++i) {
+        mj[i] = jobs[i]->mask;
+        if (mj[i].width > 0 && mj[i].height > 0) cap += omr_png_batch_max_bytes(mj[i].width, mj[i].height, 1, 1);
+    }
+    std::vector<uint8_t> buf(std::max<size_t>(cap, 16));
+    std::vector<uint64_t> offs(n);
+    std::vector<uint32_t> lens(n);
+    std::vector<int32_t> stat(n);
+    const omr_status st = omr_render_shape_mask_png_batch(c, mj.data(), n, buf.data(), buf.size(), offs.data(),
+                                                          lens.data(), stat.data());
+    if (st) return st;
+    out.assign(n, Result{});
+    for (int i = 0; i < n; ++i) {
+        out[i].st = stat[i];
+        if (stat[i]) out[i].err = "Cannot render Mask";      // ShapeMaskVerticle.java:119-128 -> 404
+        else out[i].bytes.assign(buf.begin() + offs[i], buf.begin() + offs[i] + lens[i]);
     }
     return OMR_OK;
 }
@@ -233,10 +346,23 @@ static void dispatch_loop(omr_batcher* B) {
         for (auto& g : groups) {
             std::vector<Job*> uniq;
             std::vector<int> slot(g.second.size());
-            std::map<std::tuple<int, int, int, int>, int> seen;
+            std::map<std::string, int> seen;
+            const int kind = g.second[0]->kind;
             for (size_t i = 0; i < g.second.size(); ++i) {
-                const omr_tile_job& s = g.second[i]->spec;
-                auto key = std::make_tuple(s.z, s.t, s.x, s.y);
+                const Job& jb = *g.second[i];
+                const omr_tile_job& s = jb.spec;
+                std::string key;                       // the region / shape-mask cache key within the group
+                if (kind == kJobTile) {
+                    const int32_t k4[4] = {s.z, s.t, s.x, s.y};
+                    append(key, k4, sizeof(k4));
+                } else if (kind == kJobProjection) {
+                    append(key, &s.t, sizeof(s.t));
+                } else {
+                    const int32_t m4[4] = {jb.mask.width, jb.mask.height, jb.mask.flip_h, jb.mask.flip_v};
+                    append(key, m4, sizeof(m4));
+                    append(key, jb.mask.rgba, 4);
+                    append(key, jb.mask_bits.data(), jb.mask_bits.size());
+                }
                 auto it = seen.find(key);
                 if (it == seen.end()) {
                     seen[key] = (int)uniq.size();
@@ -252,7 +378,9 @@ static void dispatch_loop(omr_batcher* B) {
             for (size_t b0 = 0; b0 < uniq.size() && st == OMR_OK; b0 += (size_t)B->max_batch) {
                 std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + std::min(uniq.size(), b0 + B->max_batch));
                 std::vector<Result> po;
-                st = run_group(B, part, po);
+                st = kind == kJobTile ? run_group(B, part, po)
+                   : kind == kJobProjection ? run_projection_group(B, part, po)
+                                            : run_mask_group(B, part, po);
                 for (auto& r : po) out.push_back(std::move(r));
             }
             rendered += uniq.size();
@@ -308,32 +436,13 @@ void omr_batcher_destroy(omr_batcher* B) {
     if (B->th.joinable()) B->th.join();
     (void)hipSetDevice(B->device);
     for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat,
-                    (void*)B->d_rstat})
+                    (void*)B->d_rstat, (void*)B->d_stack})
         if (p) (void)hipFree(p);
     omr_ctx_destroy(B->ctx);
     delete B;
 }
 
-omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t* ticket) {
-    if (!B || !job || !ticket || !job->pb || !job->qdef || !job->channels || job->size_c <= 0)
-        return OMR_INVALID_ARGUMENT;
-    if (job->width <= 0 || job->height <= 0) return OMR_INVALID_ARGUMENT;
-    if (job->format != OMR_FORMAT_JPEG && job->format != OMR_FORMAT_PNG && job->format != OMR_FORMAT_ARGB &&
-        job->format != OMR_FORMAT_TIFF)
-        return OMR_NOT_FOUND;                              // unknown format -> null -> 404 (:602-603)
-    auto j = std::make_unique<Job>();
-    j->pb = job->pb;
-    j->qdef = *job->qdef;
-    j->ch.assign(job->channels, job->channels + job->size_c);
-    j->luts.resize(job->size_c);
-    for (int c = 0; c < job->size_c; ++c)
-        if (j->ch[c].lut) {
-            j->luts[c].assign(j->ch[c].lut, j->ch[c].lut + 768);
-            j->ch[c].lut = j->luts[c].data();
-        }
-    j->spec = *job;
-    j->spec.qdef = nullptr;
-    j->spec.channels = nullptr;
+static void enqueue(omr_batcher* B, std::unique_ptr<Job> j, uint64_t* ticket) {
     j->t_submit = std::chrono::steady_clock::now();
     {
         std::lock_guard<std::mutex> g(B->m);
@@ -346,6 +455,46 @@ omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t*
         B->outstanding++;
     }
     B->cv_in.notify_one();
+}
+
+omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t* ticket) {
+    if (!B || !job || !ticket || !job->pb || !job->qdef || !job->channels || job->size_c <= 0)
+        return OMR_INVALID_ARGUMENT;
+    const bool proj = job->has_projection != 0;
+    if (!proj && (job->width <= 0 || job->height <= 0)) return OMR_INVALID_ARGUMENT;
+    if (proj && (job->projection < OMR_PROJECTION_MAX || job->projection > OMR_PROJECTION_SUM))
+        return OMR_INVALID_ARGUMENT;
+    if (job->format != OMR_FORMAT_JPEG && job->format != OMR_FORMAT_PNG && job->format != OMR_FORMAT_ARGB &&
+        job->format != OMR_FORMAT_TIFF)
+        return OMR_NOT_FOUND;                              // unknown format -> null -> 404 (:602-603)
+    auto j = std::make_unique<Job>();
+    j->kind = proj ? kJobProjection : kJobTile;
+    j->pb = job->pb;
+    j->qdef = *job->qdef;
+    j->ch.assign(job->channels, job->channels + job->size_c);
+    j->luts.resize(job->size_c);
+    for (int c = 0; c < job->size_c; ++c)
+        if (j->ch[c].lut) {
+            j->luts[c].assign(j->ch[c].lut, j->ch[c].lut + 768);
+            j->ch[c].lut = j->luts[c].data();
+        }
+    j->spec = *job;
+    j->spec.qdef = nullptr;
+    j->spec.channels = nullptr;
+    enqueue(B, std::move(j), ticket);
+    return OMR_OK;
+}
+
+omr_status omr_batcher_submit_mask(omr_batcher* B, const omr_mask_job* job, uint64_t* ticket) {
+    if (!B || !job || !ticket) return OMR_INVALID_ARGUMENT;
+    auto j = std::make_unique<Job>();
+    j->kind = kJobMask;
+    j->mask = *job;
+    if (job->bits && job->n_bytes) j->mask_bits.assign(job->bits, job->bits + job->n_bytes);
+    // a null mask stays null (the reference's NPE -> 404 at wait); an empty one points at the copy
+    j->mask.bits = job->bits ? j->mask_bits.data() : nullptr;
+    if (job->bits && !job->n_bytes) { j->mask_bits.assign(1, 0); j->mask.bits = j->mask_bits.data(); }
+    enqueue(B, std::move(j), ticket);
     return OMR_OK;
 }
 
@@ -431,19 +580,35 @@ void omr_pool_destroy(omr_pool* P) {
 
 int32_t omr_pool_size(const omr_pool* P) { return P ? (int32_t)P->b.size() : 0; }
 
-omr_status omr_pool_submit(omr_pool* P, const omr_tile_job* job, uint64_t* ticket) {
-    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
+// The batcher with the fewest jobs queued or in flight, ties rotating from a moving start.
+static int pool_pick(omr_pool* P) {
     const int n = (int)P->b.size();
     const uint32_t start = P->rr.fetch_add(1, std::memory_order_relaxed) % (uint32_t)n;
     int best = (int)start;
     int64_t best_q = P->b[best]->outstanding.load(std::memory_order_relaxed);
-    for (int k = 1; k < n; ++k) {                      // least queued, first from a rotating start
+    for (int k = 1; k < n; ++k) {
         const int i = (int)((start + k) % (uint32_t)n);
         const int64_t q = P->b[i]->outstanding.load(std::memory_order_relaxed);
         if (q < best_q) { best = i; best_q = q; }
     }
+    return best;
+}
+
+omr_status omr_pool_submit(omr_pool* P, const omr_tile_job* job, uint64_t* ticket) {
+    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
+    const int best = pool_pick(P);
     uint64_t t = 0;
     const omr_status st = omr_batcher_submit(P->b[best], job, &t);
+    if (st) return st;
+    *ticket = (t << kPoolIndexBits) | (uint64_t)best;
+    return OMR_OK;
+}
+
+omr_status omr_pool_submit_mask(omr_pool* P, const omr_mask_job* job, uint64_t* ticket) {
+    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
+    const int best = pool_pick(P);
+    uint64_t t = 0;
+    const omr_status st = omr_batcher_submit_mask(P->b[best], job, &t);
     if (st) return st;
     *ticket = (t << kPoolIndexBits) | (uint64_t)best;
     return OMR_OK;

@@ -190,6 +190,11 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
                                      int32_t flip_h, int32_t flip_v, uint32_t* argb_out, int32_t out_on_device,
                                      int32_t* d_status);
 
+// dims = {sizeX, sizeY, sizeZ, sizeC, sizeT, pixelType} of an open pixel buffer (omr_pixbuf.cpp).
+void pixel_buffer_dims(const omr_pixel_buffer* pb, int32_t dims[6]);
+// The (c, t) Z-stack of a pixel buffer into device memory on ctx's stream (omr_pixbuf.cpp).
+omr_status pixel_buffer_upload_stack(omr_ctx* ctx, const omr_pixel_buffer* pb, int32_t c, int32_t t, void* d_dst);
+
 #define OMR_HIP(ctx, expr)                                          \
     do {                                                            \
         hipError_t _e = (expr);                                     \

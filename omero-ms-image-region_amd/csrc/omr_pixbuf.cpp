@@ -454,6 +454,33 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
     return st;
 }
 
+// Geometry of an open pixel buffer (the batcher's projection jobs render the full plane).
+void pixel_buffer_dims(const omr_pixel_buffer* pb, int32_t dims[6]) {
+    dims[0] = pb->sx; dims[1] = pb->sy; dims[2] = pb->sz; dims[3] = pb->sc; dims[4] = pb->st; dims[5] = pb->pt;
+}
+
+// The whole Z-stack of (c, t) -- sizeZ planes, contiguous in the ROMIO layout -- into device memory
+// at d_dst, on ctx's stream: a DMA from the registered mapping, else pread into pinned staging
+// (synchronous).  What ProjectionService reads plane by plane (ProjectionService.java:176-291).
+omr_status pixel_buffer_upload_stack(omr_ctx* ctx, const omr_pixel_buffer* pb, int32_t c, int32_t t, void* d_dst) {
+    if (!tile_in_bounds(pb, 0, c, t, 0, 0, 0, 0)) return fail(ctx, OMR_INVALID_ARGUMENT, "stack outside the image");
+    const int64_t off = plane_offset(pb, 0, c, t), bytes = pb->plane_bytes * pb->sz;
+    if (ctx->pixbuf_direct && ensure_registered(const_cast<omr_pixel_buffer*>(pb))) {
+        OMR_HIP(ctx, hipMemcpyAsync(d_dst, pb->map + off, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+        return OMR_OK;
+    }
+    PixPipe* P = nullptr;
+    omr_status st = get_pipe(ctx, P);
+    if (st) return st;
+    st = grow(ctx, P, (size_t)bytes, 0, false);
+    if (st) return st;
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));          // the staging slot is free
+    if (!read_full(pb->fd, P->pin_in[0], (size_t)bytes, off)) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
+    OMR_HIP(ctx, hipMemcpyAsync(d_dst, P->pin_in[0], (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return OMR_OK;
+}
+
 }  // namespace omr
 
 extern "C" omr_status omr_render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb,

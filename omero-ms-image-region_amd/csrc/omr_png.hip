@@ -115,25 +115,13 @@ __device__ __forceinline__ uint32_t mask_bit(const PngArgs& A, int x, int y) {
     return (A.bits[i >> 3] >> (7 - (i & 7))) & 1;
 }
 
-__device__ __forceinline__ uint32_t raw_byte(const PngArgs& A, int64_t i) {
-    const int64_t row = i / A.rowlen, col = i - row * A.rowlen;
-    if (col == 0) return 0;
-    const int64_t c = col - 1;
-    if (A.kind == kRgb) {
-        const int64_t px = c / 3;
-        const uint32_t p = A.argb[row * A.W + px];
-        return (p >> (16 - 8 * (c - px * 3))) & 0xFF;
-    }
-    if (A.kind == kIdx8) return mask_bit(A, (int)c, (int)row);
-    uint32_t b = 0;
-    for (int k = 0; k < 8; ++k) b = (b << 1) | mask_bit(A, (int)(c * 8 + k), (int)row);
-    return b;
-}
 
-// One lane per zlib-stream byte (header, stored-block headers, payload) + Adler partials.
-__global__ void __launch_bounds__(256) k_png_layout(PngArgs A) {
+// One lane per zlib-stream byte of the stored encoding: header, stored-block headers, and the
+// filtered stream flt as payload (any filter is valid PNG; storing the same filtered rows the
+// dynamic stream codes keeps one Adler-32 -- from D1's row partials -- for both encodings, and
+// makes the single-tile and the batched encoder's files identical).
+__global__ void __launch_bounds__(256) k_png_layout(PngArgs A, const uint8_t* __restrict__ flt) {
     if (A.meta[1] == 0) return;                     // the dynamic stream was chosen
-    unsigned long long s1 = 0, s2 = 0;
     uint8_t* z = A.chunk + 8;
     for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < A.zlen - 4; j += (int64_t)gridDim.x * 256) {
         uint32_t v;
@@ -152,22 +140,10 @@ __global__ void __launch_bounds__(256) k_png_layout(PngArgs A) {
                 default: v = ((~l16) >> 8) & 0xFF; break;
                 }
             } else {
-                const int64_t i = b * kStored + (o - 5);
-                v = raw_byte(A, i);
-                s1 += v;
-                s2 += (unsigned long long)(A.raw - i) * v;
+                v = flt[b * kStored + (o - 5)];
             }
         }
         z[j] = (uint8_t)v;
-    }
-    // block reduction of the Adler partials
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_down(s1, o, 64);
-        s2 += __shfl_down(s2, o, 64);
-    }
-    if ((threadIdx.x & 63) == 0 && (s1 | s2)) {
-        atomicAdd(&A.sums[0], s1);
-        atomicAdd(&A.sums[1], s2);
     }
 }
 
@@ -449,9 +425,8 @@ __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
     png_filter_row(D.P, D.bpp, blockIdx.x, D.flt, D.row_sums + 2 * blockIdx.x, s_rows);
 }
 
-// Sum of the per-row Adler partials into A.sums (one workgroup; dynamic stream only).
+// Sum of the per-row Adler partials into A.sums (one workgroup; both encodings carry flt).
 __global__ void __launch_bounds__(256) k_png_adler_rows(DflArgs D) {
-    if (D.P.meta[1]) return;
     __shared__ unsigned long long s_ad[2][4];
     unsigned long long s1 = 0, s2 = 0;
     for (int y = threadIdx.x; y < D.P.H; y += 256) { s1 += D.row_sums[2 * y]; s2 += D.row_sums[2 * y + 1]; }
@@ -468,6 +443,16 @@ __global__ void __launch_bounds__(256) k_png_adler_rows(DflArgs D) {
 }
 
 constexpr int kParseLanes = 128;            // segments (lanes) per parse workgroup
+
+// Token slot k of segment s (image-local): segments in blocks of kParseLanes, token-major inside a
+// block, so the lanes of a wave store (D2) and load (D4/D5) one token index at consecutive
+// addresses instead of 128 bytes apart.  A stream's token buffer holds align(nseg, 128) * kSeg.
+__device__ __forceinline__ int64_t tok_at(int64_t s, int k) {
+    return ((s / kParseLanes) * kSeg + k) * kParseLanes + (s % kParseLanes);
+}
+__host__ __device__ constexpr int64_t tok_slots(int64_t nseg) {
+    return (nseg + kParseLanes - 1) / kParseLanes * kParseLanes * kSeg;
+}
 constexpr int kMaxBack = 31 * 1024;         // LDS look-back window (bytes)
 
 // One lane per kSeg-byte segment; the workgroup first stages its 4 KiB of filtered stream plus
@@ -496,7 +481,6 @@ __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw,
         const int64_t beg = s * kSeg, end = min(raw, beg + kSeg);
         const int64_t cand[4] = {1, bpp, 2 * bpp, rowlen};
         const int nc = bpp == 1 ? 2 : 3;
-        uint32_t* tok = tokens + beg;
         int nt = 0;
         int64_t p = beg;
         while (p < end) {
@@ -514,12 +498,12 @@ __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw,
                 if (best == lim) break;
             }
             if (best >= 3) {
-                tok[nt++] = 0x80000000u | (uint32_t)(best - 3) | ((uint32_t)(bd - 1) << 8);
+                tokens[tok_at(s, nt++)] = 0x80000000u | (uint32_t)(best - 3) | ((uint32_t)(bd - 1) << 8);
                 atomicAdd(&lh[c_dfl.len_sym[best]], 1u);
                 atomicAdd(&dh[dist_sym((uint32_t)bd)], 1u);
                 p += best;
             } else {
-                tok[nt++] = x0;
+                tokens[tok_at(s, nt++)] = x0;
                 atomicAdd(&lh[x0], 1u);
                 ++p;
             }
@@ -952,10 +936,9 @@ __global__ void __launch_bounds__(256) k_png_lz_bits(DflArgs D) {
     __syncthreads();
     const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (s >= D.nseg) return;
-    const uint32_t* tok = D.tokens + s * kSeg;
     const int nt = D.ntok[s];
     uint32_t b = 0;
-    for (int i = 0; i < nt; ++i) b += token_bits(tok[i], llen, dlen);
+    for (int i = 0; i < nt; ++i) b += token_bits(D.tokens[tok_at(s, i)], llen, dlen);
     D.seg_bits[s] = b;
 }
 
@@ -983,7 +966,6 @@ __global__ void __launch_bounds__(256) k_png_lz_write(DflArgs D) {
         D.tot[1] = (eob + n + 7) / 8;     // deflate bytes
     }
     if (s >= D.nseg) return;
-    const uint32_t* tok = D.tokens + s * kSeg;
     const int nt = D.ntok[s];
     uint32_t pos = hb + D.seg_bits[s];
     uint64_t acc = 0;
@@ -1003,7 +985,7 @@ __global__ void __launch_bounds__(256) k_png_lz_write(DflArgs D) {
         }
     };
     for (int i = 0; i < nt; ++i) {
-        const uint32_t t = tok[i];
+        const uint32_t t = D.tokens[tok_at(s, i)];
         if (!(t & 0x80000000u)) {
             put(lcode[t], llen[t]);
         } else {
@@ -1101,7 +1083,7 @@ static PngLayout png_layout(int kind, int W, int H) {
     L.meta = take(32);
     L.chunk = take((size_t)P.chunk_bytes);
     L.flt = take((size_t)P.raw);
-    L.tokens = take((size_t)P.raw * 4);
+    L.tokens = take((size_t)tok_slots(L.nseg) * 4);
     L.ntok = take((size_t)L.nseg * 2);
     L.lhist = take((286 + 30) * 4);                 // lhist then dhist, contiguous
     L.dhist = L.lhist + 286 * 4;
@@ -1212,7 +1194,7 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     // stored vs dynamic decided on the device; both paths are queued, the unchosen one exits
     hipLaunchKernelGGL(k_png_select, dim3(1), dim3(1), 0, ctx->stream, D);
     const unsigned gl = (unsigned)std::min<int64_t>((P.zlen + 255) / 256, (int64_t)ctx->cu_count * 8);
-    hipLaunchKernelGGL(k_png_layout, dim3(gl), dim3(256), 0, ctx->stream, A);
+    hipLaunchKernelGGL(k_png_layout, dim3(gl), dim3(256), 0, ctx->stream, A, D.flt);
     hipLaunchKernelGGL(k_png_zcopy, dim3(gl), dim3(256), 0, ctx->stream, D);
     hipLaunchKernelGGL(k_png_adler_rows, dim3(1), dim3(256), 0, ctx->stream, D);
     hipLaunchKernelGGL(k_png_adler, dim3(1), dim3(1), 0, ctx->stream, A);
@@ -1286,6 +1268,7 @@ struct PngImg {
     int32_t back, pad;                          // parse look-back (bytes, multiple of 16)
     int64_t rowlen, raw, nseg, nblk;            // row bytes + 1, filtered stream bytes, segments, stored blocks
     int64_t flt, seg0, words;                   // filtered stream offset (bytes), first segment, first word
+    int64_t tok0;                               // first token slot (tok_at layout)
     int64_t eblk0, cblk0;                       // first P8 / P9 workgroup
     uint8_t pre[72];                            // signature, IHDR (+ PLTE, tRNS)
 };
@@ -1373,7 +1356,7 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     const PngImg& I = B.img[i];
     const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
     uint32_t* h = B.hist + (size_t)i * 316;
-    png_lz_parse_block(B.flt + I.flt, I.raw, I.rowlen, I.bpp, I.nseg, blk, I.back, B.tokens + I.seg0 * kSeg,
+    png_lz_parse_block(B.flt + I.flt, I.raw, I.rowlen, I.bpp, I.nseg, blk, I.back, B.tokens + I.tok0,
                        B.ntok + I.seg0, h, h + 286, s_win);
 }
 
@@ -1422,9 +1405,9 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_bits(PngBatch B) {
     uint32_t b = 0;
     if (ls < I.nseg) {
         const int64_t s = I.seg0 + ls;
-        const uint32_t* tok = B.tokens + s * kSeg;
+        const uint32_t* tok = B.tokens + I.tok0;
         const int nt = B.ntok[s];
-        for (int k = 0; k < nt; ++k) b += token_bits(tok[k], llen, dlen);
+        for (int k = 0; k < nt; ++k) b += token_bits(tok[tok_at(ls, k)], llen, dlen);
     }
     uint32_t total;
     const uint32_t ex = pngb_block_excl_scan(b, s_wave, total);
@@ -1573,7 +1556,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_write(PngBatch B) {
     const int64_t ls = gl * kPngbGroup + threadIdx.x;
     if (ls < I.nseg) {
         const int64_t s = I.seg0 + ls;
-        const uint32_t* tok = B.tokens + s * kSeg;
+        const uint32_t* tok = B.tokens + I.tok0;
         const int nt = B.ntok[s];
         const uint32_t pos = (gbase & 31) + B.segb[s];     // bit position in sw
         uint64_t acc = 0;
@@ -1590,7 +1573,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_write(PngBatch B) {
             }
         };
         for (int k = 0; k < nt; ++k) {
-            const uint32_t t = tok[k];
+            const uint32_t t = tok[tok_at(ls, k)];
             if (!(t & 0x80000000u)) {
                 put(lcode[t], llen[t]);
             } else {
@@ -1783,7 +1766,7 @@ static omr_status ensure_crc_pow(Ctx* ctx) {
 struct PngBatchPlan {
     std::vector<PngImg> I;
     std::vector<int32_t> firsts;
-    int64_t rows = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, flt = 0, words = 0;
+    int64_t rows = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
     size_t rows_lds = 16, parse_lds = 16;
     bool uniform = true;
     size_t o_img, o_first, o_flt, o_tok, o_ntok, o_segb, o_gsum, o_goff, o_hist, o_tab, o_meta, o_rows, o_words;
@@ -1822,6 +1805,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         d.eblk0 = L.eblk;
         d.cblk0 = L.cblk;
         d.seg0 = L.segs;
+        d.tok0 = L.toks;
         d.flt = L.flt;
         d.words = L.words;
         L.firsts[i] = d.row0;
@@ -1835,6 +1819,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         L.eblk += ne;
         L.cblk += nc;
         L.segs += d.nseg;
+        L.toks += tok_slots(d.nseg);
         L.flt += (int64_t)align_up((size_t)P.raw, 16);
         L.words += (int64_t)align_up((size_t)(P.raw / 2 + 128), 4);     // <= 16 bits per byte + header
         L.rows_lds = std::max(L.rows_lds, align_up(2 * (size_t)(P.rowlen - 1), 16));
@@ -1846,7 +1831,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
     L.o_img = take(sizeof(PngImg) * n);
     L.o_first = take(sizeof(int32_t) * 5 * n);
     L.o_flt = take((size_t)L.flt);
-    L.o_tok = take((size_t)L.segs * kSeg * 4);
+    L.o_tok = take((size_t)L.toks * 4);
     L.o_ntok = take((size_t)L.segs * 2);
     L.o_segb = take((size_t)L.segs * 4);
     L.o_gsum = take((size_t)L.grp * 4);

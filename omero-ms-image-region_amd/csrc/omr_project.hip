@@ -734,6 +734,22 @@ omr_status omr_project_stack_device(omr_ctx* ctx, const void* d_stack, int32_t p
                               end, stepping, big_endian_out);
 }
 
+omr_status omr_project_stacks_device(omr_ctx* ctx, const void* const* d_stacks, int32_t n_stacks, int32_t pixel_type,
+                                     int32_t big_endian_in, int32_t size_x, int32_t size_y, int32_t size_z,
+                                     int32_t algorithm, int32_t start, int32_t end, int32_t stepping,
+                                     void* const* d_planes_out, int32_t big_endian_out) {
+    if (!ctx) return OMR_INVALID_ARGUMENT;
+    omr_status st = validate_projection(ctx, pixel_type, size_x, size_y, size_z, algorithm, start, end, stepping);
+    if (st) return st;
+    if (n_stacks < 0 || n_stacks > kMaxStacks) return fail(ctx, OMR_INVALID_ARGUMENT, "0..32 stacks per call");
+    if (n_stacks && (!d_stacks || !d_planes_out)) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack list");
+    for (int i = 0; i < n_stacks; ++i)
+        if (!d_stacks[i] || !d_planes_out[i]) return fail(ctx, OMR_INVALID_ARGUMENT, "null stack or output");
+    OMR_HIP(ctx, hipSetDevice(ctx->device));
+    return enqueue_projection(ctx, d_stacks, d_planes_out, n_stacks, pixel_type, big_endian_in, size_x, size_y,
+                              algorithm, start, end, stepping, big_endian_out);
+}
+
 omr_status omr_project_stack(omr_ctx* ctx, const void* stack, int32_t pixel_type, int32_t big_endian_in,
                              int32_t size_x, int32_t size_y, int32_t size_z, int32_t algorithm,
                              int32_t start, int32_t end, int32_t stepping, void* plane_out,

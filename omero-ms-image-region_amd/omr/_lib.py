@@ -79,7 +79,8 @@ class TileJob(ctypes.Structure):
                 ("size_c", ctypes.c_int32), ("z", ctypes.c_int32), ("t", ctypes.c_int32), ("x", ctypes.c_int32),
                 ("y", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("flip_h", ctypes.c_int32), ("flip_v", ctypes.c_int32), ("format", ctypes.c_int32),
-                ("quality", ctypes.c_float)]
+                ("quality", ctypes.c_float), ("has_projection", ctypes.c_int32), ("projection", ctypes.c_int32),
+                ("projection_start", ctypes.c_int32), ("projection_end", ctypes.c_int32)]
 
 
 FORMAT_JPEG, FORMAT_PNG, FORMAT_ARGB, FORMAT_TIFF = 0, 1, 2, 3
@@ -154,6 +155,7 @@ _SIGS = {
     "omr_batcher_create": (_i32, [_i32, _i32, _i32, ctypes.POINTER(_vp)]),
     "omr_batcher_destroy": (None, [_vp]),
     "omr_batcher_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "omr_batcher_submit_mask": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
     "omr_batcher_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_batcher_stats": (_i32, [_vp, _vp]),
     "omr_batcher_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
@@ -161,6 +163,7 @@ _SIGS = {
     "omr_pool_destroy": (None, [_vp]),
     "omr_pool_size": (_i32, [_vp]),
     "omr_pool_submit": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
+    "omr_pool_submit_mask": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_uint64)]),
     "omr_pool_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_pool_device_index": (_i32, [_vp, ctypes.c_uint64]),
     "omr_pool_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
@@ -204,6 +207,8 @@ _SIGS = {
     "omr_encode_png_device": (_i32, [_vp, _vp, _i32, _i32, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_render_shape_mask_png": (_i32, [_vp, _vp, _sz, _i32, _i32, _vp, _i32, _i32, _vp, _sz,
                                          ctypes.POINTER(_sz)]),
+    "omr_project_stacks_device": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp,
+                                         _i32]),
     "omr_encode_png_batch_device": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _vp, _sz, _vp, _vp, _vp]),
     "omr_png_batch_max_bytes": (_sz, [_i32, _i32, _i32, _i32]),
     "omr_render_shape_mask_png_batch": (_i32, [_vp, ctypes.POINTER(MaskJob), _i32, _vp, _sz, _vp, _vp, _vp]),

@@ -21,16 +21,22 @@ FORMATS = {"jpeg": _lib.FORMAT_JPEG, "png": _lib.FORMAT_PNG, "argb": _lib.FORMAT
            "tif": _lib.FORMAT_TIFF}
 
 
-def _job(pixbuf, qdef, channels, z, t, x, y, width, height, flip_h, flip_v, fmt, quality, bindings):
+PROJECTIONS = {"intmax": _lib.PROJECTION_MAX, "intmean": _lib.PROJECTION_MEAN, "intsum": _lib.PROJECTION_SUM}
+
+
+def _job(pixbuf, qdef, channels, z, t, x, y, width, height, flip_h, flip_v, fmt, quality, bindings,
+         projection=None, projection_start=-1, projection_end=-1):
     arr, keep = bindings if bindings is not None else make_bindings(channels)
+    alg = PROJECTIONS[projection] if isinstance(projection, str) else projection
     job = _lib.TileJob(pixbuf.h.value if hasattr(pixbuf.h, "value") else pixbuf.h,
                        ctypes.addressof(qdef), ctypes.addressof(arr), len(channels), z, t, x, y, width, height,
-                       int(flip_h), int(flip_v), FORMATS.get(fmt, 99), float(quality))
+                       int(flip_h), int(flip_v), FORMATS.get(fmt, 99), float(quality),
+                       int(alg is not None), int(alg or 0), int(projection_start), int(projection_end))
     return job, (arr, keep)
 
 
 class _Queue:
-    _submit = _wait = _set_semantics = _destroy = None
+    _submit = _submit_mask = _wait = _set_semantics = _destroy = None
 
     def close(self):
         if self.h:
@@ -50,11 +56,28 @@ class _Queue:
         self.close()
 
     def submit(self, pixbuf, qdef, channels, z, t, x, y, width, height, flip_h=False, flip_v=False,
-               fmt="jpeg", quality=0.85, bindings=None):
+               fmt="jpeg", quality=0.85, bindings=None, projection=None, projection_start=-1,
+               projection_end=-1):
+        """A render_image_region job.  projection ("intmax" / "intmean" / "intsum" or OMR_PROJECTION_*):
+        the full plane projected over [projection_start, projection_end] (negative: 0 / sizeZ-1)
+        at t; z, x, y, width, height are then ignored (ImageRegionRequestHandler.java:506-558)."""
         job, keep = _job(pixbuf, qdef, channels, z, t, x, y, width, height, flip_h, flip_v, fmt, quality,
-                         bindings)
+                         bindings, projection, projection_start, projection_end)
         ticket = ctypes.c_uint64()
         _lib.check(type(self)._submit(self.h, ctypes.byref(job), ctypes.byref(ticket)))
+        return ticket.value
+
+    def submit_mask(self, bits, width, height, rgba, flip_h=False, flip_v=False):
+        """A render_shape_mask job (ShapeMaskRequestHandler.java:165-207); wait() returns the PNG."""
+        b = None if bits is None else np.frombuffer(bytes(bits), dtype=np.uint8).copy()
+        job = _lib.MaskJob()
+        job.bits = b.ctypes.data if b is not None and b.size else (None if b is None else ctypes.addressof(job))
+        job.n_bytes = 0 if b is None else b.size
+        job.width, job.height = int(width), int(height)
+        job.rgba[:] = [int(v) for v in rgba]
+        job.flip_h, job.flip_v = int(bool(flip_h)), int(bool(flip_v))
+        ticket = ctypes.c_uint64()
+        _lib.check(type(self)._submit_mask(self.h, ctypes.byref(job), ctypes.byref(ticket)))
         return ticket.value
 
     def set_semantics(self, flags):
@@ -74,6 +97,7 @@ class _Queue:
 
 class Batcher(_Queue):
     _submit = lib.omr_batcher_submit
+    _submit_mask = lib.omr_batcher_submit_mask
     _wait = lib.omr_batcher_wait
     _set_semantics = lib.omr_batcher_set_semantics
     _destroy = lib.omr_batcher_destroy
@@ -93,6 +117,7 @@ class Batcher(_Queue):
 
 class Pool(_Queue):
     _submit = lib.omr_pool_submit
+    _submit_mask = lib.omr_pool_submit_mask
     _wait = lib.omr_pool_wait
     _set_semantics = lib.omr_pool_set_semantics
     _destroy = lib.omr_pool_destroy

@@ -245,6 +245,16 @@ class Context:
                                            stepping, _ptr(out), int(big_endian_out)), self.h)
         return out
 
+    def project_stacks_device(self, stacks, pixel_type, size_x, size_y, size_z, algorithm, start, end, outs,
+                              stepping=1, big_endian_in=False, big_endian_out=False):
+        """Several same-geometry stacks projected in one launch (the glue's K3)."""
+        n = len(stacks)
+        s = (ctypes.c_void_p * max(n, 1))(*[_ptr(x) for x in stacks])
+        o = (ctypes.c_void_p * max(n, 1))(*[_ptr(x) for x in outs])
+        check(lib.omr_project_stacks_device(self.h, s, n, pixel_type, int(big_endian_in), size_x, size_y, size_z,
+                                            algorithm, start, end, stepping, o, int(big_endian_out)), self.h)
+        return outs
+
     def render_projected_device(self, qdef, channels, stacks, pixel_type, size_x, size_y, size_z,
                                 algorithm, start, end, out, stepping=1, big_endian=False,
                                 flip_h=False, flip_v=False, bindings=None):

@@ -83,11 +83,15 @@ SIGS = {
     "batcherDestroy": (None, [_i64]),
     "batcherSetSemantics": (None, [_i64, _i32]),
     "batcherSubmit": (_i64, [_i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _b, _b, _i32, _f32]),
+    "batcherSubmitProjected": (_i64, [_i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _b, _b, _i32, _f32]),
+    "batcherSubmitMask": (_i64, [_i64, _vp, _i32, _i32, _vp, _b, _b]),
     "batcherWait": (_vp, [_i64, _i64]),
     "poolCreate": (_i64, [_vp, _i32, _i32]),
     "poolDestroy": (None, [_i64]),
     "poolSetSemantics": (None, [_i64, _i32]),
     "poolSubmit": (_i64, [_i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _b, _b, _i32, _f32]),
+    "poolSubmitProjected": (_i64, [_i64, _i64, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _b, _b, _i32, _f32]),
+    "poolSubmitMask": (_i64, [_i64, _vp, _i32, _i32, _vp, _b, _b]),
     "poolWait": (_vp, [_i64, _i64]),
 }
 FN = {n: _sig(n, r, a) for n, (r, a) in SIGS.items()}

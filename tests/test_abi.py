@@ -27,7 +27,9 @@ def test_binding_covers_header():
 
 
 def test_abi_version_and_struct_layout():
-    assert _lib.lib.omr_abi_version() == 1
+    assert _lib.lib.omr_abi_version() == 2
+    assert ctypes.sizeof(_lib.TileJob) == 88 and _lib.TileJob.has_projection.offset == 68
+    assert ctypes.sizeof(_lib.MaskJob) == 40 and _lib.MaskJob.flip_h.offset == 28
     # struct layouts a Panama/JNI binding must reproduce
     assert ctypes.sizeof(_lib.QuantumDef) == 16
     assert ctypes.sizeof(_lib.ChannelBinding) == 72

@@ -298,3 +298,178 @@ def test_quantization_error_fails_only_its_tile(tmp_path):
             assert s == 0
             np.testing.assert_array_equal(np.frombuffer(r, np.uint32).reshape(TH, TW), exp)
     pb.close()
+
+
+# ---- projection jobs (p=intmax|intmean|intsum, ImageRegionRequestHandler.java:506-558) ------------------
+PX_, PY_, PZ_, PC_, PT_ = 256, 128, 6, 3, 2
+
+
+@pytest.fixture(scope="module")
+def romio_stack(tmp_path_factory):
+    rng = np.random.default_rng(46)
+    px = rng.integers(0, 65536, (PT_, PC_, PZ_, PY_, PX_), dtype=np.uint16)
+    path = tmp_path_factory.mktemp("romio_z") / "pixels"
+    write_romio(path, px, _lib.PIXELS_UINT16)
+    return path, px
+
+
+def _oracle_projected(px, ch, model, t, alg, start, end, flip_h=False, flip_v=False):
+    """The glue on the CPU: every active channel's (c, t) stack projected, the full plane rendered."""
+    planes = []
+    for c in range(PC_):
+        if not ch[c].get("active", True):
+            planes.append(np.zeros(PX_ * PY_ * 2, np.uint8))
+            continue
+        stack = np.ascontiguousarray(px[t, c]).astype(">u2")
+        st, p = O.project(stack, _lib.PIXELS_UINT16, PX_, PY_, PZ_, alg, start, end, 1, be_in=True, be_out=True)
+        assert st == 0
+        planes.append(p)
+    st, exp = O.render(ch, planes, _lib.PIXELS_UINT16, PX_, PY_, big_endian=True, flip_h=flip_h, flip_v=flip_v,
+                       model=model)
+    return st, exp
+
+
+def test_projection_jobs_against_the_oracle(romio_stack):
+    """Projection requests through the batcher: every algorithm, default and explicit z ranges, both
+    t, flips, every format; the full plane regardless of the tile fields; duplicates (same t,
+    settings and projection) rendered once."""
+    import io
+    from PIL import Image
+    path, px = romio_stack
+    pb = PixelBuffer(path, PX_, PY_, PZ_, PC_, PT_, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    jobs = [dict(p="intmax", s=-1, e=-1, t=0, fh=False, fv=False, fmt="argb", model="rgb"),
+            dict(p="intmax", s=-1, e=-1, t=1, fh=True, fv=False, fmt="argb", model="rgb"),
+            dict(p="intmean", s=1, e=4, t=0, fh=False, fv=True, fmt="argb", model="greyscale"),
+            dict(p="intsum", s=0, e=5, t=1, fh=False, fv=False, fmt="argb", model="rgb"),
+            dict(p="intmax", s=2, e=3, t=1, fh=False, fv=False, fmt="jpeg", model="rgb"),
+            dict(p="intmean", s=-1, e=-1, t=0, fh=True, fv=True, fmt="png", model="rgb"),
+            dict(p="intmax", s=-1, e=-1, t=0, fh=False, fv=False, fmt="argb", model="rgb")]    # dup of job 0
+    algs = {"intmax": _lib.PROJECTION_MAX, "intmean": _lib.PROJECTION_MEAN, "intsum": _lib.PROJECTION_SUM}
+    with Batcher(0, max_batch=32, max_wait_us=50000) as b:
+        tickets = [b.submit(pb, O.make_qdef(j["model"]), ch, 0, j["t"], 64, 32, 16, 16, flip_h=j["fh"], flip_v=j["fv"],
+                            fmt=j["fmt"], quality=0.9, projection=j["p"], projection_start=j["s"],
+                            projection_end=j["e"]) for j in jobs]
+        outs = [b.wait(t) for t in tickets]
+        st = b.stats()
+    assert st["dedup"] >= 1
+    assert outs[6] == outs[0]
+    for j, got in zip(jobs, outs):
+        s = 0 if j["s"] < 0 else j["s"]
+        e = PZ_ - 1 if j["e"] < 0 else j["e"]
+        stt, exp = _oracle_projected(px, ch, j["model"], j["t"], algs[j["p"]], s, e, j["fh"], j["fv"])
+        assert stt == 0
+        if j["fmt"] == "argb":
+            np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(PY_, PX_), exp)
+        elif j["fmt"] == "jpeg":
+            assert got == O.encode_jpeg(exp, PX_, PY_, 0.9)
+        else:
+            rgb = np.asarray(Image.open(io.BytesIO(got)).convert("RGB"))
+            np.testing.assert_array_equal(rgb, exp.view(np.uint8).reshape(PY_, PX_, 4)[..., 2::-1])
+    pb.close()
+
+
+def test_projection_job_errors_fail_alone(romio_stack):
+    """The glue's quirk 3 (a rendered channel's index >= the number of active channels: OMR_INTERNAL,
+    Appendix B) and a z range past sizeZ fail only their own job; a projection job in the same round
+    still renders."""
+    path, px = romio_stack
+    pb = PixelBuffer(path, PX_, PY_, PZ_, PC_, PT_, _lib.PIXELS_UINT16)
+    ch_bad = c2_channels(3)
+    ch_bad[0]["active"] = False
+    ch_bad[1]["active"] = False                  # only c=2 active: index 2 >= 1 active channel
+    ch = c2_channels(3)
+    with Batcher(0, max_batch=32, max_wait_us=50000) as b:
+        t_bad = b.submit(pb, O.make_qdef("rgb"), ch_bad, 0, 0, 0, 0, 16, 16, fmt="argb", projection="intmax")
+        t_range = b.submit(pb, O.make_qdef("rgb"), ch, 0, 1, 0, 0, 16, 16, fmt="argb", projection="intmax",
+                           projection_start=0, projection_end=PZ_ + 3)
+        t_ok = b.submit(pb, O.make_qdef("rgb"), ch, 0, 1, 0, 0, 16, 16, fmt="argb", projection="intmax")
+        with pytest.raises(_lib.OmrError) as e:
+            b.wait(t_bad)
+        assert e.value.status == _lib.INTERNAL
+        with pytest.raises(_lib.OmrError):
+            b.wait(t_range)
+        got = b.wait(t_ok)
+        with pytest.raises(_lib.OmrError):                                 # unknown algorithm
+            b.submit(pb, O.make_qdef("rgb"), ch, 0, 1, 0, 0, 16, 16, fmt="argb", projection=7)
+    stt, exp = _oracle_projected(px, ch, "rgb", 1, _lib.PROJECTION_MAX, 0, PZ_ - 1)
+    np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(PY_, PX_), exp)
+    pb.close()
+
+
+def test_pool_projection_and_mask_jobs(romio_stack, romio):
+    """A 2-entry pool serving tile, projection and shape-mask jobs from concurrent workers: every
+    result against the CPU restatement, both batchers used."""
+    import threading
+    import torch
+    path, px = romio_stack
+    pb = PixelBuffer(path, PX_, PY_, PZ_, PC_, PT_, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    devices = [i % torch.cuda.device_count() for i in range(2)]
+    rng = np.random.default_rng(8)
+    masks = []
+    for k in range(12):
+        w, h = [(64, 32), (37, 21), (8, 8), (200, 100)][k % 4]
+        masks.append((rng.integers(0, 256, (w * h + 7) // 8, dtype=np.uint8).tobytes(), w, h,
+                      tuple(int(v) for v in rng.integers(0, 256, 4)), bool(k & 1), bool(k & 2)))
+    outs_p, outs_m, where = [None] * 8, [None] * len(masks), []
+    with Pool(devices, max_batch=16, max_wait_us=3000) as pool:
+        pool.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+
+        def worker(k):
+            for i in range(k, 8, 4):
+                t = pool.submit(pb, O.make_qdef("rgb"), ch, 0, i % 2, 0, 0, 16, 16, fmt="argb",
+                                projection=["intmax", "intmean"][i % 2])
+                where.append(pool.device_index(t))
+                outs_p[i] = pool.wait(t)
+            for i in range(k, len(masks), 4):
+                t = pool.submit_mask(*masks[i])
+                where.append(pool.device_index(t))
+                outs_m[i] = pool.wait(t)
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    assert sorted(set(where)) == [0, 1]
+    for i in range(8):
+        stt, exp = _oracle_projected(px, ch, "rgb", i % 2, [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN][i % 2], 0,
+                                     PZ_ - 1)
+        np.testing.assert_array_equal(np.frombuffer(outs_p[i], np.uint32).reshape(PY_, PX_), exp)
+    import io
+    from PIL import Image
+    with O.semantics(_lib.SEM_MASK_PIXEL_FLIP):
+        for (bits, w, h, rgba, fh, fv), png in zip(masks, outs_m):
+            st, idx = O.mask_indices(bits, w, h, fh, fv)
+            exp = np.zeros((h, w, 4), np.uint8)
+            exp[idx == 1] = rgba
+            np.testing.assert_array_equal(np.asarray(Image.open(io.BytesIO(png)).convert("RGBA")), exp)
+    pb.close()
+
+
+def test_mask_jobs_dedup_and_404(ctx):
+    """Mask jobs of one round share one batch call; identical masks render once; every case the
+    single call answers with 404 fails only its own job."""
+    bits = bytes(range(32))
+    with Batcher(0, max_batch=32, max_wait_us=50000) as b:
+        b.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+        t = [b.submit_mask(bits, 16, 16, (255, 0, 0, 255)) for _ in range(3)]
+        t.append(b.submit_mask(bits, 16, 16, (0, 255, 0, 255)))
+        t.append(b.submit_mask(bytes(2), 16, 16, (0, 255, 0, 255)))           # short: 404
+        t.append(b.submit_mask(None, 16, 16, (0, 255, 0, 255)))               # null: 404
+        t.append(b.submit_mask(bits, 0, 16, (0, 255, 0, 255)))                # zero size: 404
+        res = []
+        for x in t:
+            try:
+                res.append(b.wait(x))
+            except _lib.OmrError as e:
+                res.append(e.status)
+        st = b.stats()
+    assert res[0] == res[1] == res[2] and res[3] != res[0]
+    assert res[4:] == [_lib.NOT_FOUND] * 3
+    assert st["dedup"] >= 2
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+    try:
+        assert res[0] == ctx.render_shape_mask_png(bits, 16, 16, (255, 0, 0, 255))
+    finally:
+        ctx.set_semantics(0)

@@ -171,6 +171,10 @@ def test_batcher_and_pool_validation(fake):
     _raises(IA, "batcherSubmit", 0, *args)                 # null batcher
     _raises(IA, "poolSubmit", 0, *args)
     _raises(IA, "batcherWait", 0, 1)
+    _raises(IA, "batcherSubmitProjected", 0, 1, 1, s, luts, 0, 0, -1, -1, 0, 0, 0, np.float32(0.9))
+    _raises(IA, "poolSubmitProjected", 0, 1, 1, s, luts, 0, 0, -1, -1, 0, 0, 0, np.float32(0.9))
+    _raises(IA, "batcherSubmitMask", 0, M.jbytes(bytes(8)), 8, 8, M.jbytes(bytes(4)), 0, 0)
+    _raises(IA, "poolSubmitMask", 0, M.jbytes(bytes(8)), 8, 8, M.jbytes(bytes(4)), 0, 0)
     _raises(IA, "poolWait", 0, 1)
     _raises(IA, "poolCreate", M.jints(np.zeros(0, np.int32)), 8, 100)              # no devices
     _raises(IA, "poolCreate", None, 8, 100)

@@ -204,3 +204,43 @@ def test_batcher_and_pool(romio, kind):
             M.call(sem, q, 1 << 20)
     finally:
         M.call(destroy, q)
+
+
+@pytest.mark.parametrize("kind", ["batcher", "pool"])
+def test_projected_and_mask_jobs(romio, kind):
+    """batcherSubmitProjected / poolSubmitProjected (the full plane, p=intmax over the one z of the
+    fixture = the plane itself) and batcherSubmitMask / poolSubmitMask (PNG; a short mask throws 404
+    at wait)."""
+    import torch
+    from PIL import Image
+    pb, px = romio
+    chans = c2_channels(3)
+    if kind == "batcher":
+        q = M.call("batcherCreate", 0, 16, 2000)
+        sp, sm, wait, destroy = "batcherSubmitProjected", "batcherSubmitMask", "batcherWait", "batcherDestroy"
+    else:
+        devs = [i % torch.cuda.device_count() for i in range(2)]
+        q = M.call("poolCreate", M.jints(np.array(devs, np.int32)), 16, 2000)
+        sp, sm, wait, destroy = "poolSubmitProjected", "poolSubmitMask", "poolWait", "poolDestroy"
+    try:
+        s, luts = M.pack_channels(chans)
+        t = M.call(sp, q, pb, 1, s, luts, 0, _lib.PROJECTION_MAX, -1, -1, 1, 0, _lib.FORMAT_ARGB, np.float32(0.9))
+        got = np.frombuffer(M.to_bytes(M.call(wait, q, t)), np.uint32).reshape(512, 512)
+        np.testing.assert_array_equal(got, _oracle_tile(px, chans, 0, 0, 512, fh=True))
+        rng = np.random.default_rng(3)
+        bits = rng.integers(0, 256, 37 * 21 // 8 + 1, dtype=np.uint8).tobytes()
+        t = M.call(sm, q, M.jbytes(bits), 37, 21, M.jbytes(bytes([255, 0, 0, 128])), 1, 0)
+        png = M.to_bytes(M.call(wait, q, t))
+        st, idx = O.mask_indices(bits, 37, 21, True, False)
+        exp = np.zeros((21, 37, 4), np.uint8)
+        exp[idx == 1] = (255, 0, 0, 128)
+        np.testing.assert_array_equal(np.asarray(Image.open(io.BytesIO(png)).convert("RGBA")), exp)
+        t = M.call(sm, q, M.jbytes(bytes(2)), 37, 21, M.jbytes(bytes(4)), 0, 0)
+        with pytest.raises(M.JavaException) as e:
+            M.call(wait, q, t)
+        assert e.value.status == _lib.NOT_FOUND
+        with pytest.raises(M.JavaException) as e:                  # 3-byte colour
+            M.call(sm, q, M.jbytes(bits), 37, 21, M.jbytes(bytes(3)), 0, 0)
+        assert e.value.status == _lib.INVALID_ARGUMENT
+    finally:
+        M.call(destroy, q)

@@ -52,3 +52,44 @@ def test_java_constants_match_header():
                     assert int(val, 0) == hdr["OMR_" + name], (f, name, val)
                     checked += 1
     assert checked >= 15, checked
+
+
+def _canon(name):
+    n = name.lower().replace("_", "")
+    for key, canon in (("active", "active"), ("family", "family"), ("coefficient", "coefficient"),
+                       ("noise", "noise_reduction"), ("reverse", "reverse"), ("windowstart", "start"),
+                       ("inputstart", "start"), ("windowend", "end"), ("inputend", "end"), ("globalmin", "gmin"),
+                       ("globalmax", "gmax"), ("rgba", "rgba")):
+        if key in n:
+            return canon
+    raise AssertionError(name)
+
+
+def test_pack_channel_layout_in_lockstep():
+    """The 13-double channel record has three writers/readers that must agree field by field:
+    OmrNative.packChannel (Java), the shim's load_settings (C) and the mock's pack_channels (the
+    test double the GPU shim tests use, tests/jni_mock.py)."""
+    java = _read(JAVA)
+    body = java[java.index("public static void packChannel"):]
+    body = body[:body.index("\n    }\n")]
+    jmap = {}
+    for idx, expr in re.findall(r"settings\[o(?: \+ (\d+))?(?: \+ k)?\]\s*=\s*(\w+)", body):
+        jmap[int(idx or 0)] = _canon(expr)
+    assert "settings[o + 9 + k] = rgba[k]" in body
+    jmap.update({9 + k: "rgba" for k in range(4)})
+    c = _read(JNI_C)
+    load = c[c.index("static int load_settings"):]
+    load = load[:load.index("\n}\n")]
+    cmap = {int(i): _canon(f) for f, i in re.findall(r"b->(\w+)\s*=\s*(?:\(\w+\))?p\[(\d+)\]", load)}
+    assert "b->rgba[k] = (uint8_t)(int)p[9 + k]" in load
+    cmap.update({9 + k: "rgba" for k in range(4)})
+    mock = _read(os.path.join(REPO, "tests", "jni_mock.py"))
+    pk = mock[mock.index("def pack_channels"):]
+    pk = pk[:pk.index("\n\n\n")]
+    lst = pk[pk.index("s[o:o + 13] = ["):pk.index("]\n", pk.index("s[o:o + 13] = ["))]
+    items = re.findall(r'"(\w+)"', lst)
+    pmap = {i: _canon(n) for i, n in enumerate(items)}
+    assert "*d.get(\"rgba\"" in lst
+    pmap.update({9 + k: "rgba" for k in range(4)})
+    assert len(jmap) == len(cmap) == len(pmap) == 13, (jmap, cmap, pmap)
+    assert jmap == cmap == pmap, (jmap, cmap, pmap)

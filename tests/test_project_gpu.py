@@ -80,6 +80,24 @@ def test_projection_device_api_and_validation(ctx):
         assert ei.value.status == _lib.INVALID_ARGUMENT
 
 
+@pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN, _lib.PROJECTION_SUM])
+def test_project_stacks_device_one_launch(ctx, alg):
+    """omr_project_stacks_device: three stacks in one launch (the glue's K3), each == the oracle."""
+    import torch
+    z, h, w = 20, 64, 96
+    stacks = [rand_stack(np.uint16, z, h, w, 40 + c).astype(">u2") for c in range(3)]
+    outs = [torch.empty(h * w * 2, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    ctx.project_stacks_device([dev(s) for s in stacks], _lib.PIXELS_UINT16, w, h, z, alg, 2, z - 3, outs,
+                              big_endian_in=True)
+    ctx.synchronize()
+    for s, o in zip(stacks, outs):
+        st, exp = O.project(s, _lib.PIXELS_UINT16, w, h, z, alg, 2, z - 3, be_in=True)
+        assert st == 0
+        np.testing.assert_array_equal(o.cpu().numpy(), exp)
+    with pytest.raises(_lib.OmrError):
+        ctx.project_stacks_device([dev(stacks[0])] * 33, _lib.PIXELS_UINT16, w, h, z, alg, 0, 1, outs * 11)
+
+
 @pytest.mark.parametrize("alg", [_lib.PROJECTION_MAX, _lib.PROJECTION_MEAN])
 def test_c3_projection_then_composite_full_size(ctx, alg):
     """BASELINE config C3: 3-channel uint16 512x512x64 Z-stack -> max/mean projection -> composite.
