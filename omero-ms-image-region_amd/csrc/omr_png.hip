@@ -330,17 +330,67 @@ __device__ __forceinline__ uint32_t paeth(uint32_t a, uint32_t b, uint32_t c) {
     return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
 }
 
-// LDS: the raw bytes of this row and the row above (2 * (rowlen - 1) bytes, dynamic); every
-// filter residual is then computed from LDS.  One workgroup, row y of image A: the filter byte +
-// filtered row at flt + y * rowlen, the row's Adler partials at rs[0..1].
+// LDS of D1 for a row of rb = rowlen - 1 bytes: this row and the row above, each behind 4 zero
+// bytes (the left neighbours of the first pixel are 0) and padded to whole dwords, plus the output
+// row (filter byte + residuals) placed at the global row's address mod 4, so it leaves with aligned
+// dword stores.  Rows whose three buffers exceed the LDS budget write the residuals as bytes.
+__host__ __device__ constexpr int64_t png_row_stride(int64_t rb) { return ((rb + 3) & ~(int64_t)3) + 4; }
+__host__ __device__ constexpr int64_t png_filter_lds_in(int64_t rb) { return 2 * png_row_stride(rb); }
+__host__ __device__ constexpr int64_t png_filter_lds_out(int64_t rb) { return ((rb + 1 + 3 + 3) & ~(int64_t)3) + 16; }
+constexpr int64_t kPngFilterLdsMax = 150 * 1024;
+__host__ __device__ constexpr bool png_filter_stage_out(int64_t rb) {
+    return png_filter_lds_in(rb) + png_filter_lds_out(rb) <= kPngFilterLdsMax;
+}
+__host__ __device__ constexpr int64_t png_filter_lds(int64_t rb) {
+    return png_filter_lds_in(rb) + (png_filter_stage_out(rb) ? png_filter_lds_out(rb) : 0);
+}
+
+__device__ __forceinline__ uint32_t byte_at(uint32_t w, int k) { return (w >> (8 * k)) & 0xFF; }
+
+// The five PNG filter residuals of 4 row bytes (dword X of this row, B of the row above; A / C the
+// same bytes bpp to the left), mod 256, byte k of r[f].
+__device__ __forceinline__ void png_residuals(uint32_t X, uint32_t A, uint32_t B, uint32_t C, uint32_t (&r)[5]) {
+#pragma unroll
+    for (int f = 0; f < 5; ++f) r[f] = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = byte_at(X, k), a = byte_at(A, k), b = byte_at(B, k), c = byte_at(C, k);
+        r[0] |= x << (8 * k);
+        r[1] |= ((x - a) & 0xFF) << (8 * k);
+        r[2] |= ((x - b) & 0xFF) << (8 * k);
+        r[3] |= ((x - ((a + b) >> 1)) & 0xFF) << (8 * k);
+        r[4] |= ((x - paeth(a, b, c)) & 0xFF) << (8 * k);
+    }
+}
+
+// |signed residual| summed over the bytes of w below `valid` (libpng's minimum-sum heuristic).
+__device__ __forceinline__ uint32_t png_abs_sum(uint32_t w, int valid) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t v = byte_at(w, k);
+        s += k < valid ? min(v, 256u - v) : 0u;
+    }
+    return s;
+}
+
+// One workgroup, row y of image A: the filter byte + filtered row at flt + y * rowlen, the row's
+// Adler partials at rs[0..1].  Four row bytes per lane step: dword LDS reads, the left neighbours
+// by one alignbyte of two dwords.
 __device__ void png_filter_row(const PngArgs& A, int bpp, int y, uint8_t* __restrict__ flt,
                                unsigned long long* __restrict__ rs, uint8_t* s_rows) {
     __shared__ uint32_t s_sum[5][4];
     __shared__ int s_f;
+    __shared__ unsigned long long s_ad[2][4];
     const int rb = (int)A.rowlen - 1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t* cur = s_rows;
-    uint8_t* prev = s_rows + rb;
+    const int stride = (int)png_row_stride(rb);
+    uint8_t* cur = s_rows + 4;
+    uint8_t* prev = s_rows + 4 + stride;
+    const int nw = (rb + 3) >> 2;                  // row dwords
+    for (int k = threadIdx.x; k < 2 * stride / 4; k += 256)
+        reinterpret_cast<uint32_t*>(s_rows)[k] = 0;   // zero pads and dword tails
+    __syncthreads();
     if (A.kind == kRgb) {                         // one ARGB load per pixel and row
         for (int px = threadIdx.x; px < A.W; px += 256) {
             const uint32_t v = A.argb[(int64_t)y * A.W + px];
@@ -355,23 +405,23 @@ __device__ void png_filter_row(const PngArgs& A, int bpp, int y, uint8_t* __rest
         }
     }
     __syncthreads();
-    uint32_t sm[5] = {0, 0, 0, 0, 0};
-    auto filt = [&](int i, uint32_t (&f)[5]) {
-        const uint32_t x = cur[i];
-        const uint32_t a = i >= bpp ? cur[i - bpp] : 0u;
-        const uint32_t b = prev[i];
-        const uint32_t c = i >= bpp ? prev[i - bpp] : 0u;
-        f[0] = x;
-        f[1] = (x - a) & 0xFF;
-        f[2] = (x - b) & 0xFF;
-        f[3] = (x - ((a + b) >> 1)) & 0xFF;
-        f[4] = (x - paeth(a, b, c)) & 0xFF;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(cur);     // cw[-1] is the zero pad
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(prev);
+    const int lsh = 4 - bpp;                       // bytes i-bpp .. i-bpp+3 = alignbyte(w[i/4], w[i/4-1], 4-bpp)
+    auto load = [&](int j, uint32_t& X, uint32_t& Av, uint32_t& Bv, uint32_t& Cv) {
+        X = cw[j];
+        Bv = pw[j];
+        Av = __builtin_amdgcn_alignbyte(X, cw[j - 1], lsh);
+        Cv = __builtin_amdgcn_alignbyte(Bv, pw[j - 1], lsh);
     };
-    for (int i = threadIdx.x; i < rb; i += 256) {
-        uint32_t f[5];
-        filt(i, f);
+    uint32_t sm[5] = {0, 0, 0, 0, 0};
+    for (int j = threadIdx.x; j < nw; j += 256) {
+        uint32_t X, Av, Bv, Cv, r[5];
+        load(j, X, Av, Bv, Cv);
+        png_residuals(X, Av, Bv, Cv, r);
+        const int valid = min(4, rb - 4 * j);
 #pragma unroll
-        for (int k = 0; k < 5; ++k) sm[k] += min(f[k], 256u - f[k]);
+        for (int f = 0; f < 5; ++f) sm[f] += png_abs_sum(r[f], valid);
     }
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -392,26 +442,60 @@ __device__ void png_filter_row(const PngArgs& A, int bpp, int y, uint8_t* __rest
     __syncthreads();
     const int f = s_f;
     const int64_t row0 = (int64_t)y * A.rowlen;
-    unsigned long long s1 = 0, s2 = 0;
-    if (threadIdx.x == 0) {
-        flt[row0] = (uint8_t)f;
+    // Adler partials in 32 bits per lane: s1 = sum v, s2 = sum (raw - idx) v = (raw - row0 - 1) * sum v
+    // - sum i v over the row's bytes i (idx = row0 + 1 + i); a lane's sum i v stays below 2^32
+    uint32_t sv = 0, siv = 0;
+    const bool staged = png_filter_stage_out(rb);
+    const int o0 = (int)(row0 & 3);                // the output row's first byte, at its address mod 4
+    uint8_t* ob = s_rows + png_filter_lds_in(rb);
+    for (int j = threadIdx.x; j < nw; j += 256) {
+        uint32_t X, Av, Bv, Cv, r[5];
+        load(j, X, Av, Bv, Cv);
+        png_residuals(X, Av, Bv, Cv, r);
+        const uint32_t w = r[f];
+        const int valid = min(4, rb - 4 * j);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < valid) {
+                const uint32_t v = byte_at(w, k);
+                sv += v;
+                siv += (uint32_t)(4 * j + k) * v;
+                if (staged) ob[o0 + 1 + 4 * j + k] = (uint8_t)v;
+                else flt[row0 + 1 + 4 * j + k] = (uint8_t)v;
+            }
+        }
+    }
+    unsigned long long s1 = sv;
+    unsigned long long s2 = (unsigned long long)(A.raw - row0 - 1) * sv - siv;
+    if (threadIdx.x == 0) {                        // the filter-type byte
         s1 += (unsigned long long)f;
         s2 += (unsigned long long)(A.raw - row0) * (unsigned long long)f;
+        if (staged) ob[o0] = (uint8_t)f;
+        else flt[row0] = (uint8_t)f;
     }
-    for (int i = threadIdx.x; i < rb; i += 256) {
-        uint32_t fv[5];
-        filt(i, fv);
-        const uint32_t v = fv[f];
-        const int64_t idx = row0 + 1 + i;
-        flt[idx] = (uint8_t)v;
-        s1 += v;
-        s2 += (unsigned long long)(A.raw - idx) * v;
+    if (staged) {
+        __syncthreads();
+        // [row0, row0 + rowlen) out: interior dwords stored whole, the partial first / last dword
+        // (shared with the neighbouring rows' workgroups) byte by byte
+        const int64_t g0 = row0 >> 2, g1 = (row0 + A.rowlen - 1) >> 2;
+        uint32_t* gw = reinterpret_cast<uint32_t*>(flt);
+        const uint32_t* lw = reinterpret_cast<const uint32_t*>(ob);
+        for (int64_t g = g0 + threadIdx.x; g <= g1; g += 256) {
+            const int64_t b0 = g * 4;
+            if (b0 >= row0 && b0 + 4 <= row0 + A.rowlen) {
+                gw[g] = lw[g - g0];
+            } else {
+                for (int k = 0; k < 4; ++k) {
+                    const int64_t bi = b0 + k;
+                    if (bi >= row0 && bi < row0 + A.rowlen) flt[bi] = ob[bi - row0 + o0];
+                }
+            }
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         s1 += __shfl_down(s1, o, 64);
         s2 += __shfl_down(s2, o, 64);
     }
-    __shared__ unsigned long long s_ad[2][4];
     if (lane == 0) { s_ad[0][wv] = s1; s_ad[1][wv] = s2; }
     __syncthreads();
     if (threadIdx.x == 0) {      // per-row Adler partials; summed by k_png_adler_rows
@@ -455,18 +539,59 @@ __host__ __device__ constexpr int64_t tok_slots(int64_t nseg) {
 }
 constexpr int kMaxBack = 31 * 1024;         // LDS look-back window (bytes)
 
+// A token: a literal byte (bit 31 clear), or a match: bit 31 | lsym - 257 (bits 0-4) | dsym << 5
+// (bits 5-9) | the length's extra-bits value << 10 (5 bits) | the distance's extra-bits value << 15
+// (13 bits).  D4 / D5 then code it with the two code tables alone; the extra-bit counts follow
+// from the symbols (RFC 1951 3.2.5).
+__host__ __device__ constexpr int len_xbits_of(int ls) { return (ls < 8 || ls == 28) ? 0 : (ls - 4) >> 2; }
+__host__ __device__ constexpr int dist_xbits_of(int ds) { return ds < 4 ? 0 : (ds - 2) >> 1; }
+__device__ __forceinline__ uint32_t pack_match(const DeflateTabs& T, uint32_t l, uint32_t d) {
+    const uint32_t ls = T.len_sym[l] - 257u;
+    const uint32_t ds = (d - 1) < 256 ? T.dist_code[d - 1] : T.dist_code[256 + ((d - 1) >> 7)];
+    return 0x80000000u | ls | (ds << 5) | ((l - T.len_base[ls]) << 10) | ((d - T.dist_base[ds]) << 15);
+}
+
+// Bit q of the result: byte beg+q equals byte beg+q-d, for q < n (the segment's bytes), from the
+// segment's 32 bytes x[] (registers) and the 36 staged bytes from beg-d rounded down to a dword.
+__device__ __forceinline__ uint32_t eq_mask(const uint32_t (&x)[8], const uint32_t* sw, int64_t a) {
+    const uint32_t* q = sw + (a >> 2);
+    const int sh = (int)(a & 3);
+    uint32_t m = 0;
+    uint32_t lo = q[0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t hi = q[i + 1];
+        const uint32_t y = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        lo = hi;
+        const uint32_t e = x[i] ^ y;                          // zero bytes: equal
+        const uint32_t z = ~(((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e | 0x7F7F7F7Fu);   // 0x80 per zero byte
+        const uint32_t nib = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+        m |= nib << (4 * i);
+    }
+    return m;
+}
+
 // One lane per kSeg-byte segment; the workgroup first stages its 4 KiB of filtered stream plus
-// the look-back window (one image row, <= 31 KiB) in LDS, so the greedy parse's byte compares
-// are LDS reads instead of dependent global loads.  Parse block `blk` of one image: flt is the
-// image's filtered stream (16-byte aligned), tokens / ntok its segments' token slots and counts,
-// lhist / dhist its symbol histograms.
+// the look-back window (one image row, <= 31 KiB) in LDS.  Greedy LZ77 over the distances image
+// rows repeat at (1, bpp, 2*bpp, one row up), matches inside the segment: for each distance d a
+// 32-bit mask of "byte == byte d back" is built with dword compares, and the match length at q is
+// the run of ones from bit q -- the parse itself runs in registers.  The first candidate with the
+// longest match wins (same tokens as a byte-by-byte compare loop).  Parse block `blk` of one image:
+// flt is the image's filtered stream (16-byte aligned), tokens / ntok its segments' token slots
+// (tok_at) and counts, lhist / dhist its symbol histograms.
 __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw, int64_t rowlen, int bpp,
                                    int64_t nseg, int64_t blk, int32_t back, uint32_t* __restrict__ tokens,
                                    uint16_t* __restrict__ ntok, uint32_t* __restrict__ lhist,
                                    uint32_t* __restrict__ dhist, uint8_t* s_win) {
     __shared__ uint32_t lh[286], dh[30];
+    __shared__ DeflateTabs T;
     for (int i = threadIdx.x; i < 286; i += kParseLanes) lh[i] = 0;
     if (threadIdx.x < 30) dh[threadIdx.x] = 0;
+    {
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(&c_dfl);
+        uint8_t* dst = reinterpret_cast<uint8_t*>(&T);
+        for (int i = threadIdx.x; i < (int)sizeof(DeflateTabs); i += kParseLanes) dst[i] = src[i];
+    }
     const int64_t bbeg = blk * kParseLanes * kSeg;
     const int64_t bend = min(raw, bbeg + (int64_t)kParseLanes * kSeg);
     const int64_t wbeg = max((int64_t)0, bbeg - back);          // back is a multiple of 16
@@ -478,31 +603,56 @@ __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw,
     const int64_t s = blk * kParseLanes + threadIdx.x;
     if (s < nseg) {
         const uint8_t* f = s_win - wbeg;            // f[p] for p in [wbeg, bend)
-        const int64_t beg = s * kSeg, end = min(raw, beg + kSeg);
-        const int64_t cand[4] = {1, bpp, 2 * bpp, rowlen};
-        const int nc = bpp == 1 ? 2 : 3;
-        int nt = 0;
-        int64_t p = beg;
-        while (p < end) {
-            const int64_t lim = min((int64_t)258, end - p);
-            int64_t best = 0, bd = 0;
-            const uint32_t x0 = f[p];
+        const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_win);
+        const int64_t beg = s * kSeg;
+        const int n = (int)(min(raw, beg + kSeg) - beg);
+        const uint32_t nmask = n >= 32 ? 0xFFFFFFFFu : (1u << n) - 1u;
+        uint32_t x[8];
+        {
+            const uint4* o = reinterpret_cast<const uint4*>(s_win + (beg - wbeg));   // 16-byte aligned
+            const uint4 u0 = o[0], u1 = o[1];
+            x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+            x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+        }
+        // candidates in the compare order of the byte-wise parse: 1, bpp, 2 bpp (not for bpp 1,
+        // where bpp repeats distance 1), one row up
+        const int nd = bpp == 1 ? 2 : 4;
+        const uint32_t dl[4] = {1u, bpp == 1 ? (uint32_t)rowlen : (uint32_t)bpp,
+                                (uint32_t)(2 * bpp), (uint32_t)rowlen};
+        uint32_t m[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k >= nd) break;
+            const int64_t d = dl[k];
+            if (d > back) continue;                              // past the staged look-back
+            if (beg - d >= wbeg) {
+                m[k] = eq_mask(x, sw, beg - d - wbeg) & nmask;
+            } else {                                             // the window's first bytes
+                uint32_t mm = 0;
+                for (int q = 0; q < n; ++q)
+                    if (beg + q - d >= wbeg && f[beg + q] == f[beg + q - d]) mm |= 1u << q;
+                m[k] = mm;
+            }
+        }
+        int nt = 0, p = 0;
+        while (p < n) {
+            int best = 0;
+            uint32_t bd = 0;
+#pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (k >= nc && k != 3) continue;
-                const int64_t d = cand[k];
-                if (d > p - wbeg || d > back) continue;   // inside the staged window
-                if (f[p - d] != x0) continue;
-                int64_t l = 1;
-                while (l < lim && f[p + l] == f[p - d + l]) ++l;
-                if (l > best) { best = l; bd = d; }
-                if (best == lim) break;
+                if (k >= nd) break;
+                const uint32_t v = m[k] >> p;
+                const int l = v == 0xFFFFFFFFu ? 32 : __builtin_ctz(~v);   // run of equal bytes from p
+                if (l > best) { best = l; bd = dl[k]; }
             }
             if (best >= 3) {
-                tokens[tok_at(s, nt++)] = 0x80000000u | (uint32_t)(best - 3) | ((uint32_t)(bd - 1) << 8);
-                atomicAdd(&lh[c_dfl.len_sym[best]], 1u);
-                atomicAdd(&dh[dist_sym((uint32_t)bd)], 1u);
+                const uint32_t t = pack_match(T, (uint32_t)best, bd);
+                tokens[tok_at(s, nt++)] = t;
+                atomicAdd(&lh[257 + (t & 31)], 1u);
+                atomicAdd(&dh[(t >> 5) & 31], 1u);
                 p += best;
             } else {
+                const uint32_t x0 = f[beg + p];
                 tokens[tok_at(s, nt++)] = x0;
                 atomicAdd(&lh[x0], 1u);
                 ++p;
@@ -924,9 +1074,24 @@ static void build_dynamic_block(const uint32_t* lhist, const uint32_t* dhist, Df
 
 __device__ __forceinline__ uint32_t token_bits(uint32_t t, const uint8_t* llen, const uint8_t* dlen) {
     if (!(t & 0x80000000u)) return llen[t];
-    const uint32_t l = (t & 0xFF) + 3, d = ((t >> 8) & 0x7FFF) + 1;
-    const int ls = c_dfl.len_sym[l], ds = dist_sym(d);
-    return llen[ls] + c_dfl.len_xbits[ls - 257] + dlen[ds] + c_dfl.dist_xbits[ds];
+    const int ls = (int)(t & 31), ds = (int)((t >> 5) & 31);
+    return llen[257 + ls] + len_xbits_of(ls) + dlen[ds] + dist_xbits_of(ds);
+}
+
+// The codes of one packed token, LSB-first through put(value, bits).
+template <typename Put>
+__device__ __forceinline__ void put_token(uint32_t t, const uint16_t* lcode, const uint8_t* llen, const uint16_t* dcode,
+                                          const uint8_t* dlen, Put& put) {
+    if (!(t & 0x80000000u)) {
+        put(lcode[t], llen[t]);
+        return;
+    }
+    const int ls = (int)(t & 31), ds = (int)((t >> 5) & 31);
+    put(lcode[257 + ls], llen[257 + ls]);
+    const int lx = len_xbits_of(ls), dx = dist_xbits_of(ds);
+    if (lx) put((t >> 10) & 31u, lx);
+    put(dcode[ds], dlen[ds]);
+    if (dx) put((t >> 15) & 0x1FFFu, dx);
 }
 
 __global__ void __launch_bounds__(256) k_png_lz_bits(DflArgs D) {
@@ -984,19 +1149,7 @@ __global__ void __launch_bounds__(256) k_png_lz_write(DflArgs D) {
             nacc -= 32;
         }
     };
-    for (int i = 0; i < nt; ++i) {
-        const uint32_t t = D.tokens[tok_at(s, i)];
-        if (!(t & 0x80000000u)) {
-            put(lcode[t], llen[t]);
-        } else {
-            const uint32_t l = (t & 0xFF) + 3, d = ((t >> 8) & 0x7FFF) + 1;
-            const int ls = c_dfl.len_sym[l], ds = dist_sym(d);
-            put(lcode[ls], llen[ls]);
-            if (c_dfl.len_xbits[ls - 257]) put(l - c_dfl.len_base[ls - 257], c_dfl.len_xbits[ls - 257]);
-            put(dcode[ds], dlen[ds]);
-            if (c_dfl.dist_xbits[ds]) put(d - c_dfl.dist_base[ds], c_dfl.dist_xbits[ds]);
-        }
-    }
+    for (int i = 0; i < nt; ++i) put_token(D.tokens[tok_at(s, i)], lcode, llen, dcode, dlen, put);
     if (nacc > 0) atomicOr(&D.words[wpos], (uint32_t)acc);
 }
 
@@ -1158,8 +1311,8 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     OMR_HIP(ctx, hipMemsetAsync(ws + L.crc, 0, 4, ctx->stream));
     OMR_HIP(ctx, hipMemsetAsync(ws + L.lhist, 0, L.dhist + 30 * 4 - L.lhist, ctx->stream));
     const unsigned gseg = (unsigned)((L.nseg + 255) / 256);
-    const size_t rows_lds = align_up(2 * (size_t)(P.rowlen - 1), 16);
-    if (rows_lds > (size_t)150 * 1024) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG row too wide");
+    const size_t rows_lds = align_up((size_t)png_filter_lds(P.rowlen - 1), 16);
+    if (rows_lds > (size_t)kPngFilterLdsMax) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG row too wide");
     if (P.chunk_bytes >= ((int64_t)1 << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG image too large");
     if (rows_lds > (size_t)60 * 1024)
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_png_filter),
@@ -1572,19 +1725,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_write(PngBatch B) {
                 nacc -= 32;
             }
         };
-        for (int k = 0; k < nt; ++k) {
-            const uint32_t t = tok[tok_at(ls, k)];
-            if (!(t & 0x80000000u)) {
-                put(lcode[t], llen[t]);
-            } else {
-                const uint32_t l = (t & 0xFF) + 3, d = ((t >> 8) & 0x7FFF) + 1;
-                const int lsym = c_dfl.len_sym[l], ds = dist_sym(d);
-                put(lcode[lsym], llen[lsym]);
-                if (c_dfl.len_xbits[lsym - 257]) put(l - c_dfl.len_base[lsym - 257], c_dfl.len_xbits[lsym - 257]);
-                put(dcode[ds], dlen[ds]);
-                if (c_dfl.dist_xbits[ds]) put(d - c_dfl.dist_base[ds], c_dfl.dist_xbits[ds]);
-            }
-        }
+        for (int k = 0; k < nt; ++k) put_token(tok[tok_at(ls, k)], lcode, llen, dcode, dlen, put);
         if (nacc > 0) atomicOr(&sw[wpos], (uint32_t)acc);
     }
     __syncthreads();
@@ -1822,7 +1963,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         L.toks += tok_slots(d.nseg);
         L.flt += (int64_t)align_up((size_t)P.raw, 16);
         L.words += (int64_t)align_up((size_t)(P.raw / 2 + 128), 4);     // <= 16 bits per byte + header
-        L.rows_lds = std::max(L.rows_lds, align_up(2 * (size_t)(P.rowlen - 1), 16));
+        L.rows_lds = std::max(L.rows_lds, align_up((size_t)png_filter_lds(P.rowlen - 1), 16));
         L.parse_lds = std::max(L.parse_lds, (size_t)d.back + (size_t)kParseLanes * kSeg);
         if (i && (h.kind != im[0].kind || h.W != im[0].W || h.H != im[0].H)) L.uniform = false;
     }
