@@ -799,7 +799,113 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
                    "rounds": sum(s["batches"] for s in st)}
         else:
             leg = {"rendered": st["rendered"], "dedup": st["dedup"], "rounds": st["batches"]}
+        # stats cover the warm-up pass too: rendered / dedup per served request, and the rate of
+        # distinct renders (what the GPU did) apart from requests answered by a sibling's render
+        passes = 2
+        leg["rendered_per_s"] = round(leg["rendered"] / passes / el, 1)
+        leg["dedup_share"] = round(leg["dedup"] / max(1, leg["rendered"] + leg["dedup"]), 3)
         res[name] = {"tiles_per_s": round(n_req / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3), **leg}
+    return res
+
+
+def _serve(b, submit_fns, clients):
+    """Run submit_fns (each a callable returning a ticket) from `clients` threads, 8 in flight per
+    client; returns (elapsed_s, per-request latencies)."""
+    import threading
+    lats = []
+
+    def client(k):
+        mine = submit_fns[k::clients]
+        for s0 in range(0, len(mine), 8):
+            a = time.perf_counter()
+            ts = [f() for f in mine[s0:s0 + 8]]
+            for t in ts:
+                b.wait(t)
+                lats.append(time.perf_counter() - a)
+    ths = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return time.perf_counter() - t0, lats
+
+
+def serving_projection_and_masks(torch, ctx, clients=8):
+    """Serving legs for the other two request kinds the batcher now takes:
+    - p=intmax|intmean requests (ImageRegionRequestHandler.java:506-558) on a C3-shaped image
+      (3 x 512x512x64 u16 ROMIO stacks, 2 timepoints), JPEG out: 64 requests, all distinct
+      (t x algorithm x z range), through the batcher with its HBM stack cache, then the same
+      requests again (the cache warm: settings / range changes on an open image) -- and with the
+      cache disabled (every request uploads its 96 MiB of stacks);
+    - render_shape_mask (ShapeMaskRequestHandler.java:165-207): 1024^2 masks of random ellipses,
+      colours and flips, 256 requests over 32 distinct masks, batched PNG vs one call at a time."""
+    import tempfile
+    import numpy as np
+    from omr import Batcher, PixelBuffer, _lib, write_romio
+    from omr.context import make_bindings, make_qdef
+    from omr.synthetic import c2_channels
+    res = {}
+    S, Z, C, T = 512, 64, 3, 2
+    rng = np.random.default_rng(33)
+    img = rng.integers(0, 65536, (T, C, Z, S, S), dtype=np.uint16)
+    d = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    fd, path = tempfile.mkstemp(prefix="omr_romio_z_", dir=d)
+    os.close(fd)
+    try:
+        write_romio(path, img, _lib.PIXELS_UINT16)
+        del img
+        pb = PixelBuffer(path, S, S, Z, C, T, _lib.PIXELS_UINT16)
+        qd, chans = make_qdef("rgb"), c2_channels(C)
+        binds = make_bindings(chans)
+        specs = [(t, p, z0) for t in range(T) for p in ("intmax", "intmean") for z0 in range(16)]   # 64 distinct
+        proj = {"requests": len(specs), "clients": clients, "stack_bytes_per_request": C * Z * S * S * 2}
+        for cache_mb, label in ((4096, "stack_cache"), (0, "no_stack_cache")):
+            with Batcher(ctx.device, max_batch=64, max_wait_us=1000) as b:
+                b.set_stack_cache(cache_mb << 20)
+                fns = [(lambda t=t, p=p, z0=z0: b.submit(pb, qd, chans, 0, t, 0, 0, S, S, quality=0.9, bindings=binds,
+                                                         projection=p, projection_start=z0, projection_end=Z - 1))
+                       for t, p, z0 in specs]
+                cold, _ = _serve(b, fns, clients)
+                warm, lats = _serve(b, fns, clients)
+                st, sc = b.stats(), b.stack_cache_stats()
+            proj[label] = {"cold_requests_per_s": round(len(specs) / cold, 1),
+                           "warm_requests_per_s": round(len(specs) / warm, 1),
+                           "warm_p50_ms": round(1e3 * float(np.median(lats)), 3),
+                           "rendered": st["rendered"], "dedup": st["dedup"], "stack_cache": sc}
+        res["projection"] = proj
+        pb.close()
+    finally:
+        os.unlink(path)
+    # shape masks
+    W = H = TILE
+    yy, xx = np.mgrid[0:H, 0:W]
+    masks = []
+    for k in range(32):
+        m = np.zeros((H, W), bool)
+        for _ in range(12):
+            cy, cx, ry, rx = rng.uniform(0, H), rng.uniform(0, W), rng.uniform(10, 150), rng.uniform(10, 150)
+            m |= ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1
+        masks.append((np.packbits(m.reshape(-1)).tobytes(), W, H,
+                      tuple(int(v) for v in rng.integers(0, 256, 4)), bool(k & 1), bool(k & 2)))
+    ctx.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)     # 1024-wide + flip: the pixel flip the reference intends
+    t0 = time.perf_counter()
+    for mk in masks:
+        ctx.render_shape_mask_png(*mk)
+    one = time.perf_counter() - t0
+    ctx.set_semantics(0)
+    n_req = 256
+    with Batcher(ctx.device, max_batch=64, max_wait_us=1000) as b:
+        b.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+        fns = [(lambda mk=masks[i % len(masks)]: b.submit_mask(*mk)) for i in range(n_req)]
+        _serve(b, fns, clients)
+        el, lats = _serve(b, fns, clients)
+        st = b.stats()
+    res["shape_mask"] = {"one_at_a_time_per_s": round(len(masks) / one, 1), "requests": n_req,
+                         "distinct_masks": len(masks), "batcher_requests_per_s": round(n_req / el, 1),
+                         "batcher_p50_ms": round(1e3 * float(np.median(lats)), 3),
+                         "rendered": st["rendered"], "dedup": st["dedup"],
+                         "rendered_per_s": round(st["rendered"] / 2 / el, 1)}
     return res
 
 
@@ -879,6 +985,7 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
         _lib.lib.omr_pinned_free(ctx.h, pin)
         res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid, pool_devices=pool_devices)
         pb.close()
+        res["serving"].update(serving_projection_and_masks(torch, ctx))
     finally:
         os.unlink(path)
     return res

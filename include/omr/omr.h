@@ -273,6 +273,11 @@ omr_status omr_batcher_stats(omr_batcher* b, uint64_t stats_out[4]);
 /* OMR_SEM_* flags for jobs submitted after this call (each job keeps the flags it was submitted
  * under; jobs with different flags never share a render). */
 omr_status omr_batcher_set_semantics(omr_batcher* b, uint32_t flags);
+/* HBM stack cache of the projection jobs: the (pixel buffer, c, t) Z-stacks stay resident (least
+ * recently used evicted) up to max_bytes (default 4 GiB, env OMR_STACK_CACHE_MB; 0 disables), so
+ * repeated p= requests on an image skip the PCIe upload.  stats: hits, misses, resident bytes. */
+omr_status omr_batcher_set_stack_cache(omr_batcher* b, int64_t max_bytes);
+omr_status omr_batcher_stack_cache_stats(omr_batcher* b, uint64_t stats_out[3]);
 
 /* ---- node-level serving pool: the request batches of all worker threads over the node's GPUs ---- */
 /*
@@ -296,6 +301,7 @@ omr_status omr_pool_wait(omr_pool* p, uint64_t ticket, uint8_t* out, size_t cap,
 /* Index into devices[] of the batcher a ticket went to (-1: not a ticket of this pool). */
 int32_t    omr_pool_device_index(const omr_pool* p, uint64_t ticket);
 omr_status omr_pool_set_semantics(omr_pool* p, uint32_t flags);
+omr_status omr_pool_set_stack_cache(omr_pool* p, int64_t max_bytes_per_device);
 /* stats_out[4*i .. 4*i+3] = omr_batcher_stats of device i; n_entries >= omr_pool_size. */
 omr_status omr_pool_stats(omr_pool* p, uint64_t* stats_out, int32_t n_entries);
 

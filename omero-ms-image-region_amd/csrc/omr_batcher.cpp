@@ -13,6 +13,7 @@
 #include "omr_internal.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <map>
@@ -68,8 +69,16 @@ struct omr_batcher {
     size_t argb_cap = 0;
     uint8_t* d_jpeg = nullptr;                   // encoded files of a group (JPEG / PNG batch output)
     size_t jpeg_cap = 0;
-    uint8_t* d_stack = nullptr;                  // projection jobs: the active channels' Z-stacks
+    uint8_t* d_stack = nullptr;                  // projection jobs: scratch for stacks the cache cannot hold
     size_t stack_cap = 0;
+    // HBM stack cache (projection jobs): (pixel buffer, c, t) Z-stacks kept resident, LRU, up to
+    // stack_cache_max bytes, so repeated p= requests on one image (other settings, ranges, flips)
+    // skip the PCIe upload the reference repeats per request (ImageRegionRequestHandler.java:516-533)
+    struct StackEntry { uint64_t serial; int32_t c, t; size_t bytes; uint8_t* d; uint64_t used; };
+    std::vector<StackEntry> stacks;
+    std::atomic<int64_t> stack_cache_max{(int64_t)4 << 30};
+    std::atomic<uint64_t> stack_hits{0}, stack_misses{0}, stack_resident{0};
+    uint64_t stack_tick = 0;
     uint64_t* d_offs = nullptr;
     uint32_t* d_lens = nullptr;
     int32_t* d_stat = nullptr;
@@ -245,6 +254,55 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
     return encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, out);
 }
 
+// The cache slot of stack (serial, c, t): *resident = true when it is already in HBM; otherwise a
+// buffer of `bytes` to upload into (least recently used stacks evicted, their memory reused when the
+// size matches), or nullptr when the stack does not fit the cache beside the request's other stacks.
+static uint8_t* stack_slot(omr_batcher* B, uint64_t serial, int32_t c, int32_t t, size_t bytes, uint64_t tick,
+                           bool* resident, omr_status* st) {
+    *resident = false;
+    for (auto& e : B->stacks)
+        if (e.serial == serial && e.c == c && e.t == t && e.bytes == bytes) {
+            e.used = tick;
+            *resident = true;
+            B->stack_hits++;
+            return e.d;
+        }
+    B->stack_misses++;
+    const int64_t cap = B->stack_cache_max.load();
+    uint8_t* reuse = nullptr;
+    size_t resident_bytes = B->stack_resident.load();
+    while (resident_bytes + bytes > (size_t)std::max<int64_t>(cap, 0)) {
+        int lru = -1;
+        for (int k = 0; k < (int)B->stacks.size(); ++k)
+            if (B->stacks[k].used != tick && (lru < 0 || B->stacks[k].used < B->stacks[lru].used)) lru = k;
+        if (lru < 0) break;                              // everything resident serves this request
+        const omr_batcher::StackEntry e = B->stacks[lru];
+        B->stacks.erase(B->stacks.begin() + lru);
+        resident_bytes -= e.bytes;
+        if (!reuse && e.bytes == bytes) {
+            reuse = e.d;
+        } else {
+            const hipError_t he = hipFree(e.d);
+            if (he != hipSuccess) { *st = hip_fail(B->ctx, he, "hipFree(stack cache)"); return nullptr; }
+        }
+    }
+    B->stack_resident = resident_bytes;
+    if (resident_bytes + bytes > (size_t)std::max<int64_t>(cap, 0)) {
+        if (reuse) (void)hipFree(reuse);
+        return nullptr;
+    }
+    if (!reuse) {
+        const hipError_t he = hipMalloc(reinterpret_cast<void**>(&reuse), bytes);
+        if (he != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;                              // HBM full: upload into the scratch instead
+        }
+    }
+    B->stacks.push_back({serial, c, t, bytes, reuse, tick});
+    B->stack_resident = resident_bytes + bytes;
+    return reuse;
+}
+
 // Projection jobs of one group (same image, settings, projection, flips, format): for each
 // distinct t the active channels' Z-stacks go to HBM (DMA from the registered ROMIO mapping),
 // omr_render_projected_device projects and renders the full plane (the glue,
@@ -265,22 +323,34 @@ static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& 
     for (int ch = 0; ch < SC; ++ch)
         if (j0.ch[ch].active) act.push_back(ch);
     const size_t stack_bytes = align_up(px * (size_t)bytes_per_pixel(PT) * Z, 256);
+    const uint64_t serial = pixel_buffer_serial(j0.pb);
     omr_status st = grow_dev(B, px * 4 * n, 0, n);
     if (st) return st;
-    if (stack_bytes * std::max<size_t>(1, act.size()) > B->stack_cap) {
-        B->stack_cap = 0;
-        if ((st = regrow(c, B->d_stack, stack_bytes * std::max<size_t>(1, act.size())))) return st;
-        B->stack_cap = stack_bytes * std::max<size_t>(1, act.size());
-    }
+    const size_t scratch_bytes = stack_bytes * std::max<size_t>(1, act.size());
+    auto scratch = [&](size_t a, uint8_t** d) -> omr_status {   // the uncached fallback, grown on first use
+        if (scratch_bytes > B->stack_cap) {
+            B->stack_cap = 0;
+            const omr_status s2 = regrow(c, B->d_stack, scratch_bytes);
+            if (s2) return s2;
+            B->stack_cap = scratch_bytes;
+        }
+        *d = B->d_stack + stack_bytes * a;
+        return OMR_OK;
+    };
     out.assign(n, Result{});
     const int start = j0.spec.projection_start >= 0 ? j0.spec.projection_start : 0;   // :510-515
     const int end = j0.spec.projection_end >= 0 ? j0.spec.projection_end : Z - 1;
     std::vector<const void*> stacks(SC, nullptr);
     for (int i = 0; i < n; ++i) {
         const int t = jobs[i]->spec.t;
+        const uint64_t tick = ++B->stack_tick;
         for (size_t a = 0; a < act.size() && !st; ++a) {
-            stacks[act[a]] = B->d_stack + stack_bytes * a;
-            st = pixel_buffer_upload_stack(c, j0.pb, act[a], t, B->d_stack + stack_bytes * a);
+            bool resident = false;
+            uint8_t* d = stack_slot(B, serial, act[a], t, stack_bytes, tick, &resident, &st);
+            if (st) break;
+            if (!d && (st = scratch(a, &d))) break;              // larger than the cache: scratch
+            stacks[act[a]] = d;
+            if (!resident) st = pixel_buffer_upload_stack(c, j0.pb, act[a], t, d);
         }
         if (!st)
             st = omr_render_projected_device(c, &j0.qdef, j0.ch.data(), SC, stacks.data(), PT, 1, W, H, Z,
@@ -421,6 +491,7 @@ omr_status omr_batcher_create(int32_t device, int32_t max_batch, int32_t max_wai
         delete B;
         return st;
     }
+    if (const char* v = std::getenv("OMR_STACK_CACHE_MB")) B->stack_cache_max = (int64_t)std::atoll(v) << 20;
     B->th = std::thread(dispatch_loop, B);
     *out = B;
     return OMR_OK;
@@ -435,6 +506,7 @@ void omr_batcher_destroy(omr_batcher* B) {
     B->cv_in.notify_all();
     if (B->th.joinable()) B->th.join();
     (void)hipSetDevice(B->device);
+    for (auto& e : B->stacks) (void)hipFree(e.d);
     for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat,
                     (void*)B->d_rstat, (void*)B->d_stack})
         if (p) (void)hipFree(p);
@@ -522,6 +594,20 @@ omr_status omr_batcher_set_semantics(omr_batcher* B, uint32_t flags) {
     // (run_group), so this never touches the context another thread is rendering with
     std::lock_guard<std::mutex> g(B->m);
     B->sem = flags;
+    return OMR_OK;
+}
+
+omr_status omr_batcher_set_stack_cache(omr_batcher* B, int64_t max_bytes) {
+    if (!B || max_bytes < 0) return OMR_INVALID_ARGUMENT;
+    B->stack_cache_max = max_bytes;      // the dispatcher evicts down to it on its next projection job
+    return OMR_OK;
+}
+
+omr_status omr_batcher_stack_cache_stats(omr_batcher* B, uint64_t stats_out[3]) {
+    if (!B || !stats_out) return OMR_INVALID_ARGUMENT;
+    stats_out[0] = B->stack_hits.load();
+    stats_out[1] = B->stack_misses.load();
+    stats_out[2] = B->stack_resident.load();
     return OMR_OK;
 }
 
@@ -631,6 +717,15 @@ omr_status omr_pool_set_semantics(omr_pool* P, uint32_t flags) {
     if (flags & ~(uint32_t)OMR_SEM_ALL) return OMR_INVALID_ARGUMENT;
     for (omr_batcher* b : P->b) {
         const omr_status st = omr_batcher_set_semantics(b, flags);
+        if (st) return st;
+    }
+    return OMR_OK;
+}
+
+omr_status omr_pool_set_stack_cache(omr_pool* P, int64_t max_bytes_per_device) {
+    if (!P) return OMR_INVALID_ARGUMENT;
+    for (omr_batcher* b : P->b) {
+        const omr_status st = omr_batcher_set_stack_cache(b, max_bytes_per_device);
         if (st) return st;
     }
     return OMR_OK;

@@ -192,6 +192,8 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
 
 // dims = {sizeX, sizeY, sizeZ, sizeC, sizeT, pixelType} of an open pixel buffer (omr_pixbuf.cpp).
 void pixel_buffer_dims(const omr_pixel_buffer* pb, int32_t dims[6]);
+// Process-unique id of an open pixel buffer (cache keys outlive a buffer's address).
+uint64_t pixel_buffer_serial(const omr_pixel_buffer* pb);
 // The (c, t) Z-stack of a pixel buffer into device memory on ctx's stream (omr_pixbuf.cpp).
 omr_status pixel_buffer_upload_stack(omr_ctx* ctx, const omr_pixel_buffer* pb, int32_t c, int32_t t, void* d_dst);
 

@@ -40,7 +40,10 @@ struct omr_pixel_buffer {
     const uint8_t* map = nullptr;
     std::mutex reg_m;
     int reg_state = 0;   // 0 untried, 1 registered, -1 not registrable (pread/memcpy path)
+    uint64_t serial = 0; // process-unique id (a closed buffer's address may be reused by the next open)
 };
+
+static std::atomic<uint64_t> g_pixbuf_serial{0};
 
 namespace omr {
 
@@ -276,6 +279,7 @@ omr_status omr_pixel_buffer_open(const char* path, int32_t size_x, int32_t size_
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return OMR_NOT_FOUND;
     auto* pb = new omr_pixel_buffer;
+    pb->serial = ++g_pixbuf_serial;
     pb->fd = fd;
     pb->sx = size_x; pb->sy = size_y; pb->sz = size_z; pb->sc = size_c; pb->st = size_t_;
     pb->pt = pixel_type;
@@ -458,6 +462,8 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
 void pixel_buffer_dims(const omr_pixel_buffer* pb, int32_t dims[6]) {
     dims[0] = pb->sx; dims[1] = pb->sy; dims[2] = pb->sz; dims[3] = pb->sc; dims[4] = pb->st; dims[5] = pb->pt;
 }
+
+uint64_t pixel_buffer_serial(const omr_pixel_buffer* pb) { return pb->serial; }
 
 // The whole Z-stack of (c, t) -- sizeZ planes, contiguous in the ROMIO layout -- into device memory
 // at d_dst, on ctx's stream: a DMA from the registered mapping, else pread into pinned staging

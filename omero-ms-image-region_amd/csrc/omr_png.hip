@@ -330,183 +330,216 @@ __device__ __forceinline__ uint32_t paeth(uint32_t a, uint32_t b, uint32_t c) {
     return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
 }
 
-// LDS of D1 for a row of rb = rowlen - 1 bytes: this row and the row above, each behind 4 zero
-// bytes (the left neighbours of the first pixel are 0) and padded to whole dwords, plus the output
-// row (filter byte + residuals) placed at the global row's address mod 4, so it leaves with aligned
-// dword stores.  Rows whose three buffers exceed the LDS budget write the residuals as bytes.
+// D1 works on kPngRowsPerWg consecutive rows per workgroup (the row above each is the previous
+// row's, still in LDS: H + H / 4 row loads instead of 2 H).  LDS per workgroup, for rows of
+// rb = rowlen - 1 bytes: two row buffers (this row, the row above) and, when they fit, the five
+// candidate residual rows, each of stride align4(rb) + 4 behind 4 bytes of zeros (the left
+// neighbours of the first pixel are 0; the stash rows keep the filter byte there).
+constexpr int kPngRowsPerWg = 4;
 __host__ __device__ constexpr int64_t png_row_stride(int64_t rb) { return ((rb + 3) & ~(int64_t)3) + 4; }
-__host__ __device__ constexpr int64_t png_filter_lds_in(int64_t rb) { return 2 * png_row_stride(rb); }
-__host__ __device__ constexpr int64_t png_filter_lds_out(int64_t rb) { return ((rb + 1 + 3 + 3) & ~(int64_t)3) + 16; }
 constexpr int64_t kPngFilterLdsMax = 150 * 1024;
-__host__ __device__ constexpr bool png_filter_stage_out(int64_t rb) {
-    return png_filter_lds_in(rb) + png_filter_lds_out(rb) <= kPngFilterLdsMax;
-}
+__host__ __device__ constexpr bool png_filter_stash(int64_t rb) { return 7 * png_row_stride(rb) <= kPngFilterLdsMax; }
 __host__ __device__ constexpr int64_t png_filter_lds(int64_t rb) {
-    return png_filter_lds_in(rb) + (png_filter_stage_out(rb) ? png_filter_lds_out(rb) : 0);
+    return (png_filter_stash(rb) ? 7 : 2) * png_row_stride(rb);
 }
 
 __device__ __forceinline__ uint32_t byte_at(uint32_t w, int k) { return (w >> (8 * k)) & 0xFF; }
 
-// The five PNG filter residuals of 4 row bytes (dword X of this row, B of the row above; A / C the
-// same bytes bpp to the left), mod 256, byte k of r[f].
+// Bytewise x - y mod 256 of four packed bytes (SWAR).
+__device__ __forceinline__ uint32_t sub8(uint32_t x, uint32_t y) {
+    return ((x | 0x80808080u) - (y & 0x7F7F7F7Fu)) ^ ((x ^ ~y) & 0x80808080u);
+}
+
+// The five PNG filter residuals of 4 row bytes: dword X of this row, B of the row above, A / C the
+// same bytes bpp to the left.  None / Sub / Up / Average in SWAR, Paeth per byte.
 __device__ __forceinline__ void png_residuals(uint32_t X, uint32_t A, uint32_t B, uint32_t C, uint32_t (&r)[5]) {
-#pragma unroll
-    for (int f = 0; f < 5; ++f) r[f] = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t x = byte_at(X, k), a = byte_at(A, k), b = byte_at(B, k), c = byte_at(C, k);
-        r[0] |= x << (8 * k);
-        r[1] |= ((x - a) & 0xFF) << (8 * k);
-        r[2] |= ((x - b) & 0xFF) << (8 * k);
-        r[3] |= ((x - ((a + b) >> 1)) & 0xFF) << (8 * k);
-        r[4] |= ((x - paeth(a, b, c)) & 0xFF) << (8 * k);
-    }
-}
-
-// |signed residual| summed over the bytes of w below `valid` (libpng's minimum-sum heuristic).
-__device__ __forceinline__ uint32_t png_abs_sum(uint32_t w, int valid) {
-    uint32_t s = 0;
+    r[0] = X;
+    r[1] = sub8(X, A);
+    r[2] = sub8(X, B);
+    r[3] = sub8(X, (A & B) + (((A ^ B) & 0xFEFEFEFEu) >> 1));    // floor((a + b) / 2) per byte
+    uint32_t P = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint32_t v = byte_at(w, k);
-        s += k < valid ? min(v, 256u - v) : 0u;
+        const int a = (int)byte_at(A, k), b = (int)byte_at(B, k), c = (int)byte_at(C, k);
+        const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
+        const int pr = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+        P |= (uint32_t)pr << (8 * k);
     }
-    return s;
+    r[4] = sub8(X, P);
 }
 
-// One workgroup, row y of image A: the filter byte + filtered row at flt + y * rowlen, the row's
-// Adler partials at rs[0..1].  Four row bytes per lane step: dword LDS reads, the left neighbours
-// by one alignbyte of two dwords.
-__device__ void png_filter_row(const PngArgs& A, int bpp, int y, uint8_t* __restrict__ flt,
-                               unsigned long long* __restrict__ rs, uint8_t* s_rows) {
+// Sum over the 4 bytes of |(int8) byte| (libpng's minimum-sum heuristic): |(r ^ 0x80) - 0x80| per
+// byte, one v_sad_u8.
+__device__ __forceinline__ uint32_t abs_sum8(uint32_t r, uint32_t acc) {
+    return __builtin_amdgcn_sad_u8(r ^ 0x80808080u, 0x80808080u, acc);
+}
+
+// Row yy of image A into the LDS row buffer `row` (rb bytes, zero tail to the dword; yy < 0: zeros).
+__device__ __forceinline__ void png_load_row(const PngArgs& A, int yy, int rb, uint8_t* row) {
+    uint32_t* rw = reinterpret_cast<uint32_t*>(row);
+    const int nw = (rb + 3) >> 2;
+    if (yy < 0) {
+        for (int j = threadIdx.x; j < nw; j += 256) rw[j] = 0;
+        return;
+    }
+    if (A.kind == kRgb && (A.W & 3) == 0) {        // four pixels (one 16-byte load) -> three dwords
+        const uint4* src = reinterpret_cast<const uint4*>(A.argb + (int64_t)yy * A.W);
+        for (int q = threadIdx.x; q < (A.W >> 2); q += 256) {
+            const uint4 v = src[q];
+            rw[3 * q] = __builtin_amdgcn_perm(v.y, v.x, 0x06000102u);       // r0 g0 b0 r1
+            rw[3 * q + 1] = __builtin_amdgcn_perm(v.z, v.y, 0x05060001u);   // g1 b1 r2 g2
+            rw[3 * q + 2] = __builtin_amdgcn_perm(v.w, v.z, 0x04050600u);   // b2 r3 g3 b3
+        }
+        return;                                    // rb = 3 W: no tail
+    }
+    if (A.kind == kRgb) {
+        for (int px = threadIdx.x; px < A.W; px += 256) {
+            const uint32_t v = A.argb[(int64_t)yy * A.W + px];
+            row[3 * px] = (uint8_t)(v >> 16); row[3 * px + 1] = (uint8_t)(v >> 8); row[3 * px + 2] = (uint8_t)v;
+        }
+    } else {
+        for (int i = threadIdx.x; i < rb; i += 256) row[i] = (uint8_t)row_byte(A, yy, i);
+    }
+    for (int i = rb + threadIdx.x; i < 4 * nw; i += 256) row[i] = 0;
+}
+
+// D1: rows y0 .. y0 + nrows - 1 of image A, one workgroup: each row's filter byte + filtered bytes
+// at flt + y * rowlen, its Adler partials at rs[2 (y - y0)], rs[2 (y - y0) + 1].  Per row one pass
+// computes the five residual rows (4 bytes per lane step) with their |residual| sums and keeps them
+// in LDS; the row leaves from the chosen one with aligned dword stores (the partial first / last
+// dword, shared with the neighbouring rows, byte by byte).  Rows too wide for the stash recompute
+// the chosen filter and store bytes.
+__device__ void png_filter_rows(const PngArgs& A, int bpp, int y0, int nrows, uint8_t* __restrict__ flt,
+                                unsigned long long* __restrict__ rs, uint8_t* lds) {
     __shared__ uint32_t s_sum[5][4];
     __shared__ int s_f;
     __shared__ unsigned long long s_ad[2][4];
     const int rb = (int)A.rowlen - 1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int stride = (int)png_row_stride(rb);
-    uint8_t* cur = s_rows + 4;
-    uint8_t* prev = s_rows + 4 + stride;
-    const int nw = (rb + 3) >> 2;                  // row dwords
-    for (int k = threadIdx.x; k < 2 * stride / 4; k += 256)
-        reinterpret_cast<uint32_t*>(s_rows)[k] = 0;   // zero pads and dword tails
-    __syncthreads();
-    if (A.kind == kRgb) {                         // one ARGB load per pixel and row
-        for (int px = threadIdx.x; px < A.W; px += 256) {
-            const uint32_t v = A.argb[(int64_t)y * A.W + px];
-            cur[3 * px] = (uint8_t)(v >> 16); cur[3 * px + 1] = (uint8_t)(v >> 8); cur[3 * px + 2] = (uint8_t)v;
-            const uint32_t u = y > 0 ? A.argb[(int64_t)(y - 1) * A.W + px] : 0u;
-            prev[3 * px] = (uint8_t)(u >> 16); prev[3 * px + 1] = (uint8_t)(u >> 8); prev[3 * px + 2] = (uint8_t)u;
-        }
-    } else {
-        for (int i = threadIdx.x; i < rb; i += 256) {
-            cur[i] = (uint8_t)row_byte(A, y, i);
-            prev[i] = y > 0 ? (uint8_t)row_byte(A, y - 1, i) : (uint8_t)0;
-        }
-    }
-    __syncthreads();
-    const uint32_t* cw = reinterpret_cast<const uint32_t*>(cur);     // cw[-1] is the zero pad
-    const uint32_t* pw = reinterpret_cast<const uint32_t*>(prev);
-    const int lsh = 4 - bpp;                       // bytes i-bpp .. i-bpp+3 = alignbyte(w[i/4], w[i/4-1], 4-bpp)
-    auto load = [&](int j, uint32_t& X, uint32_t& Av, uint32_t& Bv, uint32_t& Cv) {
-        X = cw[j];
-        Bv = pw[j];
-        Av = __builtin_amdgcn_alignbyte(X, cw[j - 1], lsh);
-        Cv = __builtin_amdgcn_alignbyte(Bv, pw[j - 1], lsh);
-    };
-    uint32_t sm[5] = {0, 0, 0, 0, 0};
-    for (int j = threadIdx.x; j < nw; j += 256) {
-        uint32_t X, Av, Bv, Cv, r[5];
-        load(j, X, Av, Bv, Cv);
-        png_residuals(X, Av, Bv, Cv, r);
-        const int valid = min(4, rb - 4 * j);
+    const int nw = (rb + 3) >> 2;
+    const bool stash = png_filter_stash(rb);
+    uint8_t* rowbuf[2] = {lds + 4, lds + 4 + stride};
+    uint8_t* st0 = lds + 2 * stride + 4;           // stash row f at st0 + f * stride
+    for (int k = threadIdx.x; k < (stash ? 7 : 2); k += 256)
+        *reinterpret_cast<uint32_t*>(lds + k * stride) = 0;     // the pads
+    png_load_row(A, y0 - 1, rb, rowbuf[0]);
+    const int lsh = 4 - bpp;                       // bytes i-bpp .. i-bpp+3 = alignbyte(w[j], w[j-1], 4-bpp)
+    for (int r = 0; r < nrows; ++r) {
+        const int y = y0 + r;
+        uint8_t* cur = rowbuf[(r + 1) & 1];
+        const uint8_t* prev = rowbuf[r & 1];
+        png_load_row(A, y, rb, cur);
+        __syncthreads();
+        const uint32_t* cw = reinterpret_cast<const uint32_t*>(cur);    // cw[-1]: the zero pad
+        const uint32_t* pw = reinterpret_cast<const uint32_t*>(prev);
+        uint32_t sm[5] = {0, 0, 0, 0, 0};
+        for (int j = threadIdx.x; j < nw; j += 256) {
+            const uint32_t X = cw[j], Bv = pw[j];
+            const uint32_t Av = __builtin_amdgcn_alignbyte(X, cw[j - 1], lsh);
+            const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, pw[j - 1], lsh);
+            uint32_t rr[5];
+            png_residuals(X, Av, Bv, Cv, rr);
+            const int valid = rb - 4 * j;
+            const uint32_t vm = valid >= 4 ? 0xFFFFFFFFu : (1u << (8 * valid)) - 1u;
 #pragma unroll
-        for (int f = 0; f < 5; ++f) sm[f] += png_abs_sum(r[f], valid);
-    }
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        uint32_t v = sm[k];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (lane == 0) s_sum[k][wv] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t best = 0xFFFFFFFFu;
-        int bf = 0;
-        for (int k = 0; k < 5; ++k) {
-            const uint32_t v = s_sum[k][0] + s_sum[k][1] + s_sum[k][2] + s_sum[k][3];
-            if (v < best) { best = v; bf = k; }
-        }
-        s_f = bf;
-    }
-    __syncthreads();
-    const int f = s_f;
-    const int64_t row0 = (int64_t)y * A.rowlen;
-    // Adler partials in 32 bits per lane: s1 = sum v, s2 = sum (raw - idx) v = (raw - row0 - 1) * sum v
-    // - sum i v over the row's bytes i (idx = row0 + 1 + i); a lane's sum i v stays below 2^32
-    uint32_t sv = 0, siv = 0;
-    const bool staged = png_filter_stage_out(rb);
-    const int o0 = (int)(row0 & 3);                // the output row's first byte, at its address mod 4
-    uint8_t* ob = s_rows + png_filter_lds_in(rb);
-    for (int j = threadIdx.x; j < nw; j += 256) {
-        uint32_t X, Av, Bv, Cv, r[5];
-        load(j, X, Av, Bv, Cv);
-        png_residuals(X, Av, Bv, Cv, r);
-        const uint32_t w = r[f];
-        const int valid = min(4, rb - 4 * j);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < valid) {
-                const uint32_t v = byte_at(w, k);
-                sv += v;
-                siv += (uint32_t)(4 * j + k) * v;
-                if (staged) ob[o0 + 1 + 4 * j + k] = (uint8_t)v;
-                else flt[row0 + 1 + 4 * j + k] = (uint8_t)v;
+            for (int f = 0; f < 5; ++f) {
+                sm[f] = abs_sum8(rr[f] & vm, sm[f]);
+                if (stash) reinterpret_cast<uint32_t*>(st0 + f * stride)[j] = rr[f];
             }
         }
-    }
-    unsigned long long s1 = sv;
-    unsigned long long s2 = (unsigned long long)(A.raw - row0 - 1) * sv - siv;
-    if (threadIdx.x == 0) {                        // the filter-type byte
-        s1 += (unsigned long long)f;
-        s2 += (unsigned long long)(A.raw - row0) * (unsigned long long)f;
-        if (staged) ob[o0] = (uint8_t)f;
-        else flt[row0] = (uint8_t)f;
-    }
-    if (staged) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t v = sm[k];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) s_sum[k][wv] = v;
+        }
         __syncthreads();
-        // [row0, row0 + rowlen) out: interior dwords stored whole, the partial first / last dword
-        // (shared with the neighbouring rows' workgroups) byte by byte
-        const int64_t g0 = row0 >> 2, g1 = (row0 + A.rowlen - 1) >> 2;
-        uint32_t* gw = reinterpret_cast<uint32_t*>(flt);
-        const uint32_t* lw = reinterpret_cast<const uint32_t*>(ob);
-        for (int64_t g = g0 + threadIdx.x; g <= g1; g += 256) {
-            const int64_t b0 = g * 4;
-            if (b0 >= row0 && b0 + 4 <= row0 + A.rowlen) {
-                gw[g] = lw[g - g0];
-            } else {
-                for (int k = 0; k < 4; ++k) {
-                    const int64_t bi = b0 + k;
-                    if (bi >= row0 && bi < row0 + A.rowlen) flt[bi] = ob[bi - row0 + o0];
+        if (threadIdx.x == 0) {
+            uint32_t best = 0xFFFFFFFFu;
+            int bf = 0;
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t v = s_sum[k][0] + s_sum[k][1] + s_sum[k][2] + s_sum[k][3];
+                if (v < best) { best = v; bf = k; }
+            }
+            s_f = bf;
+            if (stash) st0[bf * stride - 1] = (uint8_t)bf;   // v[0] = the filter byte, v[j] = residual j-1
+        }
+        __syncthreads();
+        const int f = s_f;
+        const int64_t row0 = (int64_t)y * A.rowlen;
+        unsigned long long s1 = 0, s2 = 0;
+        if (stash) {
+            // global dwords [row0 / 4, (row0 + rowlen - 1) / 4]: v[jj] (jj = byte - row0) read from the
+            // stash row as an unaligned dword (two aligned reads + alignbyte)
+            const uint8_t* vrow = st0 + f * stride - 1;           // v[jj] = vrow[jj]
+            const int64_t g0 = row0 >> 2, g1 = (row0 + A.rowlen - 1) >> 2;
+            const uint32_t* vw = reinterpret_cast<const uint32_t*>(st0 + f * stride - 4);   // aligned, vw[0] = pad
+            uint32_t* gw = reinterpret_cast<uint32_t*>(flt);
+            for (int64_t g = g0 + threadIdx.x; g <= g1; g += 256) {
+                const int64_t jj = 4 * g - row0;                  // v index of the dword's first byte
+                if (jj >= 0 && jj + 4 <= A.rowlen) {
+                    // st0[jj - 1 .. jj + 2] = bytes 4 + jj - 1 .. of vw
+                    const int64_t q = jj + 3;                     // byte offset from vw[0]
+                    const uint32_t w = __builtin_amdgcn_alignbyte(vw[(q >> 2) + 1], vw[q >> 2], (uint32_t)(q & 3));
+                    gw[g] = w;
+                    const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
+                    s1 += sv;
+                    s2 += (unsigned long long)(A.raw - row0 - jj) * sv - __builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
+                } else {
+                    for (int k = 0; k < 4; ++k) {
+                        const int64_t t = jj + k;
+                        if (t >= 0 && t < A.rowlen) {
+                            const uint32_t v = vrow[t];
+                            flt[row0 + t] = (uint8_t)v;
+                            s1 += v;
+                            s2 += (unsigned long long)(A.raw - row0 - t) * v;
+                        }
+                    }
                 }
             }
+        } else {
+            for (int j = threadIdx.x; j < nw; j += 256) {
+                const uint32_t X = cw[j], Bv = pw[j];
+                const uint32_t Av = __builtin_amdgcn_alignbyte(X, cw[j - 1], lsh);
+                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, pw[j - 1], lsh);
+                uint32_t rr[5];
+                png_residuals(X, Av, Bv, Cv, rr);
+                const uint32_t w = rr[f];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int i = 4 * j + k;
+                    if (i < rb) {
+                        const uint32_t v = byte_at(w, k);
+                        flt[row0 + 1 + i] = (uint8_t)v;
+                        s1 += v;
+                        s2 += (unsigned long long)(A.raw - row0 - 1 - i) * v;
+                    }
+                }
+            }
+            if (threadIdx.x == 0) {
+                flt[row0] = (uint8_t)f;
+                s1 += (unsigned long long)f;
+                s2 += (unsigned long long)(A.raw - row0) * (unsigned long long)f;
+            }
         }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_down(s1, o, 64);
-        s2 += __shfl_down(s2, o, 64);
-    }
-    if (lane == 0) { s_ad[0][wv] = s1; s_ad[1][wv] = s2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {      // per-row Adler partials; summed by k_png_adler_rows
-        rs[0] = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
-        rs[1] = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
+        for (int o = 32; o > 0; o >>= 1) {
+            s1 += __shfl_down(s1, o, 64);
+            s2 += __shfl_down(s2, o, 64);
+        }
+        if (lane == 0) { s_ad[0][wv] = s1; s_ad[1][wv] = s2; }
+        __syncthreads();                             // also: the stash / row buffers are free again
+        if (threadIdx.x == 0) {                      // per-row Adler partials
+            rs[2 * r] = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
+            rs[2 * r + 1] = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
+        }
     }
 }
 
 __global__ void __launch_bounds__(256) k_png_filter(DflArgs D) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
-    png_filter_row(D.P, D.bpp, blockIdx.x, D.flt, D.row_sums + 2 * blockIdx.x, s_rows);
+    const int y0 = blockIdx.x * kPngRowsPerWg;
+    png_filter_rows(D.P, D.bpp, y0, min(kPngRowsPerWg, D.P.H - y0), D.flt, D.row_sums + 2 * y0, s_rows);
 }
 
 // Sum of the per-row Adler partials into A.sums (one workgroup; both encodings carry flt).
@@ -1311,13 +1344,14 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
     OMR_HIP(ctx, hipMemsetAsync(ws + L.crc, 0, 4, ctx->stream));
     OMR_HIP(ctx, hipMemsetAsync(ws + L.lhist, 0, L.dhist + 30 * 4 - L.lhist, ctx->stream));
     const unsigned gseg = (unsigned)((L.nseg + 255) / 256);
-    const size_t rows_lds = align_up((size_t)png_filter_lds(P.rowlen - 1), 16);
-    if (rows_lds > (size_t)kPngFilterLdsMax) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG row too wide");
+    const size_t rows_lds = align_up((size_t)png_filter_lds(P.rowlen - 1) + 16, 16);   // + the last stash read
+    if (rows_lds > (size_t)kPngFilterLdsMax + 64) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG row too wide");
     if (P.chunk_bytes >= ((int64_t)1 << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "PNG image too large");
     if (rows_lds > (size_t)60 * 1024)
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_png_filter),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds + 1024));
-    hipLaunchKernelGGL(k_png_filter, dim3((unsigned)H), dim3(256), rows_lds, ctx->stream, D);
+    hipLaunchKernelGGL(k_png_filter, dim3((unsigned)((H + kPngRowsPerWg - 1) / kPngRowsPerWg)), dim3(256), rows_lds,
+                       ctx->stream, D);
     const int32_t back = (int32_t)align_up((size_t)std::min<int64_t>(std::max<int64_t>(P.rowlen, 2 * D.bpp), kMaxBack), 16);
     hipLaunchKernelGGL(k_png_lz_parse, dim3((unsigned)((L.nseg + kParseLanes - 1) / kParseLanes)), dim3(kParseLanes),
                        (size_t)back + (size_t)kParseLanes * kSeg, ctx->stream, D, back);
@@ -1418,6 +1452,7 @@ struct PngImg {
     const uint8_t* bits;       // kIdx1 / kIdx8: MSB-first mask bits
     int32_t kind, W, H, flip_h, flip_v, bpp;
     int32_t row0, pblk0, grp0, pre_len;         // first global row / parse block / group; prefix bytes
+    int32_t rblk0, pad2;                        // first D1 workgroup (kPngRowsPerWg rows each)
     int32_t back, pad;                          // parse look-back (bytes, multiple of 16)
     int64_t rowlen, raw, nseg, nblk;            // row bytes + 1, filtered stream bytes, segments, stored blocks
     int64_t flt, seg0, words;                   // filtered stream offset (bytes), first segment, first word
@@ -1435,9 +1470,9 @@ struct PngMeta {
 struct PngBatch {
     const PngImg* img;
     int32_t n, uniform;                         // uniform: every image has the same geometry
-    int32_t rows_per, pblk_per, grp_per, eblk_per, cblk_per;   // per-image counts when uniform
+    int32_t rblk_per, pblk_per, grp_per, eblk_per, cblk_per;   // per-image counts when uniform
     int32_t total_grp, pad;
-    const int32_t* row0;                        // [n] first global row etc. (binary search when not uniform)
+    const int32_t* rblk0;                       // [n] first D1 workgroup etc. (binary search when not uniform)
     const int32_t* pblk0;
     const int32_t* grp0;
     const int32_t* eblk0;
@@ -1497,10 +1532,11 @@ __global__ void __launch_bounds__(256) k_png_crc_pow(uint32_t* __restrict__ pw) 
 
 __global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_rows[];
-    const int i = pngb_image(B, B.row0, B.rows_per, blockIdx.x);
+    const int i = pngb_image(B, B.rblk0, B.rblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
-    const int y = (int)blockIdx.x - (B.uniform ? i * B.rows_per : I.row0);
-    png_filter_row(pngb_args(I), I.bpp, y, B.flt + I.flt, B.row_sums + 2 * (int64_t)blockIdx.x, s_rows);
+    const int y0 = ((int)blockIdx.x - (B.uniform ? i * B.rblk_per : I.rblk0)) * kPngRowsPerWg;
+    png_filter_rows(pngb_args(I), I.bpp, y0, min(kPngRowsPerWg, I.H - y0), B.flt + I.flt,
+                    B.row_sums + 2 * ((int64_t)I.row0 + y0), s_rows);
 }
 
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
@@ -1907,7 +1943,7 @@ static omr_status ensure_crc_pow(Ctx* ctx) {
 struct PngBatchPlan {
     std::vector<PngImg> I;
     std::vector<int32_t> firsts;
-    int64_t rows = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
+    int64_t rows = 0, rblk = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
     size_t rows_lds = 16, parse_lds = 16;
     bool uniform = true;
     size_t o_img, o_first, o_flt, o_tok, o_ntok, o_segb, o_gsum, o_goff, o_hist, o_tab, o_meta, o_rows, o_words;
@@ -1941,6 +1977,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
             L.eblk + ne > INT32_MAX || L.cblk + nc > INT32_MAX)
             return fail(ctx, OMR_INVALID_ARGUMENT, "PNG batch too large");
         d.row0 = (int32_t)L.rows;
+        d.rblk0 = (int32_t)L.rblk;
         d.pblk0 = (int32_t)L.pblk;
         d.grp0 = (int32_t)L.grp;
         d.eblk0 = L.eblk;
@@ -1949,12 +1986,13 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         d.tok0 = L.toks;
         d.flt = L.flt;
         d.words = L.words;
-        L.firsts[i] = d.row0;
+        L.firsts[i] = d.rblk0;
         L.firsts[n + i] = d.pblk0;
         L.firsts[2 * (size_t)n + i] = d.grp0;
         L.firsts[3 * (size_t)n + i] = (int32_t)d.eblk0;
         L.firsts[4 * (size_t)n + i] = (int32_t)d.cblk0;
         L.rows += h.H;
+        L.rblk += (h.H + kPngRowsPerWg - 1) / kPngRowsPerWg;
         L.pblk += npb;
         L.grp += ng;
         L.eblk += ne;
@@ -1963,7 +2001,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         L.toks += tok_slots(d.nseg);
         L.flt += (int64_t)align_up((size_t)P.raw, 16);
         L.words += (int64_t)align_up((size_t)(P.raw / 2 + 128), 4);     // <= 16 bits per byte + header
-        L.rows_lds = std::max(L.rows_lds, align_up((size_t)png_filter_lds(P.rowlen - 1), 16));
+        L.rows_lds = std::max(L.rows_lds, align_up((size_t)png_filter_lds(P.rowlen - 1) + 16, 16));
         L.parse_lds = std::max(L.parse_lds, (size_t)d.back + (size_t)kParseLanes * kSeg);
         if (i && (h.kind != im[0].kind || h.W != im[0].W || h.H != im[0].H)) L.uniform = false;
     }
@@ -2000,7 +2038,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     }
     std::vector<PngImg>& I = L.I;
     std::vector<int32_t>& firsts = L.firsts;
-    const int64_t rows = L.rows, pblk = L.pblk, grp = L.grp, eblk = L.eblk, cblk = L.cblk;
+    const int64_t pblk = L.pblk, grp = L.grp, eblk = L.eblk, cblk = L.cblk;
     const size_t rows_lds = L.rows_lds, parse_lds = L.parse_lds;
     const bool uniform = L.uniform;
     auto at = [&](size_t rel) { return ws_off + rel; };
@@ -2013,14 +2051,14 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     Bt.img = reinterpret_cast<const PngImg*>(ws + o_img);
     Bt.n = n;
     Bt.uniform = uniform ? 1 : 0;
-    Bt.rows_per = im[0].H;
+    Bt.rblk_per = (im[0].H + kPngRowsPerWg - 1) / kPngRowsPerWg;
     Bt.pblk_per = n > 1 ? I[1].pblk0 : (int32_t)pblk;
     Bt.grp_per = n > 1 ? I[1].grp0 : (int32_t)grp;
     Bt.eblk_per = n > 1 ? (int32_t)I[1].eblk0 : (int32_t)eblk;
     Bt.cblk_per = n > 1 ? (int32_t)I[1].cblk0 : (int32_t)cblk;
     Bt.total_grp = (int32_t)grp;
     const int32_t* fd = reinterpret_cast<const int32_t*>(ws + o_first);
-    Bt.row0 = fd;
+    Bt.rblk0 = fd;
     Bt.pblk0 = fd + n;
     Bt.grp0 = fd + 2 * (size_t)n;
     Bt.eblk0 = fd + 3 * (size_t)n;
@@ -2053,7 +2091,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_parse),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds + 2048));
     hipStream_t s = ctx->stream;
-    hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)rows), dim3(256), rows_lds, s, Bt);
+    hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
     hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
     hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
     hipLaunchKernelGGL(k_pngb_bits, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);

@@ -159,6 +159,9 @@ _SIGS = {
     "omr_batcher_wait": (_i32, [_vp, ctypes.c_uint64, _vp, _sz, ctypes.POINTER(_sz)]),
     "omr_batcher_stats": (_i32, [_vp, _vp]),
     "omr_batcher_set_semantics": (_i32, [_vp, ctypes.c_uint32]),
+    "omr_batcher_set_stack_cache": (_i32, [_vp, _i64]),
+    "omr_batcher_stack_cache_stats": (_i32, [_vp, _vp]),
+    "omr_pool_set_stack_cache": (_i32, [_vp, _i64]),
     "omr_pool_create": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
     "omr_pool_destroy": (None, [_vp]),
     "omr_pool_size": (_i32, [_vp]),

@@ -114,6 +114,15 @@ class Batcher(_Queue):
         _lib.check(lib.omr_batcher_stats(self.h, s))
         return {"jobs": s[0], "batches": s[1], "rendered": s[2], "dedup": s[3]}
 
+    def set_stack_cache(self, max_bytes):
+        """HBM cache of the projection jobs' Z-stacks (0 disables)."""
+        _lib.check(lib.omr_batcher_set_stack_cache(self.h, int(max_bytes)))
+
+    def stack_cache_stats(self):
+        s = (ctypes.c_uint64 * 3)()
+        _lib.check(lib.omr_batcher_stack_cache_stats(self.h, s))
+        return {"hits": s[0], "misses": s[1], "resident_bytes": s[2]}
+
 
 class Pool(_Queue):
     _submit = lib.omr_pool_submit
@@ -133,6 +142,9 @@ class Pool(_Queue):
 
     def device_index(self, ticket):
         return lib.omr_pool_device_index(self.h, ticket)
+
+    def set_stack_cache(self, max_bytes_per_device):
+        _lib.check(lib.omr_pool_set_stack_cache(self.h, int(max_bytes_per_device)))
 
     def stats(self):
         n = len(self.devices)

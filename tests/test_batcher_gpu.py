@@ -473,3 +473,35 @@ def test_mask_jobs_dedup_and_404(ctx):
         assert res[0] == ctx.render_shape_mask_png(bits, 16, 16, (255, 0, 0, 255))
     finally:
         ctx.set_semantics(0)
+
+
+def test_projection_stack_cache(romio_stack):
+    """The HBM stack cache: a repeated projection (other algorithm / range / flips) on the same t hits
+    the resident stacks, a tiny cache evicts and re-uploads, a disabled cache uploads every time --
+    every result equal to the CPU restatement."""
+    path, px = romio_stack
+    pb = PixelBuffer(path, PX_, PY_, PZ_, PC_, PT_, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    stack_bytes = PX_ * PY_ * PZ_ * 2
+    runs = [("intmax", 0, -1, -1, False), ("intmean", 0, 1, 4, True), ("intmax", 1, -1, -1, False),
+            ("intsum", 0, 0, 5, False)]
+    algs = {"intmax": _lib.PROJECTION_MAX, "intmean": _lib.PROJECTION_MEAN, "intsum": _lib.PROJECTION_SUM}
+    for cap, expect_hits in [(1 << 30, True), (stack_bytes * 3, True), (stack_bytes, True), (0, False)]:
+        with Batcher(0, max_batch=8, max_wait_us=100) as b:
+            b.set_stack_cache(cap)
+            for p, t, s, e, fh in runs:                                  # one job per round
+                got = b.wait(b.submit(pb, O.make_qdef("rgb"), ch, 0, t, 0, 0, 16, 16, flip_h=fh, fmt="argb",
+                                      projection=p, projection_start=s, projection_end=e))
+                stt, exp = _oracle_projected(px, ch, "rgb", t, algs[p], 0 if s < 0 else s, PZ_ - 1 if e < 0 else e,
+                                             fh)
+                np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(PY_, PX_), exp)
+            st = b.stack_cache_stats()
+        assert (st["hits"] > 0) == expect_hits, (cap, st)
+        assert st["resident_bytes"] <= cap
+        if cap == 1 << 30:
+            assert st["hits"] == 2 * 3 and st["misses"] == 2 * 3, st    # t=0 and t=1 uploaded once each
+        elif cap == stack_bytes * 3:
+            assert st["hits"] == 3 and st["misses"] == 9, st            # t=1 evicted t=0
+    with Batcher(0) as b, pytest.raises(_lib.OmrError):
+        b.set_stack_cache(-1)
+    pb.close()
