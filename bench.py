@@ -295,6 +295,10 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
         }
         vr = jpeg_valu_roofline(name, mcus, avg.get(5), avg_f.get(5), avg.get(6))
         if vr:
+            if name.startswith("c2") and B == 256:
+                mt = jpeg_measured_traffic(B * tstride + int(ln.sum()))
+                if mt:
+                    vr["measured_traffic"] = mt
             res[name]["valu_roofline"] = vr
         if with_cpu:
             try:
@@ -314,6 +318,31 @@ VALU_PEAK_ISSUE_CYCLES_PER_S = 256 * 4 * 2.4e9   # 1,024 SIMD-32s at 2.4 GHz
 VALU_CYCLES = 2.0
 VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32")
+
+
+JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04b.json")
+JPEG_FUSED_KERNELS = ("k_jpeg_render_fdct", "k_jpeg_block_bits", "k_jpeg_group_scan", "k_jpeg_huff_thread",
+                      "k_jpeg_tile_scan", "k_jpeg_stuff_count", "k_jpeg_stuff_batch")
+
+
+def jpeg_measured_traffic(algo_bytes):
+    """HBM bytes per fused C2 -> JPEG call of 256 tiles from the committed PMC passes
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 x 1 KiB read, WRITE_SIZE x 1 KiB written, one counter per
+    pass), against this run's algorithmic bytes (planes in + JPEG files out)."""
+    try:
+        with open(JPEG_PMC) as fh:
+            ks = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    per = {}
+    for key in JPEG_FUSED_KERNELS:
+        k = next((k for k in ks if key in k["kernel"]), None)
+        if k is not None:
+            per[key] = {"read_mb": round(k["hbm_read_bytes"] / 1e6, 1), "write_mb": round(k["hbm_write_bytes"] / 1e6, 1)}
+    tot = sum(v["read_mb"] + v["write_mb"] for v in per.values()) * 1e6
+    return {"source": os.path.relpath(JPEG_PMC, os.path.dirname(os.path.abspath(__file__))), "per_kernel": per,
+            "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(algo_bytes / 1e6, 1),
+            "ratio": round(tot / algo_bytes, 3)}
 
 
 def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
@@ -966,8 +995,18 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
             "host_pageable_out": lambda: ctx.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
                                                                        out=pageable, bindings=binds),
             "to_jpeg_host": to_jpeg,
-            "device_out_staged": None,
+            # the fallback when the driver refuses to register the file mapping: reader threads
+            # memcpy rows into pinned slots (host-memcpy-bound on the box's CPU quota)
+            "device_out_staged_fallback": None,
         }
+        # the same device_out leg on a context whose pixel-buffer pipeline splits the tile copies
+        # over two DMA queues (OMR_PIXBUF_COPY_STREAMS=2, read when its pipeline is created)
+        import omr
+        os.environ["OMR_PIXBUF_COPY_STREAMS"] = "2"
+        ctx2 = omr.Context(ctx.device, torch_order=False)
+        del os.environ["OMR_PIXBUF_COPY_STREAMS"]
+        modes["device_out_2_copy_queues"] = lambda: ctx2.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
+                                                                                   out=dev_out, bindings=binds)
         for name, fn in modes.items():
             if fn is None:          # reader threads -> pinned staging instead of DMA from the mapping
                 _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 0)
@@ -983,11 +1022,40 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
             res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
         _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
         _lib.lib.omr_pinned_free(ctx.h, pin)
+        ctx2.close()
+        res["pcie_probe"] = pcie_probe(torch, uniq.device)
+        ceil = max(v["gbs"] for v in res["pcie_probe"].values() if isinstance(v, dict))
+        best = max(res["device_out"]["tiles_per_s"], res["device_out_2_copy_queues"]["tiles_per_s"])
+        res["device_out_h2d_gbs"] = round(best * res["pcie_bytes_per_tile_in"] / 1e9, 2)
+        res["device_out_vs_pcie_probe"] = round(res["device_out_h2d_gbs"] / ceil, 3)
         res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid, pool_devices=pool_devices)
         pb.close()
         res["serving"].update(serving_projection_and_masks(torch, ctx))
     finally:
         os.unlink(path)
+    return res
+
+
+def pcie_probe(torch, device, mib=512):
+    """The box's host -> HBM ceiling: pinned host memory copied to the device with hipMemcpyAsync
+    (torch's copy_) in one contiguous transfer, and split over two streams (two DMA queues), timed
+    with events after a warm-up copy.  The host-fed legs are judged against this."""
+    n = mib << 20
+    host = torch.empty(n, dtype=torch.uint8).pin_memory()
+    dev = torch.empty(n, dtype=torch.uint8, device=device)
+    res = {"bytes": n}
+    streams = [torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)]
+    for name, k in (("one_stream", 1), ("two_streams", 2)):
+        part = n // k
+        for rep in range(2):                          # warm, then timed
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(k):
+                with torch.cuda.stream(streams[i]):
+                    dev[i * part:(i + 1) * part].copy_(host[i * part:(i + 1) * part], non_blocking=True)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+        res[name] = {"gbs": round(n / el / 1e9, 2)}
     return res
 
 

@@ -123,6 +123,9 @@ struct Ctx {
     // [4096, 6144) j = hi * 4096; built on the device on first use (omr_png.hip)
     uint32_t* d_crc_pow = nullptr;
     bool f1_f32 = true;              // F1's Fast16 quantize in f32 when proven exact (OMR_F1_F32=0: f64)
+    // JPEG B4a / B6 grids: chunk groups for streams of this many bytes per pixel x 100 (longer
+    // streams loop; env OMR_JPEG_EST_CENTIBPP)
+    int jpeg_est_centibpp = 100;
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
     int k2_eval_cpt = -2;            // float / 32-bit K2: -1 / -2 pipelined chunks per lane, 2 / 4 plain

@@ -20,6 +20,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdlib>
 #include <cerrno>
 #include <condition_variable>
 #include <functional>
@@ -139,7 +140,9 @@ struct PixPipe {
     void* d_out[2] = {nullptr, nullptr};
     size_t in_cap = 0, out_cap = 0;
     hipEvent_t h2d[2] = {nullptr, nullptr}, rend[2] = {nullptr, nullptr}, d2h[2] = {nullptr, nullptr};
+    hipEvent_t h2d_b[2] = {nullptr, nullptr};   // the second copy stream's part of a slot
     hipStream_t copy = nullptr;
+    hipStream_t copy_b = nullptr;               // a second DMA queue (env OMR_PIXBUF_COPY_STREAMS=2)
     explicit PixPipe(int threads) : pool(threads) {}
     ~PixPipe() {
         if (copy) (void)hipStreamSynchronize(copy);
@@ -148,10 +151,12 @@ struct PixPipe {
             if (pin_out[i]) (void)hipHostFree(pin_out[i]);
             if (d_in[i]) (void)hipFree(d_in[i]);
             if (d_out[i]) (void)hipFree(d_out[i]);
-            for (hipEvent_t e : {h2d[i], rend[i], d2h[i]})
+            for (hipEvent_t e : {h2d[i], rend[i], d2h[i], h2d_b[i]})
                 if (e) (void)hipEventDestroy(e);
         }
+        if (copy_b) (void)hipStreamSynchronize(copy_b);
         if (copy) (void)hipStreamDestroy(copy);
+        if (copy_b) (void)hipStreamDestroy(copy_b);
     }
 };
 
@@ -164,8 +169,10 @@ static omr_status get_pipe(Ctx* c, PixPipe*& out) {
         c->pixbuf_state = p;
         c->pixbuf_state_free = free_pipe;
         OMR_HIP(c, hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking));
+        const char* ncs = std::getenv("OMR_PIXBUF_COPY_STREAMS");
+        if (ncs && std::atoi(ncs) >= 2) OMR_HIP(c, hipStreamCreateWithFlags(&p->copy_b, hipStreamNonBlocking));
         for (int i = 0; i < 2; ++i)
-            for (hipEvent_t* e : {&p->h2d[i], &p->rend[i], &p->d2h[i]})
+            for (hipEvent_t* e : {&p->h2d[i], &p->rend[i], &p->d2h[i], &p->h2d_b[i]})
                 OMR_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     out = static_cast<PixPipe*>(c->pixbuf_state);
@@ -411,6 +418,7 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
             if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
         }
         if (g >= 2) OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free
+        if (g >= 2 && P->copy_b) OMR_HIP(ctx, hipStreamWaitEvent(P->copy_b, P->rend[s], 0));
         if (direct) {
             // registered mapping: the copy engine reads each tile's rows from the page cache
             OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes, hipMemcpyHostToDevice, P->copy));
@@ -419,10 +427,12 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
                 for (int a = 0; a < (int)act.size(); ++a) {
                     const uint8_t* src = pb->map + plane_offset(pb, r.z, act[a], r.t) + (int64_t)r.y * pb->row_bytes +
                                          (int64_t)r.x * pb->bpp;
+                    // tile-channel planes alternate between the copy queues when there are two
+                    hipStream_t cs = (P->copy_b && ((i * na + a) & 1)) ? P->copy_b : P->copy;
                     OMR_HIP(ctx, hipMemcpy2DAsync(din + tab_bytes + plane_al * ((size_t)i * na + a),
                                                   (size_t)width * pb->bpp, src, (size_t)pb->row_bytes,
                                                   (size_t)width * pb->bpp, (size_t)height, hipMemcpyHostToDevice,
-                                                  P->copy));
+                                                  cs));
                 }
             }
         } else {
@@ -431,6 +441,10 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
         }
         OMR_HIP(ctx, hipEventRecord(P->h2d[s], P->copy));
         OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d[s], 0));
+        if (P->copy_b) {
+            OMR_HIP(ctx, hipEventRecord(P->h2d_b[s], P->copy_b));
+            OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d_b[s], 0));
+        }
         uint32_t* dout = out_on_device ? argb_out + (size_t)t0 * width * height : static_cast<uint32_t*>(P->d_out[s]);
         st = omr_render_batch_device(ctx, qdef, channels, size_c, reinterpret_cast<const void* const*>(din), cnt, 0,
                                      pb->pt, 1, width, height, flip_h, flip_v, dout,
