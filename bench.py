@@ -1007,6 +1007,13 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
         del os.environ["OMR_PIXBUF_COPY_STREAMS"]
         modes["device_out_2_copy_queues"] = lambda: ctx2.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
                                                                                    out=dev_out, bindings=binds)
+        # and on one that copies each tile-channel plane as its own 2-D rect (OMR_PIXBUF_BANDS=0)
+        # instead of one row band per plane for the tiles that share it (the default)
+        os.environ["OMR_PIXBUF_BANDS"] = "0"
+        ctx3 = omr.Context(ctx.device, torch_order=False)
+        del os.environ["OMR_PIXBUF_BANDS"]
+        modes["device_out_tile_rects"] = lambda: ctx3.render_pixel_buffer_tiles(qd, chans, pb, reqs, TILE, TILE,
+                                                                                out=dev_out, bindings=binds)
         for name, fn in modes.items():
             if fn is None:          # reader threads -> pinned staging instead of DMA from the mapping
                 _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 0)
@@ -1023,9 +1030,10 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
         _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
         _lib.lib.omr_pinned_free(ctx.h, pin)
         ctx2.close()
+        ctx3.close()
         res["pcie_probe"] = pcie_probe(torch, uniq.device)
         ceil = max(v["gbs"] for v in res["pcie_probe"].values() if isinstance(v, dict))
-        best = max(res["device_out"]["tiles_per_s"], res["device_out_2_copy_queues"]["tiles_per_s"])
+        best = max(res[k]["tiles_per_s"] for k in ("device_out", "device_out_2_copy_queues", "device_out_tile_rects"))
         res["device_out_h2d_gbs"] = round(best * res["pcie_bytes_per_tile_in"] / 1e9, 2)
         res["device_out_vs_pcie_probe"] = round(res["device_out_h2d_gbs"] / ceil, 3)
         res["serving"] = serving_section(torch, ctx, pb, qd, chans, binds, grid, pool_devices=pool_devices)

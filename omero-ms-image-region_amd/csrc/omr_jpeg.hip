@@ -200,6 +200,34 @@ __device__ __forceinline__ Rgb rgb_of(uint32_t p) {
     return Rgb{(int)((p >> 16) & 0xFF), (int)((p >> 8) & 0xFF), (int)(p & 0xFF)};
 }
 
+// One pixel as two packed 16-bit pairs, r | g << 16 and b | g << 16: the operands of the
+// v_dot2 colour transform below (B1/F1 pixel sources hand these over).
+struct Px2 {
+    uint32_t rg, bg;
+};
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ Px2 px2_of(uint32_t argb) {   // v_perm: bytes (r, 0, g, 0) and (b, 0, g, 0)
+    return Px2{__builtin_amdgcn_perm(0u, argb, 0x0c010c02u), __builtin_amdgcn_perm(0u, argb, 0x0c010c00u)};
+}
+__device__ __forceinline__ uint32_t udot2(uint32_t a, u16x2 k, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), k, c, false);
+}
+__device__ __forceinline__ int sdot2(uint32_t a, i16x2 k, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), k, c, false);
+}
+// jccolor.c rgb_ycc_convert as above, each component two v_dot2 (exact: every product and partial
+// sum fits 32 bits; 32768 is applied through the unsigned form, the negative weights through the
+// signed one).
+__device__ __forceinline__ void ycc(const Px2& p, int& y, int& cb, int& cr) {
+    y = (int)(udot2(p.rg, u16x2{19595, 38470}, udot2(p.bg, u16x2{7471, 0}, 32768u)) >> 16);
+    cb = sdot2(p.rg, i16x2{-11059, -21709}, (int)udot2(p.bg, u16x2{32768, 0}, (128u << 16) + 32767u)) >> 16;
+    cr = sdot2(p.bg, i16x2{-5329, -27439}, (int)udot2(p.rg, u16x2{32768, 0}, (128u << 16) + 32767u)) >> 16;
+}
+__device__ __forceinline__ bool is_grey(const Px2& p) {   // r == g == b
+    return (((p.rg ^ (p.rg >> 16)) | (p.bg ^ (p.bg >> 16))) & 0xFFFFu) == 0;
+}
+
 #define DESCALE(x, n) (((x) + (1 << ((n)-1))) >> (n))
 #define M24(a, c) __mul24((a), (c))
 
@@ -780,6 +808,10 @@ __device__ __forceinline__ int quant_recip(int t, int half, uint32_t m) {
     return (u ^ sg) - sg;                                     // sign restored, no branch
 }
 
+// v_writelane_b32: the uniform value v into lane `lane` of old (LLVM's intrinsic; the compiler
+// routes an SGPR lane select through M0 itself).
+__device__ int lane_write(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
 __constant__ uint8_t c_zigzag[64] = {
     0, 1, 8, 16, 9, 2, 3, 10, 17, 24, 32, 25, 18, 11, 4, 5,
     12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6, 7, 14, 21, 28,
@@ -831,6 +863,7 @@ constexpr int kBS = 72, kRS = 9;
 // needs for an MCU into prefetch slot S (two slots: the MCUs two ahead are in flight while the
 // current one is transformed); take<S>() hands them over at the start of that MCU.
 struct ArgbSource {
+    static constexpr bool kEdgeRows = true;   // odd heights: the bottom chroma row replicates
     const uint32_t* img;
     int W, H;
     bool even_w;
@@ -860,9 +893,9 @@ struct ArgbSource {
         }
     }
     template <int S>
-    __device__ __forceinline__ void take(Rgb (&px)[4]) {
-        px[0] = rgb_of(nclamp[S] ? na[S].y : na[S].x); px[1] = rgb_of(na[S].y);
-        px[2] = rgb_of(nclamp[S] ? nb[S].y : nb[S].x); px[3] = rgb_of(nb[S].y);
+    __device__ __forceinline__ void take(Px2 (&px)[4]) {
+        px[0] = px2_of(nclamp[S] ? na[S].y : na[S].x); px[1] = px2_of(na[S].y);
+        px[2] = px2_of(nclamp[S] ? nb[S].y : nb[S].x); px[3] = px2_of(nb[S].y);
     }
     __device__ __forceinline__ uint32_t at(int x, int y) const { return *px_at<uint32_t>((uint32_t)(y * W + x)); }
     template <typename T>
@@ -886,6 +919,7 @@ struct FusedArgs {
 
 template <int BPP, bool BE, int MODE, int NA>
 struct PlaneSource {
+    static constexpr bool kEdgeRows = false;  // fused tiles have H % 16 == 0
     const FusedArgs& F;
     const uint32_t* s_contrib;   // LDS [n_active][256]
     const uint8_t* base[kFusedMaxActive];
@@ -955,7 +989,7 @@ struct PlaneSource {
         }
     }
     template <int S>
-    __device__ __forceinline__ void take(Rgb (&px)[4]) {
+    __device__ __forceinline__ void take(Px2 (&px)[4]) {
         uint32_t acc[4] = {0, 0, 0, 0};         // source order: (lo, hi) of row 0, then row 1
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
@@ -969,7 +1003,7 @@ struct PlaneSource {
                 w1 ^= sg;
                 if (F.R.any_check && F.R.ch[a].check) {      // wave-uniform
                     const uint32_t hi2 = F.R.dhi2[a], lo2 = F.R.dlo2[a];
-                    err |= (pk_max_u16(pk_max_u16(w0, w1), hi2) != hi2) | (pk_min_u16(pk_min_u16(w0, w1), lo2) != lo2);
+                    err |= ((pk_max_u16(pk_max_u16(w0, w1), hi2) ^ hi2) | (pk_min_u16(pk_min_u16(w0, w1), lo2) ^ lo2)) != 0;
                 }
             }
             if constexpr ((OMR_ABL & kAblRender) != 0) {   // raw words instead of quantize + table
@@ -985,10 +1019,13 @@ struct PlaneSource {
             const uint32_t t0 = acc[0], t2 = acc[2];
             acc[0] = acc[1]; acc[1] = t0; acc[2] = acc[3]; acc[3] = t2;
         }
-        // components straight from the 10-bit sums (no ARGB pack for ycc() to unpack)
+        // the packed pairs straight from the 10-bit sums (r << 20 | g << 10 | b), each component
+        // clamped to 255 by one v_pk_min_u16 per pair (no ARGB pack for the colour transform)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            px[j] = Rgb{(int)min(acc[j] >> 20, 255u), (int)min((acc[j] >> 10) & 1023u, 255u), (int)min(acc[j] & 1023u, 255u)};
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t g = (acc[j] << 6) & 0x03FF0000u;
+            px[j] = Px2{pk_min_u16((acc[j] >> 20) | g, 0x00FF00FFu), pk_min_u16((acc[j] & 0x3FFu) | g, 0x00FF00FFu)};
+        }
     }
     __device__ __forceinline__ uint32_t at(int, int) const { return 0; }   // never: H % 16 == 0
     // after the last MCU: a channel whose domain holds no 16-bit value fails every pixel
@@ -1039,35 +1076,35 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         bool grey;
         {
             const int x0 = mx * 16 + 2 * cx;
-            Rgb px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
+            Px2 px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
             src.template take<SL>(px);
             if (j + 2 < cnt) fetch(slot);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
-            auto isg = [](const Rgb& p) { return p.r == p.g && p.g == p.b; };
-            grey = __ballot(!(isg(px[0]) && isg(px[1]) && isg(px[2]) && isg(px[3])) || cyg >= chv) == 0;
+            const bool edge = Src::kEdgeRows && cyg >= chv;
+            grey = __ballot(!(is_grey(px[0]) && is_grey(px[1]) && is_grey(px[2]) && is_grey(px[3])) || edge) == 0;
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
             const int o = blk * kBS + ((2 * cy) & 7) * kRS + ((2 * cx) & 7);
             if (grey) {
-                S[o] = px[0].b - 128;
-                S[o + 1] = px[1].b - 128;
-                S[o + kRS] = px[2].b - 128;
-                S[o + kRS + 1] = px[3].b - 128;
+                S[o] = (int)(px[0].bg & 0xFFFFu) - 128;
+                S[o + 1] = (int)(px[1].bg & 0xFFFFu) - 128;
+                S[o + kRS] = (int)(px[2].bg & 0xFFFFu) - 128;
+                S[o + kRS + 1] = (int)(px[3].bg & 0xFFFFu) - 128;
             } else if constexpr ((OMR_ABL & kAblColour) != 0) {
-                S[o] = px[0].r; S[o + 1] = px[1].g; S[o + kRS] = px[2].b; S[o + kRS + 1] = px[3].r;
-                S[4 * kBS + cy * kRS + cx] = px[0].g;
-                S[5 * kBS + cy * kRS + cx] = px[1].b;
+                S[o] = px[0].rg & 0xFF; S[o + 1] = px[1].bg >> 16; S[o + kRS] = px[2].bg & 0xFF; S[o + kRS + 1] = px[3].rg & 0xFF;
+                S[4 * kBS + cy * kRS + cx] = px[0].rg >> 16;
+                S[5 * kBS + cy * kRS + cx] = px[1].bg & 0xFF;
             } else {
             ycc(px[0], y, cb0, cr0); S[o] = y - 128;
             ycc(px[1], y, cb1, cr1); S[o + 1] = y - 128;
             ycc(px[2], y, cb2, cr2); S[o + kRS] = y - 128;
             ycc(px[3], y, cb3, cr3); S[o + kRS + 1] = y - 128;
-            if (cyg >= chv) {
+            if (edge) {
                 const int xa = min(x0, W - 1), xb = min(x0 + 1, W - 1);
                 const int r0 = min(2 * (chv - 1), H - 1), r1 = min(2 * (chv - 1) + 1, H - 1);
-                ycc(src.at(xa, r0), y, cb0, cr0); ycc(src.at(xb, r0), y, cb1, cr1);
-                ycc(src.at(xa, r1), y, cb2, cr2); ycc(src.at(xb, r1), y, cb3, cr3);
+                ycc(px2_of(src.at(xa, r0)), y, cb0, cr0); ycc(px2_of(src.at(xb, r0)), y, cb1, cr1);
+                ycc(px2_of(src.at(xa, r1)), y, cb2, cr2); ycc(px2_of(src.at(xb, r1)), y, cb3, cr3);
             }
             const int bias = (cx & 1) ? 2 : 1;
             S[4 * kBS + cy * kRS + cx] = ((cb0 + cb1 + cb2 + cb3 + bias) >> 2) - 128;
@@ -1126,9 +1163,8 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         if constexpr ((OMR_ABL & kAblLane0) != 0) {
             abl_sink ^= dc[0] + dc[5];
         } else {
-            const int slot = lane - 6 * j;
 #pragma unroll
-            for (int k = 0; k < 6; ++k) rec = slot == k ? (int)((uint32_t)dc[k] << 16) : rec;
+            for (int k = 0; k < 6; ++k) rec = lane_write((int)((uint32_t)dc[k] << 16), 6 * j + k, rec);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
@@ -1789,7 +1825,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     // 0.8); longer streams loop in B4a/B6.  Workgroups past the stream end only exit, but at
     // 2 B per pixel they were 4/5 of both grids.
     const int64_t est_groups = std::max<int64_t>(1, std::min<int64_t>(L.slot_groups,
-                                   ((int64_t)W * H / kStuffBytes + kGrp - 1) / kGrp));
+                                   ((int64_t)W * H * ctx->jpeg_est_centibpp / 100 / kStuffBytes + kGrp - 1) / kGrp));
     KernelTimer whole(ctx, 4);
     {
         KernelTimer t(ctx, 5);

@@ -143,6 +143,7 @@ struct PixPipe {
     hipEvent_t h2d_b[2] = {nullptr, nullptr};   // the second copy stream's part of a slot
     hipStream_t copy = nullptr;
     hipStream_t copy_b = nullptr;               // a second DMA queue (env OMR_PIXBUF_COPY_STREAMS=2)
+    bool bands = true;                          // row-band copies (env OMR_PIXBUF_BANDS=0: per-tile rects)
     explicit PixPipe(int threads) : pool(threads) {}
     ~PixPipe() {
         if (copy) (void)hipStreamSynchronize(copy);
@@ -171,6 +172,8 @@ static omr_status get_pipe(Ctx* c, PixPipe*& out) {
         OMR_HIP(c, hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking));
         const char* ncs = std::getenv("OMR_PIXBUF_COPY_STREAMS");
         if (ncs && std::atoi(ncs) >= 2) OMR_HIP(c, hipStreamCreateWithFlags(&p->copy_b, hipStreamNonBlocking));
+        const char* nb = std::getenv("OMR_PIXBUF_BANDS");
+        if (nb && std::atoi(nb) == 0) p->bands = false;
         for (int i = 0; i < 2; ++i)
             for (hipEvent_t* e : {&p->h2d[i], &p->rend[i], &p->d2h[i], &p->h2d_b[i]})
                 OMR_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -368,10 +371,7 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
     const size_t plane = (size_t)width * height * pb->bpp;
     const size_t plane_al = align_up(plane, 256);
     const size_t tile_out = (size_t)width * height * 4;
-    // group: ~64 MiB of planes per slot
     const int na = std::max<int>(1, (int)act.size());
-    const int G = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, ((size_t)64 << 20) / (plane_al * na)));
-    const size_t tab_bytes = align_up(sizeof(void*) * (size_t)G * size_c, 256);
     bool host_out = !out_on_device;
     bool out_pinned = false;
     if (host_out) {
@@ -379,13 +379,74 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
         if (hipPointerGetAttributes(&attr, argb_out) == hipSuccess && attr.type == hipMemoryTypeHost) out_pinned = true;
         (void)hipGetLastError();
     }
-    st = grow(ctx, P, tab_bytes + plane_al * (size_t)G * na, tile_out * G, host_out && !out_pinned);
-    if (st) return st;
-    const int ngroups = (n + G - 1) / G;
     const bool direct = ctx->pixbuf_direct && ensure_registered(const_cast<omr_pixel_buffer*>(pb));
+    // Band mode: the tiles of a group that share a row band of one plane -- same z, c, t and y,
+    // the neighbouring tiles a viewer asks for together -- come in as one band laid out at the
+    // image's full row width: by DMA from the registered mapping, a single contiguous copy when
+    // they cover the whole row, else one 2-D copy of their column span; staged, one pread per
+    // chunk of rows (or per row of the span) into the pinned slot, then one copy of the slot.
+    // K2 reads each tile in place with the image's row stride.  Per-tile mode: one 2-D copy (or
+    // one pread per row) of width x height per tile and channel into a compact plane.
+    const bool bands = P->bands && (int64_t)pb->sx * pb->bpp == pb->row_bytes;
+    const size_t band_bytes = align_up((size_t)height * (size_t)pb->row_bytes, 256);
+    const size_t budget = (size_t)64 << 20;   // planes per slot
+    struct Band {
+        int32_t z, c, t, y, x0, x1;
+    };
+    // groups: [start, end) tile ranges, slot g & 1; per-tile-channel band index (band mode)
+    std::vector<int> gstart;
+    std::vector<int32_t> tile_band((size_t)n * na, -1);
+    std::vector<std::vector<Band>> gbands;
+    size_t in_need = 0;
+    int gmax = 1;
+    if (bands) {
+        const size_t cap = std::max(budget, band_bytes * (size_t)na);
+        std::vector<int32_t> hit(act.size());
+        for (int i = 0; i < n;) {
+            gstart.push_back(i);
+            std::vector<Band> bl;
+            const int i0 = i;
+            for (; i < n; ++i) {
+                const omr_tile_request& r = reqs[i];
+                int fresh = 0;
+                for (int a = 0; a < (int)act.size(); ++a) {
+                    hit[a] = -1;
+                    for (size_t k = 0; k < bl.size(); ++k)
+                        if (bl[k].z == r.z && bl[k].c == act[a] && bl[k].t == r.t && bl[k].y == r.y) { hit[a] = (int32_t)k; break; }
+                    fresh += hit[a] < 0;
+                }
+                if (i > i0 && (bl.size() + fresh) * band_bytes > cap) break;
+                for (int a = 0; a < (int)act.size(); ++a) {
+                    if (hit[a] < 0) {
+                        hit[a] = (int32_t)bl.size();
+                        bl.push_back(Band{r.z, act[a], r.t, r.y, r.x, r.x + width});
+                    } else {
+                        Band& b = bl[hit[a]];
+                        b.x0 = std::min(b.x0, r.x);
+                        b.x1 = std::max(b.x1, r.x + width);
+                    }
+                    tile_band[(size_t)i * na + a] = hit[a];
+                }
+            }
+            gmax = std::max(gmax, i - i0);
+            in_need = std::max(in_need, bl.size() * band_bytes);
+            gbands.push_back(std::move(bl));
+        }
+    } else {
+        // ~64 MiB of compact planes per slot
+        const int G = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / (plane_al * na)));
+        for (int i = 0; i < n; i += G) gstart.push_back(i);
+        gmax = G;
+        in_need = plane_al * (size_t)G * na;
+    }
+    const int ngroups = (int)gstart.size();
+    gstart.push_back(n);
+    const size_t tab_bytes = align_up(sizeof(void*) * (size_t)gmax * size_c, 256);
+    st = grow(ctx, P, tab_bytes + in_need, tile_out * gmax, host_out && !out_pinned);
+    if (st) return st;
     std::atomic<bool> io_error{false};
     auto finish_host = [&](int g) -> omr_status {   // bounce slot -> caller (pageable output)
-        const int s = g & 1, t0 = g * G, cnt = std::min(G, n - t0);
+        const int s = g & 1, t0 = gstart[g], cnt = gstart[g + 1] - t0;
         OMR_HIP(ctx, hipEventSynchronize(P->d2h[s]));
         const uint8_t* src = static_cast<const uint8_t*>(P->pin_out[s]);
         uint8_t* dst = reinterpret_cast<uint8_t*>(argb_out) + (size_t)t0 * tile_out;
@@ -398,7 +459,7 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
         return OMR_OK;
     };
     for (int g = 0; g < ngroups; ++g) {
-        const int s = g & 1, t0 = g * G, cnt = std::min(G, n - t0);
+        const int s = g & 1, t0 = gstart[g], cnt = gstart[g + 1] - t0;
         if (g >= 2) OMR_HIP(ctx, hipEventSynchronize(P->h2d[s]));   // pinned slot s is free again
         uint8_t* hin = static_cast<uint8_t*>(P->pin_in[s]);
         uint8_t* din = static_cast<uint8_t*>(P->d_in[s]);
@@ -407,8 +468,32 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
             for (int c = 0; c < size_c; ++c) tab[(size_t)i * size_c + c] = nullptr;
         for (int i = 0; i < cnt; ++i)
             for (int a = 0; a < (int)act.size(); ++a)
-                tab[(size_t)i * size_c + act[a]] = din + tab_bytes + plane_al * ((size_t)i * na + a);
-        if (!direct) {
+                tab[(size_t)i * size_c + act[a]] =
+                    bands ? din + tab_bytes + band_bytes * (size_t)tile_band[(size_t)(t0 + i) * na + a] +
+                                (size_t)reqs[t0 + i].x * pb->bpp
+                          : din + tab_bytes + plane_al * ((size_t)i * na + a);
+        if (!direct && bands) {
+            // file -> pinned, one job per 64 rows of a band: whole rows in one pread when the
+            // band's tiles cover them, else one pread per row of the column span
+            const std::vector<Band>& bl = gbands[g];
+            constexpr int kRows = 64;
+            const int chunks = (height + kRows - 1) / kRows;
+            P->pool.run((int)bl.size() * chunks, [&](int j) {
+                const Band& b = bl[j / chunks];
+                const int r0 = (j % chunks) * kRows, r1 = std::min(height, r0 + kRows);
+                const int64_t src = plane_offset(pb, b.z, b.c, b.t) + (int64_t)(b.y + r0) * pb->row_bytes;
+                uint8_t* dst = hin + tab_bytes + band_bytes * (size_t)(j / chunks) + (size_t)r0 * pb->row_bytes;
+                if (b.x0 == 0 && b.x1 == pb->sx) {
+                    if (!read_full(pb->fd, dst, (size_t)(r1 - r0) * pb->row_bytes, src)) io_error = true;
+                    return;
+                }
+                const size_t off = (size_t)b.x0 * pb->bpp, seg = (size_t)(b.x1 - b.x0) * pb->bpp;
+                for (int r = 0; r < r1 - r0; ++r)
+                    if (!read_full(pb->fd, dst + (size_t)r * pb->row_bytes + off, seg,
+                                   src + (int64_t)r * pb->row_bytes + (int64_t)off)) { io_error = true; return; }
+            });
+            if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
+        } else if (!direct) {
             P->pool.run(cnt * (int)act.size(), [&](int j) {   // file -> pinned, one tile-channel plane per job
                 const int i = j / (int)act.size(), a = j % (int)act.size();
                 const omr_tile_request& r = reqs[t0 + i];
@@ -419,7 +504,26 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
         }
         if (g >= 2) OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free
         if (g >= 2 && P->copy_b) OMR_HIP(ctx, hipStreamWaitEvent(P->copy_b, P->rend[s], 0));
-        if (direct) {
+        if (bands && !direct) {
+            OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes + band_bytes * gbands[g].size(), hipMemcpyHostToDevice,
+                                        P->copy));
+        } else if (bands) {
+            OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes, hipMemcpyHostToDevice, P->copy));
+            const std::vector<Band>& bl = gbands[g];
+            for (size_t k = 0; k < bl.size(); ++k) {
+                const Band& b = bl[k];
+                const uint8_t* src = pb->map + plane_offset(pb, b.z, b.c, b.t) + (int64_t)b.y * pb->row_bytes;
+                uint8_t* dst = din + tab_bytes + band_bytes * k;
+                hipStream_t cs = (P->copy_b && (k & 1)) ? P->copy_b : P->copy;
+                if (b.x0 == 0 && b.x1 == pb->sx)   // the tiles cover the row: the band is contiguous
+                    OMR_HIP(ctx, hipMemcpyAsync(dst, src, (size_t)height * pb->row_bytes, hipMemcpyHostToDevice, cs));
+                else
+                    OMR_HIP(ctx, hipMemcpy2DAsync(dst + (size_t)b.x0 * pb->bpp, (size_t)pb->row_bytes,
+                                                  src + (size_t)b.x0 * pb->bpp, (size_t)pb->row_bytes,
+                                                  (size_t)(b.x1 - b.x0) * pb->bpp, (size_t)height,
+                                                  hipMemcpyHostToDevice, cs));
+            }
+        } else if (direct) {
             // registered mapping: the copy engine reads each tile's rows from the page cache
             OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes, hipMemcpyHostToDevice, P->copy));
             for (int i = 0; i < cnt; ++i) {
@@ -446,8 +550,8 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
             OMR_HIP(ctx, hipStreamWaitEvent(ctx->stream, P->h2d_b[s], 0));
         }
         uint32_t* dout = out_on_device ? argb_out + (size_t)t0 * width * height : static_cast<uint32_t*>(P->d_out[s]);
-        st = omr_render_batch_device(ctx, qdef, channels, size_c, reinterpret_cast<const void* const*>(din), cnt, 0,
-                                     pb->pt, 1, width, height, flip_h, flip_v, dout,
+        st = omr_render_batch_device(ctx, qdef, channels, size_c, reinterpret_cast<const void* const*>(din), cnt,
+                                     bands ? (int64_t)pb->sx : 0, pb->pt, 1, width, height, flip_h, flip_v, dout,
                                      d_status ? d_status + t0 : nullptr);
         if (st) return st;
         OMR_HIP(ctx, hipEventRecord(P->rend[s], ctx->stream));

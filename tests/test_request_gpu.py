@@ -258,3 +258,42 @@ def test_pipelined_pixel_buffer_tiles(ctx, tmp_path, dma):
         np.testing.assert_array_equal(host[i], exp, err_msg=f"host tile {i}")
         np.testing.assert_array_equal(dev_np[i], exp, err_msg=f"device tile {i}")
         np.testing.assert_array_equal(pinned_copy[i], exp, err_msg=f"pinned tile {i}")
+
+
+@pytest.mark.parametrize("dma", [True, False])
+@pytest.mark.parametrize("W,H,flip", [(512, 384, (False, True)), (300, 200, (True, False))])
+def test_pixel_buffer_row_bands(ctx, tmp_path, W, H, flip, dma):
+    """Band mode of omr_render_pixel_buffer_tiles (DMA): tiles that share a row band of a plane
+    come in as one band at the image's row width -- a contiguous copy when they cover the whole
+    row, a 2-D copy of their column span otherwise -- and render in place with the image's row
+    stride.  Full rows, partial spans, overlapping bands, repeats and unaligned tile sizes against
+    the CPU restatement; by DMA from the registered mapping and staged through pinned memory."""
+    import torch
+    from omr import PixelBuffer, write_romio
+    from omr.synthetic import c2_channels
+    X, Y, Zf, Cf, T = 4 * W, 4 * H, 2, 4, 1
+    rng = np.random.default_rng(11)
+    px = rng.integers(0, 65536, (T, Cf, Zf, Y, X), dtype=np.uint16)
+    path = tmp_path / "bands"
+    write_romio(path, px, _lib.PIXELS_UINT16)
+    chans = c2_channels(4)
+    chans[1]["active"] = False
+    q = O.make_qdef("rgb")
+    reqs = [(0, 0, k * W, 0) for k in range(4)]                      # a whole row: one contiguous band
+    reqs += [(0, 0, W, H), (0, 0, 2 * W, H)]                         # a column span
+    reqs += [(1, 0, 0, H // 2), (1, 0, 3 * W, H // 2)]               # overlapping band, wide span
+    reqs += [(0, 0, 0, 0), (1, 0, W, 3 * H)]                         # a repeat; the last row
+    fh, fv = flip
+    _lib.check(_lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, int(dma)))
+    with PixelBuffer(path, X, Y, Zf, Cf, T, _lib.PIXELS_UINT16) as pb:
+        host = ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, flip_h=fh, flip_v=fv)
+        dev = torch.empty((len(reqs), H, W), dtype=torch.int32, device="cuda")
+        ctx.render_pixel_buffer_tiles(q, chans, pb, reqs, W, H, out=dev, flip_h=fh, flip_v=fv)
+    _lib.lib.omr_ctx_set_pixel_buffer_dma(ctx.h, 1)
+    dev_np = dev.cpu().numpy().view(np.uint32)
+    for i, (z, t, x, y) in enumerate(reqs):
+        planes = [np.ascontiguousarray(px[t, c, z, y:y + H, x:x + W]).astype(">u2") for c in range(Cf)]
+        st, exp = O.render(chans, planes, _lib.PIXELS_UINT16, W, H, big_endian=True, flip_h=fh, flip_v=fv)
+        assert st == 0
+        np.testing.assert_array_equal(host[i], exp, err_msg=f"host tile {i}")
+        np.testing.assert_array_equal(dev_np[i], exp, err_msg=f"device tile {i}")

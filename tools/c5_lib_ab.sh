@@ -13,5 +13,6 @@ for i in 1 2; do
     timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-jpeg --no-latency \
         > $O/b_$v$i.json 2> $O/b_$v$i.err || exit $?
     python3 -c "import json; d=json.loads(open('$O/b_$v$i.json').read().strip().splitlines()[-1])['c5_float']; print('$v run $i', d['roofline']['avg_launch_ms'], d['roofline']['frac'])"
+    python3 -c "import json; h=json.loads(open('$O/b_$v$i.json').read().strip().splitlines()[-1])['host_fed']; print('  host_fed', {k: h[k]['tiles_per_s'] for k in h if k.startswith('device_out') and isinstance(h[k], dict)}, h.get('device_out_vs_pcie_probe'))"
   done
 done
