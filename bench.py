@@ -1020,10 +1020,11 @@ def host_fed_section(torch, ctx, uniq, n_req, cpu_seconds, threads, with_cpu, po
                 fn = modes["device_out"]
             fn()
             ctx.synchronize()
-            reps = 3
+            reps = 0                  # calls over >= 0.5 s (three calls read 10-15 % low on the first leg)
             t0 = time.perf_counter()
-            for _ in range(reps):
+            while reps < 3 or time.perf_counter() - t0 < 0.5:
                 fn()
+                reps += 1
             ctx.synchronize()
             el = time.perf_counter() - t0
             res[name] = {"tiles_per_s": round(n_req * reps / el, 1), "ms_per_tile": round(1e3 * el / (n_req * reps), 4)}
