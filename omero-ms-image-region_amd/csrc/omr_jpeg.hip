@@ -829,8 +829,9 @@ enum : int { kAblColour = 2, kAblFdct = 4, kAblLane0 = 8, kAblCoefStore = 16, kA
 struct B1Args {
     const uint32_t* argb;
     int64_t tile_stride;  // pixels between tiles
-    int16_t* coefs;       // [tile][nb][64] zig-zag order
-    uint32_t* blk;        // [tile][nb] AC bits incl. ZRL/EOB | DC after dummy-block propagation << 16
+    int16_t* coefs;       // [tile][nb][64] zig-zag order, int16: blocks with an AC outside int8
+    int8_t* coef8;        // [tile][nb][64] zig-zag order, int8: the other blocks (DC in the record)
+    uint32_t* blk;        // [tile][nb] DC after dummy-block propagation << 16 | 1 for an int16 block
     int32_t W, H, mcux, n_mcu, nb;
     int32_t mpw;          // MCUs per wave (prefetch depth vs. waves in flight)
     QTabs qt;
@@ -1125,6 +1126,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const int64_t b0 = (int64_t)tile * A.nb + (int64_t)m * 6;
         int16_t* out = A.coefs + b0 * 64;
+        int8_t* out8 = A.coef8 + b0 * 64;
         int qv[6];
         int coef[6];                              // all six blocks' coefficients read back to back
 #pragma unroll
@@ -1140,9 +1142,11 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             qv[k] = q;
         }
         // jccoefct.c dummy-block DC propagation on the wave-uniform DCs (lane 0's coefficient),
-        // then each block's 64 coefficients in one store (lane 0 stores the propagated DC).  The
-        // blocks' Huffman lengths are B2a's (one lane per block walks the stored coefficients:
-        // half the instructions of a ballot-per-coefficient length here).
+        // then each block's 64 coefficients in one store.  A block whose 63 ACs all fit int8 --
+        // nearly every block at any quality -- goes out as 64 bytes, so B2a and B3 read half the
+        // bytes; one with a larger AC as 128 (int16, lane 0 storing the propagated DC), flagged in
+        // bit 0 of its record.  The blocks' Huffman lengths are B2a's (one lane per block walks
+        // the stored coefficients: half the instructions of a ballot-per-coefficient length here).
         int dc[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) dc[k] = __builtin_amdgcn_readfirstlane(qv[k]);
@@ -1152,11 +1156,22 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             if (row1) { dc[2] = dc[1]; dc[3] = dc[1]; }
             else if (c1) dc[3] = dc[2];
         }
+        // one choice for the MCU's six blocks: an AC outside int8 in any of them (OR of the
+        // biased values: a bit above bit 7 in any) makes all six int16
+        uint32_t big = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) big |= (uint32_t)(qv[k] + 128);
+        const uint32_t wide = __ballot(lane != 0 && big > 255u) != 0 ? 0x3Fu : 0u;   // bit k: block k int16
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int v = lane == 0 ? dc[k] : qv[k];
-            if constexpr ((OMR_ABL & kAblCoefStore) != 0) abl_sink ^= v;
-            else *reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(out) + (uint32_t)(k * 128 + lane * 2)) = (int16_t)v;
+            if constexpr ((OMR_ABL & kAblCoefStore) != 0) {
+                abl_sink ^= v;
+            } else if (wide) {
+                *reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(out) + (uint32_t)(k * 128 + lane * 2)) = (int16_t)v;
+            } else {
+                *reinterpret_cast<int8_t*>(reinterpret_cast<uint8_t*>(out8) + (uint32_t)(k * 64 + lane)) = (int8_t)qv[k];
+            }
         }
         // the six per-block DC records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in
         // the wave's run); one store per wave after the loop instead of six one-lane stores per MCU
@@ -1164,7 +1179,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             abl_sink ^= dc[0] + dc[5];
         } else {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) rec = lane_write((int)((uint32_t)dc[k] << 16), 6 * j + k, rec);
+            for (int k = 0; k < 6; ++k) rec = lane_write((int)(((uint32_t)dc[k] << 16) | ((wide >> k) & 1u)), 6 * j + k, rec);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // S is rewritten by the next MCU
         __builtin_amdgcn_wave_barrier();
@@ -1194,7 +1209,9 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
 // F1: fused render + B1 (see PlaneSource).  The contribution tables are staged once per
 // workgroup; a pixel outside its channel's LUT domain flags the tile (QuantizationException).
 template <int BPP, bool BE, int MODE, int NA>
-__global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F) {
+// The C2 headline instantiation (fast16 in f32) is held to 64 VGPRs: 8 waves per SIMD, no spill.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFusedFast16F ? 8 : 1)))
+k_jpeg_render_fdct(B1Args A, FusedArgs F) {
     __shared__ int s[4][6 * kBS + 8];
     __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
     for (int i = threadIdx.x; i < NA * 256; i += 256) s_contrib[i] = F.R.contrib[i];
@@ -1232,8 +1249,9 @@ __device__ __forceinline__ uint32_t block_reduce_sum(uint32_t v, uint32_t* s_wav
 // zig-zag coefficients (eight 16-byte loads into registers, the walk unrolled): run length,
 // magnitude category by frexp, code length from an LDS table, ZRLs and EOB, branch-free.
 struct B2aArgs {
-    const int16_t* coefs;  // [tile][nb][64] zig-zag order
-    const uint32_t* blk;   // B1's per-block records (DC << 16)
+    const int16_t* coefs;  // [tile][nb][64] zig-zag order (int16 blocks)
+    const int8_t* coef8;   // [tile][nb][64] zig-zag order (int8 blocks)
+    const uint32_t* blk;   // B1's per-block records (DC << 16 | int16 flag)
     uint16_t* bits;        // [tile][nb]
     uint32_t* gsum;        // [tile][ngb]
     int32_t nb, ngb;
@@ -1243,6 +1261,37 @@ struct B2aArgs {
 // uniform base plus a 32-bit byte offset (an SGPR-base load, no 64-bit address VALU).
 __device__ __forceinline__ const uint4* group_block_coefs(const int16_t* coefs, int64_t g0, int i) {
     return reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(coefs + g0 * 64) + (uint32_t)i * 128u);
+}
+__device__ __forceinline__ const uint4* group_block_coefs8(const int8_t* coef8, int64_t g0, int i) {
+    return reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(coef8 + g0 * 64) + (uint32_t)i * 64u);
+}
+
+__device__ __forceinline__ uint32_t u4_at(const uint4& v, int c) {   // c static after unrolling
+    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+// Zig-zag coefficient k of a block held in registers: int8 blocks in q[0..3] (byte k), int16
+// blocks in q[0..7] (half k).
+template <bool NARROW>
+__device__ __forceinline__ int block_coef(const uint4 (&q)[8], int k) {
+    if constexpr (NARROW) {
+        const uint32_t w = u4_at(q[k >> 4], (k >> 2) & 3);
+        return (int)(int8_t)(w >> (8 * (k & 3)));
+    } else {
+        const uint32_t w = u4_at(q[k >> 3], (k >> 1) & 3);
+        return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
+    }
+}
+// An int8 block in q[0..3] widened in place to the int16 form in q[0..7] (the lanes of a wave
+// that also holds an int16 block: the wave then walks every block in the int16 form).
+__device__ __forceinline__ void widen_block(uint4 (&q)[8]) {
+    auto pair = [](uint32_t w, int h) {
+        return ((uint32_t)(int)(int8_t)(w >> (16 * h)) & 0xFFFFu) | ((uint32_t)(int)(int8_t)(w >> (16 * h + 8)) << 16);
+    };
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {   // q[i] from q[i >> 1], which a later (lower) i still reads
+        const uint32_t w0 = u4_at(q[i >> 1], (i & 1) * 2), w1 = u4_at(q[i >> 1], (i & 1) * 2 + 1);
+        q[i] = make_uint4(pair(w0, 0), pair(w0, 1), pair(w1, 0), pair(w1, 1));
+    }
 }
 
 // Magnitude category (bit length of |c|, 0 for 0) of a coefficient: frexp's exponent of the exact
@@ -1265,12 +1314,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     uint32_t bits = 0;
     if (b < A.nb) {
         const int64_t gb = (int64_t)tile * A.nb + b;
-        uint4 q[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = group_block_coefs(A.coefs, (int64_t)tile * A.nb + b0, threadIdx.x)[i];
         const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
-        const int pb = prev_block_in_tile(b);
         const uint32_t rb = blk[b];
+        const bool wide = (rb & 1u) != 0;
+        uint4 q[8];
+        const int pb = prev_block_in_tile(b);
         const int d = (int)(int16_t)(rb >> 16) - (pb >= 0 ? (int)(int16_t)(blk[pb] >> 16) : 0);
         const int nbd = mag_bits(d);
         const int t = (b % 6) < 4 ? 0 : 1;
@@ -1279,22 +1327,34 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
         uint32_t r16 = 0;                                  // zero run before coefficient k, times 16
         // eight coefficients at a time: their table indices first (the run chain is VALU only),
         // then the eight LDS reads in flight together
+        if (!wide) {
+            // an int8 block: its 64 bytes in registers, the walk unrolled
 #pragma unroll
-        for (int k0 = 0; k0 < 64; k0 += 8) {
-            uint32_t idx[8];
+            for (int i = 0; i < 4; ++i) q[i] = group_block_coefs8(A.coef8, (int64_t)tile * A.nb + b0, threadIdx.x)[i];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = k0 + j;
-                if (k == 0) { idx[j] = 0; continue; }
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
-                const int c = (k & 1) ? (int)(int16_t)(w[(k >> 1) & 3] >> 16) : (int)(int16_t)(w[(k >> 1) & 3] & 0xFFFF);
-                const int nb = mag_bits(c);
-                idx[j] = r16 | nb;
-                bits += nb;
+            for (int k0 = 0; k0 < 64; k0 += 8) {
+                uint32_t idx[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int k = k0 + j;
+                    if (k == 0) { idx[j] = 0; continue; }
+                    const int nb = mag_bits(block_coef<true>(q, k));
+                    idx[j] = r16 | nb;
+                    bits += nb;
+                    r16 = nb ? 0u : r16 + 16;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bits += (k0 + j) ? len[idx[j]] : 0u;   // zero coefficient: entry 0
+            }
+        } else {
+            // an int16 block (an AC outside int8: rare): a rolled walk over its stored coefficients
+            const int16_t* cp = A.coefs + gb * 64;
+#pragma unroll 1
+            for (int k = 1; k < 64; ++k) {
+                const int nb = mag_bits(cp[k]);
+                bits += nb + len[r16 | nb];
                 r16 = nb ? 0u : r16 + 16;
             }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bits += (k0 + j) ? len[idx[j]] : 0u;   // zero coefficient: entry 0
         }
         if (r16) bits += c_huff[1 + 2 * t].size[0x00];     // EOB after the last non-zero
         A.bits[gb] = (uint16_t)bits;                       // bit count | 0x800 x ZRL-prefixed coefficients
@@ -1356,8 +1416,9 @@ __global__ void __launch_bounds__(kTileThreads) k_jpeg_group_scan(GroupScanArgs 
 }
 
 struct B3Args {
-    const int16_t* coefs;
-    const uint32_t* blk;     // B1's per-block records (DC << 16)
+    const int16_t* coefs;    // int16 blocks
+    const int8_t* coef8;     // int8 blocks
+    const uint32_t* blk;     // B1's per-block records (DC << 16 | int16 flag)
     const uint16_t* bits;    // [tile][nb]
     const uint32_t* goff;    // [tile][ngb] exclusive bit offset of each 256-block group
     uint32_t* words;
@@ -1406,12 +1467,24 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     // The coder, instantiated for the LDS-staged group (the common case: a flush is one ds_or at
     // a running LDS pointer) and for a group too long for the staging buffer (word stores, the
     // block's shared first word ORed into HBM).
-    auto code_block = [&](auto staged_c) {
+    // NARROW: every block of the wave is int8 (and no ZRL, staged): the walk reads bytes.
+    // Otherwise int8 blocks are widened in registers and the wave walks the int16 form.
+    const uint32_t myrec = live ? A.blk[gb] : 0u;
+    const bool wide = (myrec & 1u) != 0;
+    const bool any_wide = __ballot(wide) != 0;
+    auto code_block = [&](auto staged_c, auto narrow_c) {
         constexpr bool STAGED = decltype(staged_c)::value;
-        const uint4* src = group_block_coefs(A.coefs, (int64_t)tile * A.nb + (int64_t)blockIdx.x * kGrp, threadIdx.x);
+        constexpr bool NARROW = decltype(narrow_c)::value;
+        const int64_t g0 = (int64_t)tile * A.nb + (int64_t)blockIdx.x * kGrp;
         uint4 q[8];
+        if (NARROW || !wide) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = src[i];
+            for (int i = 0; i < 4; ++i) q[i] = group_block_coefs8(A.coef8, g0, threadIdx.x)[i];
+            if constexpr (!NARROW) widen_block(q);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) q[i] = group_block_coefs(A.coefs, g0, threadIdx.x)[i];
+        }
         const int pb = prev_block_in_tile(b);
         const int pred = pb >= 0 ? (int)(int16_t)(A.blk[(int64_t)tile * A.nb + pb] >> 16) : 0;
         uint64_t acc = 0;
@@ -1436,15 +1509,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
                 nacc -= 32;
             }
         };
-        auto coef = [&](int k) -> int {
-            const uint32_t* d = reinterpret_cast<const uint32_t*>(&q[k >> 3]);
-            const uint32_t w = d[(k >> 1) & 3];
-            return (k & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF);
-        };
+        auto coef = [&](int k) -> int { return block_coef<NARROW>(q, k); };
         const int kk = b % 6;
         const int ta = kk < 4 ? 0 : 1;
         {
-            int d = coef(0) - pred, d2 = d;
+            int d = (int)(int16_t)(myrec >> 16) - pred, d2 = d;
             if (d < 0) { d = -d; d2--; }
             const int nbits = d ? 32 - __clz(d) : 0;
             const uint32_t dcc = s_t.dc[ta][nbits];
@@ -1473,7 +1542,8 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
                 r = nzk ? 0 : r + 1;
             }
         };
-        if (any_zrl) walk(std::true_type{});
+        if constexpr (NARROW) walk(std::false_type{});
+        else if (any_zrl) walk(std::true_type{});
         else walk(std::false_type{});
         if (r > 0) put(eob & 0xFFFF, (int)(eob >> 16));                   // EOB
         if (nacc > 0) {                                                   // shared with the next block
@@ -1483,8 +1553,9 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         }
     };
     if (live) {
-        if (staged) code_block(std::true_type{});
-        else code_block(std::false_type{});
+        if (staged && !any_zrl && !any_wide) code_block(std::true_type{}, std::true_type{});
+        else if (staged) code_block(std::true_type{}, std::false_type{});
+        else code_block(std::false_type{}, std::false_type{});
     }
     if (staged) {
         __syncthreads();
@@ -1720,7 +1791,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
 // Batch workspace layout.
 struct JpegBatchLayout {
     int64_t n_mcu, nb, ngb, slot_words, slot_chunks, slot_groups;
-    size_t coef, blk, bits, gsum, tbits, words, cnt, csum, ngroups, stuffed, hdr, total;
+    size_t coef, coef8, blk, bits, gsum, tbits, words, cnt, csum, ngroups, stuffed, hdr, total;
 };
 
 static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
@@ -1734,6 +1805,7 @@ static JpegBatchLayout jpeg_batch_layout(int W, int H, int n, size_t base) {
     size_t o = align_up(base, 256);
     auto take = [&](size_t bytes) { const size_t r = o; o = align_up(o + bytes, 256); return r; };
     L.coef = take((size_t)n * L.nb * 128);
+    L.coef8 = take((size_t)n * L.nb * 64);
     L.blk = take((size_t)n * L.nb * 4);
     L.bits = take((size_t)n * L.nb * 2);
     L.gsum = take((size_t)n * L.ngb * 4);
@@ -1799,6 +1871,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     a1.argb = d_argb;
     a1.tile_stride = tile_stride;
     a1.coefs = reinterpret_cast<int16_t*>(ws + L.coef);
+    a1.coef8 = reinterpret_cast<int8_t*>(ws + L.coef8);
     a1.blk = reinterpret_cast<uint32_t*>(ws + L.blk);
     a1.W = W;
     a1.H = H;
@@ -1810,9 +1883,9 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
     for (int i = 0; i < 64; ++i) { a1.qt.q[0][i] = ql[i]; a1.qt.q[1][i] = qc[i]; }
     set_recips(a1.qt);
     uint16_t* d_bits = reinterpret_cast<uint16_t*>(ws + L.bits);
-    B2aArgs a2{a1.coefs, a1.blk, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
+    B2aArgs a2{a1.coefs, a1.coef8, a1.blk, d_bits, u32(L.gsum), (int32_t)L.nb, (int32_t)L.ngb};
     GroupScanArgs a2b{u32(L.gsum), nullptr, u32(L.tbits), u32(L.words), nullptr, L.ngb, L.slot_words, (int32_t)L.ngb};
-    B3Args a3{a1.coefs, a1.blk, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
+    B3Args a3{a1.coefs, a1.coef8, a1.blk, d_bits, u32(L.gsum), u32(L.words), (int32_t)L.nb, (int32_t)L.ngb, L.slot_words};
     B4aArgs a4{u32(L.words), u32(L.tbits), ws + L.cnt, u32(L.csum), u32(L.ngroups), L.slot_words, L.slot_chunks,
                L.slot_groups};
     GroupScanArgs a4b{u32(L.csum), u32(L.ngroups), u32(L.stuffed), nullptr, u32(L.tbits), L.slot_groups, 0, 0};
