@@ -106,6 +106,9 @@ __constant__ ZzInv c_zzinv = make_zzinv();
 // bit count (< 2^11) plus 0x800 per ZRL-prefixed coefficient, so B2a flags B3's ZRL path for free.
 // [0] luma, [1] chroma; 2 KiB each, copied to LDS with 16-B loads.
 constexpr uint32_t kZrlFlag = 0x800;
+// B2a's per-block record also carries the block's int16 flag (B3 then knows which form to load
+// before loading anything): bit 15, above the bit count and at most three ZRL flags (< 0x2000).
+constexpr uint32_t kWideFlag = 0x8000;
 struct AcLen {
     uint16_t v[2][1024];
 };
@@ -1315,9 +1318,13 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
     if (b < A.nb) {
         const int64_t gb = (int64_t)tile * A.nb + b;
         const uint32_t* blk = A.blk + (int64_t)tile * A.nb;
+        // the int8 form is loaded before the record says which form the block has, so the two
+        // loads overlap (an int16 block -- rare -- then reads its own form below)
+        uint4 q[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = group_block_coefs8(A.coef8, (int64_t)tile * A.nb + b0, threadIdx.x)[i];
         const uint32_t rb = blk[b];
         const bool wide = (rb & 1u) != 0;
-        uint4 q[8];
         const int pb = prev_block_in_tile(b);
         const int d = (int)(int16_t)(rb >> 16) - (pb >= 0 ? (int)(int16_t)(blk[pb] >> 16) : 0);
         const int nbd = mag_bits(d);
@@ -1329,8 +1336,6 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
         // then the eight LDS reads in flight together
         if (!wide) {
             // an int8 block: its 64 bytes in registers, the walk unrolled
-#pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = group_block_coefs8(A.coef8, (int64_t)tile * A.nb + b0, threadIdx.x)[i];
 #pragma unroll
             for (int k0 = 0; k0 < 64; k0 += 8) {
                 uint32_t idx[8];
@@ -1347,17 +1352,26 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_block_bits(B2aArgs A) {
                 for (int j = 0; j < 8; ++j) bits += (k0 + j) ? len[idx[j]] : 0u;   // zero coefficient: entry 0
             }
         } else {
-            // an int16 block (an AC outside int8: rare): a rolled walk over its stored coefficients
-            const int16_t* cp = A.coefs + gb * 64;
+            // an int16 block (an AC outside int8: rare): eight coefficients per 16-byte load, the
+            // next load in flight while these are walked
+            const uint4* cp = group_block_coefs(A.coefs, (int64_t)tile * A.nb + b0, threadIdx.x);
+            uint4 v = cp[0];
 #pragma unroll 1
-            for (int k = 1; k < 64; ++k) {
-                const int nb = mag_bits(cp[k]);
-                bits += nb + len[r16 | nb];
-                r16 = nb ? 0u : r16 + 16;
+            for (int i = 0; i < 8; ++i) {
+                const uint4 nv = i < 7 ? cp[i + 1] : v;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    if (i == 0 && j == 0) continue;
+                    const uint32_t w = u4_at(v, j >> 1);
+                    const int nb = mag_bits((j & 1) ? (int)(int16_t)(w >> 16) : (int)(int16_t)(w & 0xFFFF));
+                    bits += nb + len[r16 | nb];
+                    r16 = nb ? 0u : r16 + 16;
+                }
+                v = nv;
             }
         }
         if (r16) bits += c_huff[1 + 2 * t].size[0x00];     // EOB after the last non-zero
-        A.bits[gb] = (uint16_t)bits;                       // bit count | 0x800 x ZRL-prefixed coefficients
+        A.bits[gb] = (uint16_t)(bits | (wide ? kWideFlag : 0u));   // bit count | 0x800 x ZRL-prefixed coefficients
         bits &= kZrlFlag - 1;
     }
     const uint32_t total = block_reduce_sum(bits, sw);
@@ -1449,7 +1463,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     const uint32_t mybits = brec & (kZrlFlag - 1);
     // no block of the wave has a zero run of 16+ before a non-zero (B2a's kZrlFlag multiples): the
     // walk below drops its per-coefficient ZRL vote
-    const bool any_zrl = __ballot(brec >= kZrlFlag) != 0;
+    const bool any_zrl = __ballot((brec & ~kWideFlag) >= kZrlFlag) != 0;
+    // B2a's copy of the block's int16 flag: which form to load is known before any coefficient
+    // load, so the loads need not wait for the block record
+    const bool wide = (brec & kWideFlag) != 0;
+    const bool any_wide = __ballot(wide) != 0;
     uint32_t gtot;
     const uint32_t gbit0 = A.goff[(int64_t)tile * A.ngb + blockIdx.x];
     const uint32_t boff = gbit0 + block_exclusive_scan(mybits, sw, gtot);
@@ -1469,13 +1487,11 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
     // block's shared first word ORed into HBM).
     // NARROW: every block of the wave is int8 (and no ZRL, staged): the walk reads bytes.
     // Otherwise int8 blocks are widened in registers and the wave walks the int16 form.
-    const uint32_t myrec = live ? A.blk[gb] : 0u;
-    const bool wide = (myrec & 1u) != 0;
-    const bool any_wide = __ballot(wide) != 0;
     auto code_block = [&](auto staged_c, auto narrow_c) {
         constexpr bool STAGED = decltype(staged_c)::value;
         constexpr bool NARROW = decltype(narrow_c)::value;
         const int64_t g0 = (int64_t)tile * A.nb + (int64_t)blockIdx.x * kGrp;
+        const uint32_t myrec = A.blk[gb];
         uint4 q[8];
         if (NARROW || !wide) {
 #pragma unroll
