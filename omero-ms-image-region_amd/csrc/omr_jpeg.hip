@@ -1161,20 +1161,23 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         }
         // one choice for the MCU's six blocks: an AC outside int8 in any of them (OR of the
         // biased values: a bit above bit 7 in any) makes all six int16
-        uint32_t big = 0;
+        uint64_t big = 0;                         // lanes holding an AC outside int8 (lane 0: the DC)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) big |= (uint32_t)(qv[k] + 128);
-        const uint32_t wide = __ballot(lane != 0 && big > 255u) != 0 ? 0x3Fu : 0u;   // bit k: block k int16
+        for (int k = 0; k < 6; ++k) big |= __ballot((uint32_t)(qv[k] + 128) > 255u);
+        const uint32_t wide = (big & ~1ull) != 0 ? 0x3Fu : 0u;   // bit k: block k int16
+        // the int16 form is one rarely taken, wave-uniform branch; the int8 stores are
+        // unconditional (an int16 MCU's bytes are never read)
+        if ((OMR_ABL & kAblCoefStore) == 0 && wide) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const int v = lane == 0 ? dc[k] : qv[k];
+                *reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(out) + (uint32_t)(k * 128 + lane * 2)) = (int16_t)v;
+            }
+        }
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
-            const int v = lane == 0 ? dc[k] : qv[k];
-            if constexpr ((OMR_ABL & kAblCoefStore) != 0) {
-                abl_sink ^= v;
-            } else if (wide) {
-                *reinterpret_cast<int16_t*>(reinterpret_cast<uint8_t*>(out) + (uint32_t)(k * 128 + lane * 2)) = (int16_t)v;
-            } else {
-                *reinterpret_cast<int8_t*>(reinterpret_cast<uint8_t*>(out8) + (uint32_t)(k * 64 + lane)) = (int8_t)qv[k];
-            }
+            if constexpr ((OMR_ABL & kAblCoefStore) != 0) abl_sink ^= qv[k];
+            else *reinterpret_cast<int8_t*>(reinterpret_cast<uint8_t*>(out8) + (uint32_t)(k * 64 + lane)) = (int8_t)qv[k];
         }
         // the six per-block DC records go to lanes 6j .. 6j+5 of `rec` (j: this MCU's index in
         // the wave's run); one store per wave after the loop instead of six one-lane stores per MCU
@@ -1212,9 +1215,7 @@ __global__ void __launch_bounds__(256) k_jpeg_fdct_batch(B1Args A) {
 // F1: fused render + B1 (see PlaneSource).  The contribution tables are staged once per
 // workgroup; a pixel outside its channel's LUT domain flags the tile (QuantizationException).
 template <int BPP, bool BE, int MODE, int NA>
-// The C2 headline instantiation (fast16 in f32) is held to 64 VGPRs: 8 waves per SIMD, no spill.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kFusedFast16F ? 8 : 1)))
-k_jpeg_render_fdct(B1Args A, FusedArgs F) {
+__global__ void __launch_bounds__(256) k_jpeg_render_fdct(B1Args A, FusedArgs F) {
     __shared__ int s[4][6 * kBS + 8];
     __shared__ uint32_t s_contrib[kFusedMaxActive * 256];
     for (int i = threadIdx.x; i < NA * 256; i += 256) s_contrib[i] = F.R.contrib[i];
