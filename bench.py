@@ -310,7 +310,7 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
     return res
 
 
-VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r03", "jpeg_valu_pmc.json")
+VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "jpeg_valu_pmc.json")
 VALU_PEAK_ISSUE_CYCLES_PER_S = 256 * 4 * 2.4e9   # 1,024 SIMD-32s at 2.4 GHz
 # issue cycles of one wave64 VALU instruction: 2 on a SIMD-32; f64 add / mul / fma issue at half
 # the f32 rate and transcendentals (v_exp / v_log / v_sqrt / v_rcp ...) at half the issue rate
@@ -347,7 +347,7 @@ def jpeg_measured_traffic(algo_bytes):
 
 def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
     """B1 / F1 / B3 are VALU-issue-bound: achieved = VALU issue cycles per launch
-    (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r03.sh, at 2 cycles,
+    (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r04.sh, at 2 cycles,
     plus 2 more for every f64 and transcendental instruction) x MCUs / the kernel's measured average
     duration; peak = every SIMD issuing every cycle at 2.4 GHz."""
     case = "c1" if name.startswith("c1") else "c2"

@@ -19,6 +19,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 #include <cerrno>
@@ -144,6 +145,7 @@ struct PixPipe {
     hipStream_t copy = nullptr;
     hipStream_t copy_b = nullptr;               // a second DMA queue (env OMR_PIXBUF_COPY_STREAMS=2)
     bool bands = true;                          // row-band copies (env OMR_PIXBUF_BANDS=0: per-tile rects)
+    size_t group_bytes = (size_t)64 << 20;      // planes per staging slot (env OMR_PIXBUF_GROUP_MB)
     explicit PixPipe(int threads) : pool(threads) {}
     ~PixPipe() {
         if (copy) (void)hipStreamSynchronize(copy);
@@ -174,6 +176,8 @@ static omr_status get_pipe(Ctx* c, PixPipe*& out) {
         if (ncs && std::atoi(ncs) >= 2) OMR_HIP(c, hipStreamCreateWithFlags(&p->copy_b, hipStreamNonBlocking));
         const char* nb = std::getenv("OMR_PIXBUF_BANDS");
         if (nb && std::atoi(nb) == 0) p->bands = false;
+        const char* gm = std::getenv("OMR_PIXBUF_GROUP_MB");
+        if (gm && std::atoi(gm) >= 8) p->group_bytes = (size_t)std::atoi(gm) << 20;
         for (int i = 0; i < 2; ++i)
             for (hipEvent_t* e : {&p->h2d[i], &p->rend[i], &p->d2h[i], &p->h2d_b[i]})
                 OMR_HIP(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -389,7 +393,7 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
     // one pread per row) of width x height per tile and channel into a compact plane.
     const bool bands = P->bands && (int64_t)pb->sx * pb->bpp == pb->row_bytes;
     const size_t band_bytes = align_up((size_t)height * (size_t)pb->row_bytes, 256);
-    const size_t budget = (size_t)64 << 20;   // planes per slot
+    const size_t budget = P->group_bytes;   // planes per slot
     struct Band {
         int32_t z, c, t, y, x0, x1;
     };
@@ -428,9 +432,19 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
                     tile_band[(size_t)i * na + a] = hit[a];
                 }
             }
+            // slots in file order, so bands adjacent in the file (the same plane's consecutive
+            // row bands, or whole planes) are adjacent in the slot too and go as one copy
+            std::vector<int32_t> ord(bl.size()), pos(bl.size());
+            for (size_t k = 0; k < bl.size(); ++k) ord[k] = (int32_t)k;
+            auto foff = [&](const Band& b) { return plane_offset(pb, b.z, b.c, b.t) + (int64_t)b.y * pb->row_bytes; };
+            std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return foff(bl[a]) < foff(bl[b]); });
+            std::vector<Band> sorted(bl.size());
+            for (size_t k = 0; k < bl.size(); ++k) { sorted[k] = bl[ord[k]]; pos[ord[k]] = (int32_t)k; }
+            for (int t = i0; t < i; ++t)
+                for (int a = 0; a < (int)act.size(); ++a) tile_band[(size_t)t * na + a] = pos[tile_band[(size_t)t * na + a]];
             gmax = std::max(gmax, i - i0);
-            in_need = std::max(in_need, bl.size() * band_bytes);
-            gbands.push_back(std::move(bl));
+            in_need = std::max(in_need, sorted.size() * band_bytes);
+            gbands.push_back(std::move(sorted));
         }
     } else {
         // ~64 MiB of compact planes per slot
@@ -510,18 +524,30 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
         } else if (bands) {
             OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes, hipMemcpyHostToDevice, P->copy));
             const std::vector<Band>& bl = gbands[g];
-            for (size_t k = 0; k < bl.size(); ++k) {
+            const size_t hb = (size_t)height * pb->row_bytes;
+            auto full = [&](const Band& b) { return b.x0 == 0 && b.x1 == pb->sx; };
+            for (size_t k = 0; k < bl.size();) {
                 const Band& b = bl[k];
-                const uint8_t* src = pb->map + plane_offset(pb, b.z, b.c, b.t) + (int64_t)b.y * pb->row_bytes;
+                const int64_t fo = plane_offset(pb, b.z, b.c, b.t) + (int64_t)b.y * pb->row_bytes;
+                const uint8_t* src = pb->map + fo;
                 uint8_t* dst = din + tab_bytes + band_bytes * k;
                 hipStream_t cs = (P->copy_b && (k & 1)) ? P->copy_b : P->copy;
-                if (b.x0 == 0 && b.x1 == pb->sx)   // the tiles cover the row: the band is contiguous
-                    OMR_HIP(ctx, hipMemcpyAsync(dst, src, (size_t)height * pb->row_bytes, hipMemcpyHostToDevice, cs));
-                else
+                if (full(b)) {   // the tiles cover the row: the band is contiguous, and so is a run of
+                                 // whole bands that follow each other in the file and in the slot
+                    size_t e = k + 1;
+                    while (e < bl.size() && band_bytes == hb && full(bl[e]) &&
+                           plane_offset(pb, bl[e].z, bl[e].c, bl[e].t) + (int64_t)bl[e].y * pb->row_bytes ==
+                               fo + (int64_t)(hb * (e - k)))
+                        ++e;
+                    OMR_HIP(ctx, hipMemcpyAsync(dst, src, hb * (e - k), hipMemcpyHostToDevice, cs));
+                    k = e;
+                    continue;
+                } else
                     OMR_HIP(ctx, hipMemcpy2DAsync(dst + (size_t)b.x0 * pb->bpp, (size_t)pb->row_bytes,
                                                   src + (size_t)b.x0 * pb->bpp, (size_t)pb->row_bytes,
                                                   (size_t)(b.x1 - b.x0) * pb->bpp, (size_t)height,
                                                   hipMemcpyHostToDevice, cs));
+                ++k;
             }
         } else if (direct) {
             // registered mapping: the copy engine reads each tile's rows from the page cache

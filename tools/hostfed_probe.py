@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Host-fed C2 render (omr_render_pixel_buffer_tiles, DMA from the registered ROMIO mapping or
 staged through pinned memory) per copy mode, alternated over rounds of >= 0.5 s each on one box:
-row bands (default), per-tile 2-D rects (OMR_PIXBUF_BANDS=0), bands on two copy queues
-(OMR_PIXBUF_COPY_STREAMS=2); 4096^2 4-channel uint16 file in /dev/shm, requests walking its 16
+row bands (default: 64 MiB staging groups, file-adjacent bands as one copy), per-tile 2-D rects
+(OMR_PIXBUF_BANDS=0), bands with 128 / 256 MiB groups (OMR_PIXBUF_GROUP_MB); 4096^2 4-channel uint16 file in /dev/shm, requests walking its 16
 tiles in raster order.  One JSON line."""
 import json
 import os
@@ -37,7 +37,8 @@ def main():
         out = torch.empty((n_req, T, T), dtype=torch.int32, device="cuda")
         ctxs = {}
         for name, env in (("bands", {}), ("tile_rects", {"OMR_PIXBUF_BANDS": "0"}),
-                          ("bands_2_queues", {"OMR_PIXBUF_COPY_STREAMS": "2"})):
+                          ("bands_group_128mib", {"OMR_PIXBUF_GROUP_MB": "128"}),
+                          ("bands_group_256mib", {"OMR_PIXBUF_GROUP_MB": "256"})):
             os.environ.update(env)
             ctxs[name] = omr.Context(0, torch_order=False)
             for k in env:
