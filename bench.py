@@ -1128,7 +1128,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-jpeg", action="store_true", help="skip the render->JPEG batch section")
     ap.add_argument("--jpeg-batch", type=int, default=256, help="tiles per JPEG step (the headline step size)")
-    ap.add_argument("--jpeg-steps", type=int, default=10)
+    ap.add_argument("--jpeg-steps", type=int, default=40)
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the C3 (projection) and C5 (float32 families, shape mask) sections")
     ap.add_argument("--no-latency", action="store_true",
