@@ -147,3 +147,28 @@ def test_jpeg_sweep_sizes_qualities(ctx, seed):
         assert got[i] == exp, f"batch tile {i} {w}x{h} q={q}"
     d = torch.from_numpy(tiles[0].reshape(-1).view(np.int32).copy()).to("cuda")
     assert ctx.encode_jpeg_device(d, w, h, q) == O.encode_jpeg(tiles[0], w, h, q), f"single {w}x{h} q={q}"
+
+
+def patchwork(h, w, seed, p_noise=0.3):
+    """16x16 patches of full-range noise among smooth ones: at high quality the noisy MCUs hold
+    ACs outside int8 (their blocks go out in the int16 form) next to int8 MCUs in the same wave."""
+    rng = np.random.default_rng(seed)
+    img = content("smooth", h, w, seed)
+    noise = content("noise", h, w, seed + 1)
+    for y in range(0, h, 16):
+        for x in range(0, w, 16):
+            if rng.random() < p_noise:
+                img[y:y + 16, x:x + 16] = noise[y:y + 16, x:x + 16]
+    return img
+
+
+@pytest.mark.parametrize("q", [1.0, 0.97, 0.9])
+@pytest.mark.parametrize("p_noise", [0.05, 0.3])
+def test_batch_int8_and_int16_blocks_in_one_wave(ctx, q, p_noise):
+    """B1 stores an MCU's blocks as int8 when every AC fits and as int16 otherwise; B2a walks each
+    form and B3 widens int8 blocks in waves that also hold int16 ones: files byte-identical."""
+    w, h = 256, 128
+    tiles = [patchwork(h, w, 77 + i, p_noise) for i in range(3)]
+    got = run_batch(ctx, tiles, w, h, q)
+    for i, t in enumerate(tiles):
+        assert got[i] == O.encode_jpeg(t, w, h, q), f"tile {i}"

@@ -290,3 +290,37 @@ def test_int16_fused_window_ends_at_the_int32_limits(ctx):
         files, st = _run(ctx, chans, tiles, _lib.PIXELS_INT16, w, h, qd_kw=qd_kw)
         assert st.tolist() == [0, 0]
         assert files == _expect(chans, tiles, _lib.PIXELS_INT16, w, h, qdef=make_qdef("rgb", **(qd_kw or {})))
+
+
+@pytest.mark.parametrize("q", [1.0, 0.95])
+def test_fused_int8_and_int16_blocks_in_one_wave(ctx, q):
+    """F1's per-MCU int8 / int16 choice on rendered pixels: 16x16 patches of full-range noise in
+    a smooth 8-bit plane, greyscale and colour, at qualities where the noisy MCUs need int16."""
+    rng = np.random.default_rng(31)
+    h, w, n = 128, 256, 2
+    yy, xx = np.mgrid[0:h, 0:w]
+    tiles = []
+    for t in range(n):
+        planes = []
+        for c in range(2):
+            p = ((xx * 255 // (w - 1) + yy + 40 * c + 7 * t) % 256).astype(np.uint8)
+            noise = rng.integers(0, 256, (h, w), dtype=np.uint8)
+            for y in range(0, h, 16):
+                for x in range(0, w, 16):
+                    if rng.random() < 0.3:
+                        p[y:y + 16, x:x + 16] = noise[y:y + 16, x:x + 16]
+            planes.append(p)
+        tiles.append(planes)
+    chans = [{"input_start": 0.0, "input_end": 255.0, "global_min": 0.0, "global_max": 255.0, "rgba": rgba}
+             for rgba in ((255, 0, 0, 255), (0, 255, 255, 255))]
+    for model in ("greyscale", "rgb"):
+        got, st = _run(ctx, chans, tiles, _lib.PIXELS_UINT8, w, h, q=q, model=model)
+        assert (st == 0).all()
+        assert got == _expect(chans, tiles, _lib.PIXELS_UINT8, w, h, q=q, model=model), model
+    # 16-bit planes (F1's fast16 modes), big-endian as ROMIO stores them
+    tiles16 = [[(p.astype(np.uint16) * 257 + 3).astype(">u2") for p in t] for t in tiles]
+    chans16 = [{"input_start": 300.0, "input_end": 64000.0, "global_min": 0.0, "global_max": 65535.0, "rgba": rgba}
+               for rgba in ((255, 0, 0, 255), (0, 255, 255, 255))]
+    got, st = _run(ctx, chans16, tiles16, _lib.PIXELS_UINT16, w, h, q=q, be=True)
+    assert (st == 0).all()
+    assert got == _expect(chans16, tiles16, _lib.PIXELS_UINT16, w, h, q=q, be=True)
