@@ -1049,6 +1049,10 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
     const int nat = c_zigzag[lane];                 // this lane owns zig-zag position `lane`
     const int qy = A.qt.q[0][nat], qc = A.qt.q[1][nat];
     const uint32_t my_ = A.qt.m[0][nat], mc_ = A.qt.m[1][nat];   // host-computed (no 64-bit divide)
+    // s_waitcnt vmcnt(0) once, here: the quantiser's per-lane table loads are then known complete,
+    // so the loop's first use of them does not wait for the pixel prefetches and coefficient
+    // stores issued since (vmcnt counts every load and store in issue order)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     const int hy = qy << 2, hc = qc << 2;
     // The workgroup's 4 * mpw MCUs are dealt round robin: at step j its four waves transform four
     // horizontally adjacent MCUs (m = base + 4j + wave), so each row's 4 x 32 bytes of 16-bit
@@ -1063,8 +1067,11 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         x += 4;
         while (x >= A.mcux) { x -= A.mcux; ++y; }
     };
-    auto fetch = [&](auto slot) {
-        src.template issue<decltype(slot)::value>(nx * 16 + 2 * cx, ny * 16 + 2 * cy);
+    // Every step issues its prefetch -- past the wave's last MCU it reloads the current one -- so
+    // the load / store stream is the same on every trip and the compiler's wait counts stay exact
+    // (a conditional prefetch made it wait for every outstanding load, the prefetch included).
+    auto fetch = [&](auto slot, bool valid) {
+        src.template issue<decltype(slot)::value>((valid ? nx : mx) * 16 + 2 * cx, (valid ? ny : my) * 16 + 2 * cy);
         step(nx, ny);
     };
     int abl_sink = 0;                             // ablation builds only: keeps dropped results live
@@ -1082,7 +1089,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             const int x0 = mx * 16 + 2 * cx;
             Px2 px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
             src.template take<SL>(px);
-            if (j + 2 < cnt) fetch(slot);
+            fetch(slot, j + 2 < cnt);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             const bool edge = Src::kEdgeRows && cyg >= chv;
@@ -1194,8 +1201,10 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
-    if (cnt > 0) fetch(S0{});
-    if (cnt > 1) fetch(S1{});
+    if (cnt > 0) {
+        fetch(S0{}, true);
+        fetch(S1{}, cnt > 1);
+    }
     for (int j = 0; j < cnt; j += 2) {   // wave-uniform loop, two steps per trip (static slots)
         mcu(S0{}, j);
         if (j + 1 < cnt) mcu(S1{}, j + 1);
