@@ -923,7 +923,8 @@ struct FusedArgs {
 
 template <int BPP, bool BE, int MODE, int NA>
 struct PlaneSource {
-    static constexpr bool kEdgeRows = false;  // fused tiles have H % 16 == 0
+    static constexpr bool kEdgeRows = false;  // fused tiles have W % 16 == H % 16 == 0: no edge
+                                              // replication and no dummy blocks
     const FusedArgs& F;
     const uint32_t* s_contrib;   // LDS [n_active][256]
     const uint8_t* base[kFusedMaxActive];
@@ -1145,7 +1146,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         for (int k = 0; k < 6; ++k) {
             int q = (k >= 4 && grey) ? 0                       // zero chroma block
                   : (OMR_ABL & kAblQuant) ? coef[k] : k < 4 ? quant_recip(coef[k], hy, my_) : quant_recip(coef[k], hc, mc_);
-            if (k < 4) {
+            if (Src::kEdgeRows && k < 4) {
                 const int bx = mx * 2 + (k & 1), by = my * 2 + (k >> 1);
                 if ((bx >= ywib || by >= yhib) && lane != 0) q = 0;   // dummy block: AC zero
             }
@@ -1160,7 +1161,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         int dc[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) dc[k] = __builtin_amdgcn_readfirstlane(qv[k]);
-        {
+        if constexpr (Src::kEdgeRows) {
             const bool c1 = mx * 2 + 1 >= ywib, row1 = my * 2 + 1 >= yhib;
             if (c1) dc[1] = dc[0];
             if (row1) { dc[2] = dc[1]; dc[3] = dc[1]; }
@@ -1171,7 +1172,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
         uint64_t big = 0;                         // lanes holding an AC outside int8 (lane 0: the DC)
 #pragma unroll
         for (int k = 0; k < 6; ++k) big |= __ballot((uint32_t)(qv[k] + 128) > 255u);
-        const uint32_t wide = (big & ~1ull) != 0 ? 0x3Fu : 0u;   // bit k: block k int16
+        const uint32_t wide = (big & ~1ull) != 0 ? 0x3Fu : 0u;   // bit k: block k int16 (all or none)
         // the int16 form is one rarely taken, wave-uniform branch; the int8 stores are
         // unconditional (an int16 MCU's bytes are never read)
         if ((OMR_ABL & kAblCoefStore) == 0 && wide) {
