@@ -1548,7 +1548,7 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
         }
         const uint32_t zrl = ((uint32_t)c_huff[1 + 2 * ta].size[0xF0] << 16) | c_huff[1 + 2 * ta].code[0xF0];
         const uint32_t eob = ((uint32_t)c_huff[1 + 2 * ta].size[0x00] << 16) | c_huff[1 + 2 * ta].code[0x00];
-        int r = 0;
+        int r16 = 0;                                  // zero run before coefficient k, times 16
         // Branch-free per coefficient: a zero contributes a zero-length code; runs of 16+ zeros
         // before a non-zero (ZRL) take a wave-uniform, rarely entered branch, checked only in
         // waves where B2a saw one.
@@ -1556,23 +1556,24 @@ __global__ void __launch_bounds__(kGrp) k_jpeg_huff_thread(B3Args A) {
 #pragma unroll
             for (int k = 1; k < 64; ++k) {
                 const int c = coef(k);
-                const bool nzk = c != 0;
+                const int nbits = mag_bits(c);                         // 0 for c == 0
+                const bool nzk = nbits != 0;                           // one compare on the category
                 if constexpr (decltype(with_zrl)::value) {
-                    if (k > 16 && __ballot(nzk && r > 15)) {                // r <= k - 1: no ZRL before k 17
-                        if (nzk) while (r > 15) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r -= 16; }
+                    if (k > 16 && __ballot(nzk && r16 > 15 * 16)) {        // r <= k - 1: no ZRL before k 17
+                        if (nzk) while (r16 > 15 * 16) { put(zrl & 0xFFFF, (int)(zrl >> 16)); r16 -= 16 * 16; }
                     }
                 }
-                const int nbits = mag_bits(c);                         // 0 for c == 0
-                const uint32_t cs = s_t.ac[ta][((r & 15) << 4) | nbits];
+                // (r & 15) << 4 is r16 & 0xF0: one v_and_or builds the table index
+                const uint32_t cs = s_t.ac[ta][(r16 & 0xF0) | nbits];
                 const uint32_t v = ((cs & 0xFFFF) << nbits) | ((uint32_t)(c < 0 ? c - 1 : c) & ((1u << nbits) - 1));
                 put(v, (int)(cs >> 16) + nbits);                        // c == 0: cs == 0, nbits == 0
-                r = nzk ? 0 : r + 1;
+                r16 = nzk ? 0 : r16 + 16;
             }
         };
         if constexpr (NARROW) walk(std::false_type{});
         else if (any_zrl) walk(std::true_type{});
         else walk(std::false_type{});
-        if (r > 0) put(eob & 0xFFFF, (int)(eob >> 16));                   // EOB
+        if (r16 > 0) put(eob & 0xFFFF, (int)(eob >> 16));                 // EOB
         if (nacc > 0) {                                                   // shared with the next block
             const uint32_t w = (uint32_t)(acc << (32 - nacc));
             if constexpr (STAGED) atomicOr(sp, w);
