@@ -868,6 +868,7 @@ constexpr int kBS = 72, kRS = 9;
 // current one is transformed); take<S>() hands them over at the start of that MCU.
 struct ArgbSource {
     static constexpr bool kEdgeRows = true;   // odd heights: the bottom chroma row replicates
+    static constexpr int kDepth = 2;          // MCUs of pixels in flight per wave
     const uint32_t* img;
     int W, H;
     bool even_w;
@@ -928,7 +929,17 @@ struct PlaneSource {
     const FusedArgs& F;
     const uint32_t* s_contrib;   // LDS [n_active][256]
     const uint8_t* base[kFusedMaxActive];
-    uint32_t raw[2][kFusedMaxActive][2];       // [prefetch slot][channel][row]
+    // Pixel prefetch depth (MCUs in flight per wave).  One MCU of cover is ~5 us per wave, far
+    // above the load latency; the second slot only costs VGPRs.  Two where that keeps the kernel
+    // at <= 64 VGPRs anyway (8 waves per SIMD either way: C1 1-ch u8 -1 % at depth 1), one where
+    // the second slot crosses 64: the four-channel table / linear / mixed / fast16-f32 forms
+    // (65-72 VGPRs at depth 2, 57-64 at depth 1; C2 fused 229.9k -> 234.2k tiles/s,
+    // profiles/r04/ab_jpeg_f1_prefetch_depth.txt).
+#ifndef OMR_F1_DEPTH
+#define OMR_F1_DEPTH (NA == kFusedMaxActive && MODE != kFusedFast16 && MODE != kFusedFast16I ? 1 : 2)
+#endif
+    static constexpr int kDepth = OMR_F1_DEPTH;
+    uint32_t raw[kDepth][kFusedMaxActive][2];  // [prefetch slot][channel][row]
     int W, H;
     bool err = false;
     __device__ PlaneSource(const FusedArgs& f, const uint32_t* sc, int tile, int w, int h)
@@ -1090,7 +1101,7 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             const int x0 = mx * 16 + 2 * cx;
             Px2 px[4];                                  // (x0, y0) (x0+1, y0) (x0, y0+1) (x0+1, y0+1)
             src.template take<SL>(px);
-            fetch(slot, j + 2 < cnt);
+            fetch(slot, j + Src::kDepth < cnt);
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             const bool edge = Src::kEdgeRows && cyg >= chv;
@@ -1202,13 +1213,18 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
-    if (cnt > 0) {
-        fetch(S0{}, true);
-        fetch(S1{}, cnt > 1);
-    }
-    for (int j = 0; j < cnt; j += 2) {   // wave-uniform loop, two steps per trip (static slots)
-        mcu(S0{}, j);
-        if (j + 1 < cnt) mcu(S1{}, j + 1);
+    if constexpr (Src::kDepth == 1) {
+        if (cnt > 0) fetch(S0{}, true);
+        for (int j = 0; j < cnt; ++j) mcu(S0{}, j);
+    } else {
+        if (cnt > 0) {
+            fetch(S0{}, true);
+            fetch(S1{}, cnt > 1);
+        }
+        for (int j = 0; j < cnt; j += 2) {   // wave-uniform loop, two steps per trip (static slots)
+            mcu(S0{}, j);
+            if (j + 1 < cnt) mcu(S1{}, j + 1);
+        }
     }
     if ((OMR_ABL & kAblLane0) == 0 && lane < 6 * cnt)
         A.blk[(int64_t)tile * A.nb + (int64_t)(mbase + 4 * (lane / 6) + wv) * 6 + lane % 6] = (uint32_t)rec;
