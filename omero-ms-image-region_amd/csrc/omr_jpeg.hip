@@ -1653,27 +1653,42 @@ struct B4aArgs {
 };
 
 __global__ void __launch_bounds__(kGrp) k_jpeg_stuff_count(B4aArgs A) {
-    __shared__ uint32_t sw[16];
+    // One wave per 256-chunk group, chunks lane, lane + 64, lane + 128, lane + 192 (each load
+    // instruction reads 1 KiB of contiguous stream; the four are issued before any is used), the
+    // group sum a wave reduction: no workgroup barrier (the workgroup's four waves take four groups).
     const int tile = blockIdx.y;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t tb = A.tile_bits[tile], nbytes = (tb + 7) / 8;
     const uint32_t nch = (nbytes + kStuffBytes - 1) / kStuffBytes;
     const uint32_t ng = (nch + kGrp - 1) / kGrp;
     if (blockIdx.x == 0 && threadIdx.x == 0) A.n_groups[tile] = ng;
-    const uint32_t* words = A.words + (int64_t)tile * A.slot_words;
-    for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
-        const uint32_t c = g * kGrp + threadIdx.x;
-        uint32_t n = 0;
-        if (c < nch) {
-            uint32_t w[4];
-            chunk_bytes(words, c, nbytes, tb, w);
-            const uint32_t e = min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes);
-            // four bytes at a time: exact 0xFF-byte detection, popcount of the valid ones
+    const uint4* words4 = reinterpret_cast<const uint4*>(A.words + (int64_t)tile * A.slot_words);
+    uint8_t* cnt = A.cnt + (int64_t)tile * A.slot_chunks;
+    for (uint32_t g = blockIdx.x * 4 + wv; g < ng; g += gridDim.x * 4) {
+        uint4 q[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) n += __popc(ff_bytes(w[q]) & first_bytes_mask((int)e - 4 * q));
-            A.cnt[(int64_t)tile * A.slot_chunks + c] = (uint8_t)n;
+        for (int k = 0; k < 4; ++k) q[k] = words4[min(g * kGrp + k * 64 + lane, nch - 1)];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = g * kGrp + k * 64 + lane;
+            uint32_t w[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+            const uint32_t last = nbytes - 1;
+            if ((tb & 7) && last >= c * kStuffBytes && last < (c + 1) * kStuffBytes) {   // jchuff pad bits
+                const uint32_t i = last - c * kStuffBytes;
+                w[i >> 2] |= (0xFFu >> (tb & 7)) << (24 - 8 * (i & 3));
+            }
+            const uint32_t e = c < nch ? min(nbytes - c * kStuffBytes, (uint32_t)kStuffBytes) : 0u;
+            // four bytes at a time: exact 0xFF-byte detection, popcount of the valid ones
+            uint32_t n = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) n += __popc(ff_bytes(w[j]) & first_bytes_mask((int)e - 4 * j));
+            if (c < nch) cnt[c] = (uint8_t)n;
+            tot += n;
         }
-        const uint32_t total = block_reduce_sum(n, sw);
-        if (threadIdx.x == 0) A.csum[(int64_t)tile * A.slot_groups + g] = total;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        if (lane == 0) A.csum[(int64_t)tile * A.slot_groups + g] = tot;
     }
 }
 
@@ -1762,7 +1777,7 @@ struct B6Args {
 // (nearly all of them) lands as five ORed LDS words, funnel-shifted to its byte offset; a chunk
 // with 0xFF bytes ORs its expanded bytes one by one.  (Per-byte stores from every lane at a
 // 16-byte lane stride had 40 % LDS bank-conflict cycles.)
-__global__ void __launch_bounds__(kGrp) k_jpeg_stuff_batch(B6Args A) {
+__global__ void __launch_bounds__(kGrp) __attribute__((amdgpu_waves_per_eu(8))) k_jpeg_stuff_batch(B6Args A) {
     constexpr int kSW = kGrp * kStuffBytes * 2 / 4;
     __shared__ uint32_t swords[kSW + 4];
     __shared__ uint32_t sw[16];
@@ -1963,7 +1978,7 @@ static omr_status encode_jpeg_batch_ws(Ctx* ctx, const uint32_t* d_argb, int64_t
         KernelTimer t(ctx, 6);
         hipLaunchKernelGGL(k_jpeg_huff_thread, dim3((unsigned)L.ngb, (unsigned)n), dim3(kGrp), 0, ctx->stream, a3);
     }
-    hipLaunchKernelGGL(k_jpeg_stuff_count, dim3((unsigned)est_groups, (unsigned)n), dim3(kGrp), 0, ctx->stream, a4);
+    hipLaunchKernelGGL(k_jpeg_stuff_count, dim3((unsigned)((est_groups + 3) / 4), (unsigned)n), dim3(kGrp), 0, ctx->stream, a4);
     hipLaunchKernelGGL(k_jpeg_group_scan, dim3((unsigned)n), dim3(kTileThreads), 0, ctx->stream, a4b);
     hipLaunchKernelGGL(k_jpeg_tile_scan, dim3(1), dim3(kTileThreads), 0, ctx->stream, a5);
     hipLaunchKernelGGL(k_jpeg_stuff_batch, dim3((unsigned)est_groups, (unsigned)n), dim3(kGrp), 0, ctx->stream, a6);
