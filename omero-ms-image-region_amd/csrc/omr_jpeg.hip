@@ -1004,12 +1004,49 @@ struct PlaneSource {
             return tab[v];
         }
     }
+#ifndef OMR_F1_PK
+#define OMR_F1_PK 1
+#endif
+    // fast16f on a pixel pair in packed f32: each 16-bit half becomes the float 2^23 + x by one
+    // v_perm (exponent byte 0x4B over the half's two bytes, big-endian swap included), one
+    // v_pk_add_f32 subtracts 2^23 + wsi (exact: integers below 2^24) and one v_pk_fma_f32 applies
+    // fa, fb -- the same floats and the same single rounding as fast16f's cvt + fma per pixel.
+    __device__ __forceinline__ void entry_pair_f32(int a, uint32_t w, uint32_t& lo, uint32_t& hi) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const uint32_t* tab = s_contrib + a * 256;
+        // w in file order: a big-endian half's first byte is its high byte
+        constexpr uint32_t kSelLo = BE ? 0x070C0001u : 0x070C0100u, kSelHi = BE ? 0x070C0203u : 0x070C0302u;
+        const f2 X = {__int_as_float((int)__builtin_amdgcn_perm(0x4B000000u, w, kSelLo)),
+                      __int_as_float((int)__builtin_amdgcn_perm(0x4B000000u, w, kSelHi))};
+        const float c = F.R.fc[a], fa = F.R.fa[a], fb = F.R.fb[a];
+        const f2 d = X - (f2){c, c};
+        const f2 y = __builtin_elementwise_fma(d, (f2){fa, fa}, (f2){fb, fb});
+        const int32_t b0 = __float_as_int(y.x), b1 = __float_as_int(y.y);
+        lo += tab[min(max(b0, kMagicBits), kMagicBits + 255) - kMagicBits];
+        hi += tab[min(max(b1, kMagicBits), kMagicBits + 255) - kMagicBits];
+    }
     template <int S>
     __device__ __forceinline__ void take(Px2 (&px)[4]) {
         uint32_t acc[4] = {0, 0, 0, 0};         // source order: (lo, hi) of row 0, then row 1
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             uint32_t w0 = raw[S][a][0], w1 = raw[S][a][1];
+            if constexpr (BPP == 2 && MODE == kFusedFast16F && OMR_F1_PK && (OMR_ABL & kAblRender) == 0) {
+                // packed form: the byte swap of big-endian pixels is folded into the v_perm that
+                // builds 2^23 + x, so the raw word stays in file order (the sign bias moves to
+                // each half's first byte)
+                const uint32_t sg = F.R.is_signed ? (BE ? 0x00800080u : 0x80008000u) : 0u;
+                w0 ^= sg;
+                w1 ^= sg;
+                if (F.R.any_check && F.R.ch[a].check) {      // wave-uniform
+                    const uint32_t n0 = BE ? bswap16x2(w0) : w0, n1 = BE ? bswap16x2(w1) : w1;
+                    const uint32_t hi2 = F.R.dhi2[a], lo2 = F.R.dlo2[a];
+                    err |= ((pk_max_u16(pk_max_u16(n0, n1), hi2) ^ hi2) | (pk_min_u16(pk_min_u16(n0, n1), lo2) ^ lo2)) != 0;
+                }
+                entry_pair_f32(a, w0, acc[0], acc[1]);
+                entry_pair_f32(a, w1, acc[2], acc[3]);
+                continue;
+            }
             if constexpr (BPP == 2) {
                 if constexpr (BE) { w0 = bswap16x2(w0); w1 = bswap16x2(w1); }
                 // int16 pixels biased to unsigned (x + 32768, one XOR per pixel pair); the host

@@ -126,6 +126,7 @@ struct FusedRender {
     int32_t ws_int;              // every window start is an integer (|ws| < 2^30): x - ws in int32
     int32_t f32;                 // Fast16 with every channel's (fa, fb) proven exact: kFusedFast16F
     float fa[kFusedMaxActive], fb[kFusedMaxActive];
+    float fc[kFusedMaxActive];   // 2^23 + wsi (exact: |wsi| <= 2^23): F1's packed form of x - wsi
     // 16-bit LUT domains of the checked channels in the kernel's (biased) pixel domain, clamped to
     // [0, 65535] and packed twice (lo | lo << 16) for v_pk_min/max_u16 compares; dnone: some
     // checked channel's domain holds no 16-bit value at all (every pixel fails)

@@ -1254,6 +1254,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         F.f32 = 1;
         for (int i = 0; i < na && F.f32; ++i)
             F.f32 = fast16_f32_params(F.ch[i].a0, F.ch[i].wsi, 65535, &F.fa[i], &F.fb[i]) ? 1 : 0;
+        for (int i = 0; i < na && F.f32; ++i) F.fc[i] = (float)((int64_t)(1 << 23) + F.ch[i].wsi);
     }
     F.contrib = d_contrib;
     F.plan = d_plan;

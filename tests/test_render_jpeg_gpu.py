@@ -324,3 +324,35 @@ def test_fused_int8_and_int16_blocks_in_one_wave(ctx, q):
     got, st = _run(ctx, chans16, tiles16, _lib.PIXELS_UINT16, w, h, q=q, be=True)
     assert (st == 0).all()
     assert got == _expect(chans16, tiles16, _lib.PIXELS_UINT16, w, h, q=q, be=True)
+
+
+@pytest.mark.parametrize("n_ch", [1, 3, 4])
+@pytest.mark.parametrize("be", [False, True])
+@pytest.mark.parametrize("pt", [_lib.PIXELS_UINT16, _lib.PIXELS_INT16])
+def test_fast16_f32_pairs_byte_order_sign_and_domain_check(ctx, pt, be, n_ch):
+    """F1's packed fast16-f32 render: each pixel pair becomes 2^23 + x by one v_perm per half
+    (the big-endian swap folded into its selector), then one packed subtract and one packed fma.
+    u16 and int16 (the sign bias on each half's first byte in file order), both byte orders,
+    1 / 3 / 4 channels with integral window starts, channel 0 with a LUT domain narrower than the
+    type (the domain check byte-swaps on its own), horizontal flip."""
+    w, h = 128, 64
+    rng = np.random.default_rng(41 + n_ch + 8 * be + 16 * (pt == _lib.PIXELS_INT16))
+    if pt == _lib.PIXELS_INT16:
+        lo, hi, dt = -32768, 32767, np.int16
+        starts, ends = (-20000, -500, 100, 3000), (25000.0, 9000.0, 30000.0, 32000.0)
+    else:
+        lo, hi, dt = 0, 65535, np.uint16
+        starts, ends = (0, 1000, 123, 40000), (65535.0, 20000.0, 5000.0, 65000.0)
+    tiles = [[rng.integers(lo, hi + 1, (h, w)).astype(dt) for _ in range(n_ch)] for _ in range(2)]
+    for t in tiles:                                   # channel 0 inside its narrower domain
+        np.clip(t[0], lo + 100, hi - 101, out=t[0])
+        t[0][3, 5], t[0][60, 127] = lo + 100, hi - 101
+    if be:
+        tiles = [[p.astype(p.dtype.newbyteorder(">")) for p in t] for t in tiles]
+    colours = [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255), (200, 100, 50, 255)]
+    chans = [{"input_start": f32(float(starts[k])), "input_end": f32(ends[k]),
+              "global_min": float(lo + 100 if k == 0 else lo), "global_max": float(hi - 101 if k == 0 else hi),
+              "rgba": colours[k]} for k in range(n_ch)]
+    files, st = _run(ctx, chans, tiles, pt, w, h, be=be, flip=(True, False))
+    assert st.tolist() == [0, 0]
+    assert files == _expect(chans, tiles, pt, w, h, be=be, flip=(True, False))
