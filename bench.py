@@ -320,7 +320,7 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32")
 
 
-JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04t.json")
+JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04u2.json")
 JPEG_FUSED_KERNELS = ("k_jpeg_render_fdct", "k_jpeg_block_bits", "k_jpeg_group_scan", "k_jpeg_huff_thread",
                       "k_jpeg_tile_scan", "k_jpeg_stuff_count", "k_jpeg_stuff_batch")
 
