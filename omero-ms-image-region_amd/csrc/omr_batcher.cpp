@@ -26,6 +26,9 @@ namespace omr {
 
 enum JobKind : int { kJobTile = 0, kJobProjection = 1, kJobMask = 2 };
 
+// Device bytes one projection sub-batch may take for its full planes (ARGB + encoder output).
+static constexpr size_t kProjectionBatchBytes = (size_t)2 << 30;
+
 struct Job {
     uint64_t ticket = 0;
     int kind = kJobTile;
@@ -53,6 +56,8 @@ struct omr_batcher {
     int device = 0;
     int max_batch = 64;
     int max_wait_us = 500;
+    int gap_us = 200;                        // arrival pause that closes a gather (<= max_wait_us)
+    std::chrono::steady_clock::time_point t_last_submit{};
     omr_ctx* ctx = nullptr;
     std::thread th;
     std::mutex m;
@@ -232,26 +237,46 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
     omr_ctx* c = B->ctx;
     const Job& j0 = *jobs[0];
     c->sem = j0.sem;      // the group's semantics (every job of a group has the same), dispatcher thread only
-    const int n = (int)jobs.size();
     const int W = j0.spec.width, H = j0.spec.height;
     const size_t px = (size_t)W * H;
-    std::vector<omr_tile_request> reqs(n);
-    for (int i = 0; i < n; ++i) reqs[i] = {jobs[i]->spec.z, jobs[i]->spec.t, jobs[i]->spec.x, jobs[i]->spec.y};
+    // A tile outside the image (the reference's DimensionsOutOfBoundsException from the pixel
+    // buffer) fails alone; the group renders the rest.
+    int32_t dims[6];
+    pixel_buffer_dims(j0.pb, dims);
+    out.assign(jobs.size(), Result{});
+    std::vector<int> live;
+    std::vector<omr_tile_request> reqs;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        const omr_tile_job& s = jobs[i]->spec;
+        if (s.z < 0 || s.z >= dims[2] || s.t < 0 || s.t >= dims[4] || s.x < 0 || s.y < 0 ||
+            (int64_t)s.x + W > dims[0] || (int64_t)s.y + H > dims[1]) {
+            out[i].st = OMR_INVALID_ARGUMENT;
+            out[i].err = "tile outside the image";
+            continue;
+        }
+        live.push_back((int)i);
+        reqs.push_back({s.z, s.t, s.x, s.y});
+    }
+    const int n = (int)live.size();
+    if (!n) return OMR_OK;
     omr_status st = grow_dev(B, px * 4 * n, 0, n);
     if (st) return st;
     st = render_pixel_buffer_tiles(c, j0.pb, &j0.qdef, j0.ch.data(), (int32_t)j0.ch.size(), reqs.data(), n, W, H,
                                    j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1, B->d_rstat);
     if (st) return st;
-    out.assign(n, Result{});
+    std::vector<Result> sub(n);
     std::vector<int32_t> rstat(n);
     OMR_HIP(c, hipMemcpyAsync(rstat.data(), B->d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
     OMR_HIP(c, hipStreamSynchronize(c->stream));
     for (int i = 0; i < n; ++i)
         if (rstat[i]) {
-            out[i].st = rstat[i];
-            out[i].err = "pixel value outside the quantization LUT domain";
+            sub[i].st = rstat[i];
+            sub[i].err = "pixel value outside the quantization LUT domain";
         }
-    return encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, out);
+    st = encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, sub);
+    if (st) return st;
+    for (int i = 0; i < n; ++i) out[live[i]] = std::move(sub[i]);
+    return OMR_OK;
 }
 
 // The cache slot of stack (serial, c, t): *resident = true when it is already in HBM; otherwise a
@@ -303,6 +328,18 @@ static uint8_t* stack_slot(omr_batcher* B, uint64_t serial, int32_t c, int32_t t
     return reuse;
 }
 
+// A stack whose upload failed leaves the cache: its slot never held the (serial, c, t) planes, so a
+// later request for them must upload (and fail or succeed) again rather than read stale HBM.
+static void stack_drop(omr_batcher* B, const uint8_t* d) {
+    for (size_t k = 0; k < B->stacks.size(); ++k)
+        if (B->stacks[k].d == d) {
+            B->stack_resident = B->stack_resident.load() - B->stacks[k].bytes;
+            (void)hipFree(B->stacks[k].d);
+            B->stacks.erase(B->stacks.begin() + (long)k);
+            return;
+        }
+}
+
 // Projection jobs of one group (same image, settings, projection, flips, format): for each
 // distinct t the active channels' Z-stacks go to HBM (DMA from the registered ROMIO mapping),
 // omr_render_projected_device projects and renders the full plane (the glue,
@@ -343,14 +380,23 @@ static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& 
     std::vector<const void*> stacks(SC, nullptr);
     for (int i = 0; i < n; ++i) {
         const int t = jobs[i]->spec.t;
+        if (t < 0 || t >= dims[4]) {                           // checked before any cache slot is taken
+            out[i].st = OMR_INVALID_ARGUMENT;
+            out[i].err = "projection t outside the image";
+            continue;
+        }
         const uint64_t tick = ++B->stack_tick;
         for (size_t a = 0; a < act.size() && !st; ++a) {
             bool resident = false;
             uint8_t* d = stack_slot(B, serial, act[a], t, stack_bytes, tick, &resident, &st);
             if (st) break;
+            const bool cached = d != nullptr;
             if (!d && (st = scratch(a, &d))) break;              // larger than the cache: scratch
             stacks[act[a]] = d;
-            if (!resident) st = pixel_buffer_upload_stack(c, j0.pb, act[a], t, d);
+            if (!resident) {
+                st = pixel_buffer_upload_stack(c, j0.pb, act[a], t, d);
+                if (st && cached) stack_drop(B, d);
+            }
         }
         if (!st)
             st = omr_render_projected_device(c, &j0.qdef, j0.ch.data(), SC, stacks.data(), PT, 1, W, H, Z,
@@ -376,7 +422,12 @@ static omr_status run_mask_group(omr_batcher* B, const std::vector<Job*>& jobs, 
     size_t cap = 0;
     for (int i = 0; i < n; ++i) {
         mj[i] = jobs[i]->mask;
-        if (mj[i].width > 0 && mj[i].height > 0) cap += omr_png_batch_max_bytes(mj[i].width, mj[i].height, 1, 1);
+        // room only for masks the batch will encode: the ones it answers 404 (the single call's
+        // checks) take none, so declared dimensions alone cannot size the buffer
+        const int64_t npx = (int64_t)mj[i].width * mj[i].height;
+        if (mj[i].width > 0 && mj[i].height > 0 && npx <= INT32_MAX && mj[i].bits &&
+            (int64_t)mj[i].n_bytes * 8 >= npx)
+            cap += omr_png_batch_max_bytes(mj[i].width, mj[i].height, 1, 1);
     }
     std::vector<uint8_t> buf(std::max<size_t>(cap, 16));
     std::vector<uint64_t> offs(n);
@@ -400,9 +451,19 @@ static void dispatch_loop(omr_batcher* B) {
     for (;;) {
         B->cv_in.wait(lk, [&] { return B->stop || !B->pending.empty(); });
         if (B->pending.empty() && B->stop) return;
-        // gather: up to max_batch jobs, or what arrives within max_wait_us of the oldest one
-        const auto deadline = B->pending.front()->t_submit + std::chrono::microseconds(B->max_wait_us);
-        B->cv_in.wait_until(lk, deadline, [&] { return B->stop || (int)B->pending.size() >= B->max_batch; });
+        // gather: up to max_batch jobs, what arrives within max_wait_us of the oldest one, or --
+        // whichever comes first -- until the arrivals pause for gap_us.  The device is idle while
+        // the dispatcher gathers, so a burst (a viewer's screenful, the clients answered by the last
+        // round) is taken as soon as it has landed instead of after the whole max_wait_us.
+        for (;;) {
+            if (B->stop || (int)B->pending.size() >= B->max_batch) break;
+            const auto now = std::chrono::steady_clock::now();
+            const auto deadline =
+                std::min(B->pending.front()->t_submit + std::chrono::microseconds(B->max_wait_us),
+                         B->t_last_submit + std::chrono::microseconds(B->gap_us));
+            if (now >= deadline) break;
+            B->cv_in.wait_until(lk, deadline);
+        }
         std::vector<std::unique_ptr<Job>> take;
         const size_t nt = std::min(B->pending.size(), (size_t)B->max_batch);
         for (size_t i = 0; i < nt; ++i) take.push_back(std::move(B->pending[i]));
@@ -428,8 +489,12 @@ static void dispatch_loop(omr_batcher* B) {
                 } else if (kind == kJobProjection) {
                     append(key, &s.t, sizeof(s.t));
                 } else {
+                    // the caller's byte count and null-ness too: an empty mask (padded to one zero
+                    // byte) must not share the result of a real 1-byte zero mask
+                    const int64_t nb = jb.mask.bits ? (int64_t)jb.mask.n_bytes : -1;
                     const int32_t m4[4] = {jb.mask.width, jb.mask.height, jb.mask.flip_h, jb.mask.flip_v};
                     append(key, m4, sizeof(m4));
+                    append(key, &nb, sizeof(nb));
                     append(key, jb.mask.rgba, 4);
                     append(key, jb.mask_bits.data(), jb.mask_bits.size());
                 }
@@ -445,12 +510,28 @@ static void dispatch_loop(omr_batcher* B) {
             }
             std::vector<Result> out;
             omr_status st = OMR_OK;
-            for (size_t b0 = 0; b0 < uniq.size() && st == OMR_OK; b0 += (size_t)B->max_batch) {
-                std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + std::min(uniq.size(), b0 + B->max_batch));
+            size_t chunk = (size_t)B->max_batch;
+            if (kind == kJobProjection) {
+                // full planes: ARGB (px*4) + the batched JPEG's reservation (px*4 + 64 KiB) per plane,
+                // kept under a fixed budget so a large image splits into sub-batches instead of
+                // failing the whole group with OMR_OOM
+                int32_t dims[6];
+                pixel_buffer_dims(uniq[0]->pb, dims);
+                const size_t per = (size_t)dims[0] * dims[1] * 8 + 65536;
+                chunk = std::max<size_t>(1, std::min(chunk, kProjectionBatchBytes / per));
+            }
+            for (size_t b0 = 0; b0 < uniq.size() && st == OMR_OK; b0 += chunk) {
+                std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + std::min(uniq.size(), b0 + chunk));
                 std::vector<Result> po;
-                st = kind == kJobTile ? run_group(B, part, po)
-                   : kind == kJobProjection ? run_projection_group(B, part, po)
-                                            : run_mask_group(B, part, po);
+                try {
+                    st = kind == kJobTile ? run_group(B, part, po)
+                       : kind == kJobProjection ? run_projection_group(B, part, po)
+                                                : run_mask_group(B, part, po);
+                } catch (const std::bad_alloc&) {     // host memory: this group fails, the server lives
+                    st = fail(B->ctx, OMR_OOM, "host allocation failed in the batcher");
+                } catch (const std::exception& e) {
+                    st = fail(B->ctx, OMR_INTERNAL, std::string("batcher: ") + e.what());
+                }
                 for (auto& r : po) out.push_back(std::move(r));
             }
             rendered += uniq.size();
@@ -492,6 +573,8 @@ omr_status omr_batcher_create(int32_t device, int32_t max_batch, int32_t max_wai
         return st;
     }
     if (const char* v = std::getenv("OMR_STACK_CACHE_MB")) B->stack_cache_max = (int64_t)std::atoll(v) << 20;
+    B->gap_us = std::min(max_wait_us, 200);
+    if (const char* v = std::getenv("OMR_BATCH_GAP_US")) B->gap_us = std::max(0, std::min(max_wait_us, std::atoi(v)));
     B->th = std::thread(dispatch_loop, B);
     *out = B;
     return OMR_OK;
@@ -522,6 +605,7 @@ static void enqueue(omr_batcher* B, std::unique_ptr<Job> j, uint64_t* ticket) {
         j->group_key = settings_key(*j);  // reach a job already queued or a group in flight
         j->ticket = B->next_ticket++;
         *ticket = j->ticket;
+        B->t_last_submit = j->t_submit;
         B->pending.push_back(std::move(j));
         B->n_jobs++;
         B->outstanding++;

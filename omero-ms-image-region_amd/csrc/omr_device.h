@@ -9,7 +9,7 @@ namespace omr {
 
 // Java Math.round(double) (JDK 8): floor(a + 0.5) with the 0.49999999999999994 case,
 // then (long) conversion (NaN -> 0, saturating).
-__device__ __forceinline__ int64_t java_round_d(double a) {
+__host__ __device__ __forceinline__ int64_t java_round_d(double a) {
     if (a == 0x1.fffffffffffffp-2) return 0;
     const double f = floor(a + 0.5);
     if (f != f) return 0;
@@ -19,7 +19,7 @@ __device__ __forceinline__ int64_t java_round_d(double a) {
 }
 
 // Family maps (SEMANTICS TABLE S2 in oracle/omr_oracle.c) of a channel.
-__device__ __forceinline__ double family_map(const ChanParam& p, double x) {
+__host__ __device__ __forceinline__ double family_map(const ChanParam& p, double x) {
     return family_map_code(p.family, x, p.k, p.ws, p.we);
 }
 
@@ -27,7 +27,7 @@ __device__ __forceinline__ double family_map(const ChanParam& p, double x) {
 // stages (S3/S4).  The window ends are the integer thresholds p.lo / p.hi the host derived from
 // the double window under the OMR_SEM_WINDOW_INT_BOUNDS choice (x < ws <=> x < ceil(ws) for
 // integer x by default; x < (int)ws with the switch).
-__device__ __forceinline__ int quantize_eval(double x, const ChanParam& p, int cds, int cde) {
+__host__ __device__ __forceinline__ int quantize_eval(double x, const ChanParam& p, int cds, int cde) {
     if (x < (double)p.lo) return cds & 0xFF;
     if (x >= (double)p.hi) return cde & 0xFF;
     if (p.nr) {

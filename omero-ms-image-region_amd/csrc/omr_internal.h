@@ -73,6 +73,7 @@ struct ChanParam {
     float cratio[3];    // c/255f     (OMR_SEM_ALPHA_SEPARATE)
     float pad1;
     uint64_t lut_off;   // byte offset of this channel's quantization LUT in the workspace
+    uint8_t qtab[256];  // kModeTable8: q of raw byte t, built on the host (host libm, exact)
     uint8_t lut_rgb[768];  // LutReader colours (valid when has_lut)
 };
 

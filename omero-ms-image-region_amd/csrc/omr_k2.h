@@ -102,7 +102,7 @@ __device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__
     if (p.mode == kModeTable8) {
         const int value = is_signed8 ? (int)(int8_t)(uint8_t)t : t;
         if (value < p.gmin || value > p.gmax) return kErrBit;
-        const int v = quantize_eval((double)value, p, cds, cde);
+        const int v = p.qtab[t];                      // q(value), from the host (prepare_plan)
         return pack_contrib(p, v, cds, cde, plan->greyscale, plan->sem);
     }
     return pack_contrib(p, t, cds, cde, plan->greyscale, plan->sem);

@@ -1471,7 +1471,7 @@ struct PngBatch {
     const PngImg* img;
     int32_t n, uniform;                         // uniform: every image has the same geometry
     int32_t rblk_per, pblk_per, grp_per, eblk_per, cblk_per;   // per-image counts when uniform
-    int32_t total_grp, pad;
+    int32_t total_grp, fw_bands;                // fw_bands: row bands per image of the wave-form D1
     const int32_t* rblk0;                       // [n] first D1 workgroup etc. (binary search when not uniform)
     const int32_t* pblk0;
     const int32_t* grp0;
@@ -1537,6 +1537,136 @@ __global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
     const int y0 = ((int)blockIdx.x - (B.uniform ? i * B.rblk_per : I.rblk0)) * kPngRowsPerWg;
     png_filter_rows(pngb_args(I), I.bpp, y0, min(kPngRowsPerWg, I.H - y0), B.flt + I.flt,
                     B.row_sums + 2 * ((int64_t)I.row0 + y0), s_rows);
+}
+
+// D1, wave form (round 5): for a uniform batch of RGB images with W % 4 == 0 and W <= 1024 (the
+// rendered tiles), one wave filters a band of kFilterBandRows rows.  Lane l holds pixel quads
+// q = l + 64 m (4 px = 3 dwords of RGB, one coalesced 16-byte load), the row above stays in
+// registers from the previous row, the left neighbours come from lane l - 1 (or lane 63 of quad
+// block m - 1) by a lane shift, the five residual sums reduce inside the wave -- no LDS, no
+// workgroup barrier.  The chosen row leaves as aligned dwords (alignbyte of two neighbouring
+// residual dwords; the filter byte and the partial dwords shared with the neighbouring rows byte
+// by byte) and the band's Adler partials go to its first row's slot (the others 0: P5 sums every
+// row).  Same filter choice (minimum sum of |residual|, lowest filter on ties) and bytes as
+// png_filter_rows.
+constexpr int kFilterBandRows = 8;
+
+template <int M>
+__global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = (int)(wid / B.fw_bands);
+    if (i >= B.n) return;
+    const PngImg& I = B.img[i];
+    const int y0 = (int)(wid - (int64_t)i * B.fw_bands) * kFilterBandRows;
+    const int y1 = min(I.H, y0 + kFilterBandRows);
+    const int W = I.W, nq = W >> 2, rb = 3 * W;
+    const uint32_t* __restrict__ argb = I.argb;
+    uint8_t* __restrict__ flt = B.flt + I.flt;
+    const int64_t rowlen = I.rowlen, raw = I.raw;
+    uint32_t pv[M][3], cv[M][3];
+    auto load_row = [&](int y, uint32_t (&d)[M][3]) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int q = lane + 64 * m;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (y >= 0 && q < nq) v = reinterpret_cast<const uint4*>(argb + (int64_t)y * W)[q];
+            d[m][0] = __builtin_amdgcn_perm(v.y, v.x, 0x06000102u);       // r0 g0 b0 r1
+            d[m][1] = __builtin_amdgcn_perm(v.z, v.y, 0x05060001u);       // g1 b1 r2 g2
+            d[m][2] = __builtin_amdgcn_perm(v.w, v.z, 0x04050600u);       // b2 r3 g3 b3
+        }
+    };
+    load_row(y0 - 1, pv);
+    unsigned long long s1 = 0, s2 = 0;
+    for (int y = y0; y < y1; ++y) {
+        load_row(y, cv);
+        uint32_t rr[5][M][3];
+        uint32_t sm[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            // the dword left of this quad: the previous quad's third dword (0 left of the row)
+            const uint32_t wx = m ? __shfl(cv[m - 1][2], 63, 64) : 0u;
+            const uint32_t wp = m ? __shfl(pv[m - 1][2], 63, 64) : 0u;
+            uint32_t lx = __shfl_up(cv[m][2], 1, 64), lp = __shfl_up(pv[m][2], 1, 64);
+            lx = lane ? lx : wx;
+            lp = lane ? lp : wp;
+            const bool live = lane + 64 * m < nq;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t X = cv[m][k], Bv = pv[m][k];
+                const uint32_t Av = __builtin_amdgcn_alignbyte(X, k ? cv[m][k - 1] : lx, 1);
+                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, k ? pv[m][k - 1] : lp, 1);
+                uint32_t r[5];
+                png_residuals(X, Av, Bv, Cv, r);
+#pragma unroll
+                for (int f = 0; f < 5; ++f) {
+                    rr[f][m][k] = r[f];
+                    sm[f] = live ? abs_sum8(r[f], sm[f]) : sm[f];
+                }
+            }
+        }
+        int f = 0;
+        uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            uint32_t v = sm[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (v < best) { best = v; f = k; }                 // wave-uniform
+        }
+        const int64_t ypos = (int64_t)y * rowlen;              // the row's offset in the stream
+        const int64_t row0 = I.flt + ypos;                     // ... and in B.flt (16-aligned base)
+        const int u = (int)((-row0 - 1) & 3);                  // residual byte at an aligned address
+        uint32_t c[M][3];
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                c[m][k] = f == 0 ? rr[0][m][k] : f == 1 ? rr[1][m][k] : f == 2 ? rr[2][m][k]
+                        : f == 3 ? rr[3][m][k] : rr[4][m][k];
+        uint32_t* gw = reinterpret_cast<uint32_t*>(B.flt + row0 + u + 1);   // aligned: out dword J
+        const int jfull = (rb - u) >> 2;                       // out dwords J < jfull lie inside the row
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int q = lane + 64 * m;
+            uint32_t nx = __shfl_down(c[m][0], 1, 64);          // the next quad's first dword
+            const uint32_t wn = m + 1 < M ? __shfl(c[m + 1][0], 0, 64) : 0u;
+            nx = lane == 63 ? wn : nx;
+            if (q < nq) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int J = 3 * q + k;
+                    const uint32_t w = c[m][k];
+                    const uint32_t hi = k < 2 ? c[m][k + 1] : (q + 1 < nq ? nx : 0u);
+                    if (J < jfull) gw[J] = __builtin_amdgcn_alignbyte(hi, w, u);
+                    const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
+                    s1 += sv;
+                    s2 += (unsigned long long)(raw - ypos - 4 * J - 1) * sv - __builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
+                    // bytes outside the whole out dwords: the row's first u, the last (rb - u) & 3
+                    for (int b = 0; b < 4; ++b) {
+                        const int t = 4 * J + b;
+                        if (t < u || t >= u + 4 * jfull) flt[ypos + 1 + t] = (uint8_t)byte_at(w, b);
+                    }
+                }
+            }
+        }
+        if (lane == 0) {
+            flt[ypos] = (uint8_t)f;
+            s1 += (unsigned long long)f;
+            s2 += (unsigned long long)(raw - ypos) * (unsigned long long)f;
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) pv[m][k] = cv[m][k];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+    }
+    unsigned long long* rs = B.row_sums + 2 * ((int64_t)I.row0 + y0);
+    if (lane < 2 * (y1 - y0)) rs[lane] = lane == 0 ? s1 : lane == 1 ? s2 : 0ull;
 }
 
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
@@ -1840,6 +1970,49 @@ __global__ void __launch_bounds__(256) k_pngb_emit(PngBatch B) {
     *reinterpret_cast<uint4*>(B.out + M.off + k0) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// P9 tables (round 5): braid[b][v] = raw CRC of byte v at position b of a 4-byte word followed
+// by 255 - b zero bytes (the state then sits at the same lane's next word, 256 bytes on: zlib's
+// "braided" CRC with 64 lanes of one word); last[b][v] the same without the trailing 252 bytes
+// (slicing-by-4: the state at the end of the word); lane[k] = x^(32 (63 - k)) mod P, the shift
+// from lane k's last word end to the end of its strip.
+struct CrcBraid {
+    uint32_t braid[4][256];
+    uint32_t last[4][256];
+    uint32_t lane[64];
+};
+
+constexpr CrcBraid make_crc_braid() {
+    CrcBraid c{};
+    uint32_t t[256] = {};                      // t[n]: CRC of byte n followed by k zero bytes
+    for (uint32_t n = 0; n < 256; ++n) {
+        uint32_t r = n;
+        for (int k = 0; k < 8; ++k) r = (r & 1) ? kCrcPoly ^ (r >> 1) : r >> 1;
+        t[n] = r;
+    }
+    uint32_t t0[256] = {};
+    for (int n = 0; n < 256; ++n) t0[n] = t[n];
+    for (int k = 0; k <= 255; ++k) {           // t = k zero bytes after the byte
+        for (int b = 0; b < 4; ++b) {
+            if (k == 3 - b)
+                for (int n = 0; n < 256; ++n) c.last[b][n] = t[n];
+            if (k == 255 - b)
+                for (int n = 0; n < 256; ++n) c.braid[b][n] = t[n];
+        }
+        for (int n = 0; n < 256; ++n) t[n] = (t[n] >> 8) ^ t0[t[n] & 0xFF];
+    }
+    uint32_t x32 = 1u << 31;                   // x^0
+    uint32_t x8 = 1u << 30;                    // x^1 -> x^8 by squaring three times
+    for (int i = 0; i < 3; ++i) x8 = multmodp_c(x8, x8);
+    const uint32_t x32step = multmodp_c(multmodp_c(x8, x8), multmodp_c(x8, x8));   // x^32
+    for (int k = 63; k >= 0; --k) {            // lane[63] = x^0, lane[62] = x^32, ...
+        c.lane[k] = x32;
+        x32 = multmodp_c(x32step, x32);
+    }
+    return c;
+}
+
+__constant__ CrcBraid c_braid = make_crc_braid();
+
 __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {   // unaligned 32-bit load
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
@@ -1848,44 +2021,60 @@ __device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {   // unalig
     return sh ? (w0 >> sh) | (q[1] << (32 - sh)) : w0;
 }
 
-// P9: CRC-32 of 'IDAT' + zlib stream (4 + zlen bytes) in the output.  Lane j (per image) owns the
-// 256 bytes ending 256*j bytes before the end: its CRC times x^(8*256*j) (two table products)
-// is its share of the whole CRC (the init / final XOR terms telescope), XOR-combined per image.
+// P9: CRC-32 of 'IDAT' + zlib stream (n = 4 + zlen bytes of the output file).  Each wave owns a
+// strip of kCrcStrip bytes, strips counted back from the end of the range (strip g ends g strips
+// before it; the first strip may start before the range, those bytes read as 0, which leaves a
+// zero-initialised CRC unchanged).  Lane k reads the word at strip + 256 j + 4 k (a wave reads 256
+// contiguous bytes per step: coalesced) and keeps a braided state (braid tables); the last step
+// leaves lane k's state at its word end, the lane constant shifts it to the strip end, the wave
+// XOR-reduces, and lane 0 shifts the strip's CRC to the range end (x^(8 * kCrcStrip * g)) and
+// XORs it into the file's CRC.  The init / final inversions add ~(x^(8n) * 0xFFFFFFFF) once.
+constexpr int kCrcStrip = 64 * 256;            // bytes per wave (64 steps of 256)
+static_assert(kPngbCrcBytes == 4 * kCrcStrip, "P9: four strips per workgroup");
+
 __global__ void __launch_bounds__(256) k_pngb_crc(PngBatch B) {
-    __shared__ uint32_t t[8][256];
-    __shared__ uint32_t s_x[4];
-    for (int k = threadIdx.x; k < 8 * 256; k += 256) t[k >> 8][k & 255] = c_crc8.t[k >> 8][k & 255];
+    __shared__ uint32_t sb[4][256], sl[4][256];
+    for (int k = threadIdx.x; k < 4 * 256; k += 256) {
+        sb[k >> 8][k & 255] = c_braid.braid[k >> 8][k & 255];
+        sl[k >> 8][k & 255] = c_braid.last[k >> 8][k & 255];
+    }
     __syncthreads();
     const int i = pngb_image(B, B.cblk0, B.cblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const PngMeta& M = B.meta[i];
     if (M.off < 0) return;
-    const int64_t lb = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.cblk_per : I.cblk0);
-    const int64_t j = lb * 256 + threadIdx.x;
-    const int64_t n = 4 + M.zlen, hi = n - 256 * j, lo = max((int64_t)0, hi - 256);
-    uint32_t v = 0;
-    if (hi > 0) {
-        const uint8_t* d = B.out + M.off + I.pre_len + 4;
-        uint32_t r = 0xFFFFFFFFu;
-        int64_t q = lo;
-        for (; q + 8 <= hi; q += 8) {
-            const uint32_t w0 = load_u32_any(d + q) ^ r, w1 = load_u32_any(d + q + 4);
-            r = t[7][w0 & 0xFF] ^ t[6][(w0 >> 8) & 0xFF] ^ t[5][(w0 >> 16) & 0xFF] ^ t[4][w0 >> 24] ^
-                t[3][w1 & 0xFF] ^ t[2][(w1 >> 8) & 0xFF] ^ t[1][(w1 >> 16) & 0xFF] ^ t[0][w1 >> 24];
+    const int lane = threadIdx.x & 63;
+    const int64_t g = ((int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.cblk_per : I.cblk0)) * 4 + (threadIdx.x >> 6);
+    const int64_t n = 4 + M.zlen;
+    const int64_t s0 = n - kCrcStrip * (g + 1);           // strip start, relative to the range
+    if (s0 + kCrcStrip <= 0) return;                      // wave-uniform: past the range's start
+    const uint8_t* base = B.out + M.off + I.pre_len + 4;
+    uint32_t q = 0;
+    for (int j = 0; j < 64; ++j) {
+        const int64_t rel = s0 + 256 * j + 4 * lane;
+        uint32_t w = 0;
+        if (rel >= 0) {
+            w = load_u32_any(base + rel);
+        } else if (rel > -4) {
+            w = load_u32_any(base + rel) & (0xFFFFFFFFu << (8 * (int)(-rel)));   // bytes before the range: 0
         }
-        for (; q < hi; ++q) r = t[0][(r ^ d[q]) & 0xFF] ^ (r >> 8);
-        v = ~r;
-        if (j) {
-            v = multmodp(B.crc_pow[j & (kCrcPowLo - 1)], v);
-            if (j >= kCrcPowLo) v = multmodp(B.crc_pow[kCrcPowLo + (j / kCrcPowLo)], v);
+        const uint32_t x = q ^ w;
+        if (j < 63) {
+            q = sb[0][x & 255] ^ sb[1][(x >> 8) & 255] ^ sb[2][(x >> 16) & 255] ^ sb[3][x >> 24];
+        } else {
+            q = sl[0][x & 255] ^ sl[1][(x >> 8) & 255] ^ sl[2][(x >> 16) & 255] ^ sl[3][x >> 24];
         }
     }
+    uint32_t v = q ? multmodp(c_braid.lane[lane], q) : 0u;
     for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0) s_x[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t x = s_x[0] ^ s_x[1] ^ s_x[2] ^ s_x[3];
-        if (x) atomicXor(&B.meta[i].crc, x);
+    if (lane == 0) {
+        const uint64_t jj = (uint64_t)g * (kCrcStrip / 256);   // x^(8 * 256 * jj)
+        if (v && jj) {
+            v = multmodp(B.crc_pow[jj & (kCrcPowLo - 1)], v);
+            if (jj >= kCrcPowLo) v = multmodp(B.crc_pow[kCrcPowLo + (jj / kCrcPowLo)], v);
+        }
+        if (g == 0) v ^= ~multmodp(x2nmodp((uint64_t)n, 3), 0xFFFFFFFFu);
+        if (v) atomicXor(&B.meta[i].crc, v);
     }
 }
 
@@ -2091,7 +2280,26 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_parse),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds + 2048));
     hipStream_t s = ctx->stream;
-    hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
+    // D1: the wave form for uniform batches of RGB tiles up to 1024 wide (OMR_PNG_FILTER_WAVE=0: the
+    // workgroup form, for measurement)
+    static const bool wave_filter = [] {
+        const char* e = std::getenv("OMR_PNG_FILTER_WAVE");
+        return !(e && *e == '0');
+    }();
+    const int W0 = im[0].W, H0 = im[0].H;
+    const int fw_m = (W0 / 4 + 63) / 64;
+    if (wave_filter && uniform && im[0].kind == kRgb && W0 % 4 == 0 && W0 <= 1024) {
+        Bt.fw_bands = (H0 + kFilterBandRows - 1) / kFilterBandRows;
+        const unsigned blocks = (unsigned)(((int64_t)n * Bt.fw_bands + 3) / 4);
+        switch (fw_m) {
+        case 1: hipLaunchKernelGGL(k_pngb_filter_wave<1>, dim3(blocks), dim3(256), 0, s, Bt); break;
+        case 2: hipLaunchKernelGGL(k_pngb_filter_wave<2>, dim3(blocks), dim3(256), 0, s, Bt); break;
+        case 3: hipLaunchKernelGGL(k_pngb_filter_wave<3>, dim3(blocks), dim3(256), 0, s, Bt); break;
+        default: hipLaunchKernelGGL(k_pngb_filter_wave<4>, dim3(blocks), dim3(256), 0, s, Bt); break;
+        }
+    } else {
+        hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
+    }
     hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
     hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
     hipLaunchKernelGGL(k_pngb_bits, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
@@ -2210,7 +2418,10 @@ omr_status omr_render_shape_mask_png_batch(omr_ctx* ctx, const omr_mask_job* job
         }
         const int kind = j.width % 8 == 0 ? kIdx1 : kIdx8;
         const PngPlan P = png_plan(kind, j.width, j.height);
-        if (P.raw > ((int64_t)1 << 27)) {                // > 2^31 bits worst case: single path
+        // > 2^31 bits worst case, or a row too wide for the batch filter's LDS: the single path
+        // (which answers the too-wide row for this mask alone)
+        if (P.raw > ((int64_t)1 << 27) ||
+            align_up((size_t)png_filter_lds(P.rowlen - 1) + 16, 16) > (size_t)kPngFilterLdsMax + 64) {
             big.push_back(i);
             continue;
         }
@@ -2274,8 +2485,8 @@ omr_status omr_render_shape_mask_png_batch(omr_ctx* ctx, const omr_mask_job* job
             offsets[i] = used;
             lengths[i] = (uint32_t)len;
             used = align_up(used + len, 16);
-        } else if (st != OMR_BUFFER_TOO_SMALL && st != OMR_NOT_FOUND) {
-            return st;
+        } else if (st != OMR_BUFFER_TOO_SMALL && st != OMR_NOT_FOUND && st != OMR_INVALID_ARGUMENT) {
+            return st;                                  // a device failure fails the call
         }
     }
     return OMR_OK;

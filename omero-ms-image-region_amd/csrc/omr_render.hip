@@ -69,16 +69,6 @@ __global__ void __launch_bounds__(256) k_build_contrib(const RenderPlan* __restr
     contrib[blockIdx.x * 256 + threadIdx.x] = contrib_entry(plan, blockIdx.x, threadIdx.x, is_signed8);
 }
 
-// grid: (ceil(n/256), n_active); builds the byte LUT of every kModeLut16 channel.
-__global__ void __launch_bounds__(256) k_build_lut(const RenderPlan* __restrict__ plan,
-                                                   uint8_t* __restrict__ ws_base) {
-    const ChanParam& p = plan->ch[blockIdx.y];
-    if (p.mode != kModeLut16) return;
-    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        ws_base[p.lut_off + i] = (uint8_t)quantize_eval((double)(p.gmin + i), p, plan->cd_start, plan->cd_end);
-}
-
 // ------------------------------------------------------------------------------- K2
 enum K2Mode : int { kK2Table8 = 0, kK2Linear16 = 1, kK2Mixed16 = 2, kK2Eval = 3, kK2Fast16 = 4,
                     kK2Thresh = 5 /* float / 32-bit, every channel kModeThresh: no double math */ };
@@ -188,7 +178,8 @@ __device__ __forceinline__ double pixel_double(const Chunk<BPP, VEC>& c, int j) 
 }
 
 // General q(x) in double (float / 32-bit types): Java semantics, selects instead of branches.
-__device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds, int cde) {
+// Host and device: the host runs it to find the kModeThresh code thresholds (host_thresholds).
+__host__ __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds, int cde) {
     const double f = family_map(p, x);
     const double a = p.a0 * (f - p.ys);
     double r = floor(a + 0.5);
@@ -207,15 +198,8 @@ __device__ __forceinline__ uint32_t eval_q(double x, const ChanParam& p, int cds
 // q that is monotone non-decreasing in x (checked on the host: window, NR, family and both
 // rounding stages are all monotone once f is monotone on [ws, we)):
 //   q(x) = min(#{c in 1..255 : T[c] <= key(x)}, q(max key)),  T[c] = min{key : q(key) >= c}.
-// T is found by K1 with the very eval_q K2's kModeEval path evaluates, so the two modes give
-// identical codes; K2 then costs 8 LDS reads per pixel instead of a double log/pow.
-template <int PT> struct KeyDomain;
-template <> struct KeyDomain<OMR_PIXELS_FLOAT> {             // non-NaN keys: -inf .. +inf
-    static constexpr uint32_t lo = 0x007FFFFFu, hi = 0xFF800000u;
-};
-template <> struct KeyDomain<OMR_PIXELS_INT32> { static constexpr uint32_t lo = 0u, hi = 0xFFFFFFFFu; };
-template <> struct KeyDomain<OMR_PIXELS_UINT32> { static constexpr uint32_t lo = 0u, hi = 0xFFFFFFFFu; };
-
+// T is found on the host with eval_q (host_thresholds), the q K2's kModeEval path evaluates on
+// the device; K2 then costs a bucket read and a short search instead of a double log/pow.
 __device__ __forceinline__ uint32_t float_key(uint32_t bits) {
     return (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
 }
@@ -226,51 +210,9 @@ template <int PT> __device__ __forceinline__ uint32_t raw_key(uint32_t raw) {
     else return raw;
 }
 
-template <int PT> __device__ __forceinline__ double key_value(uint32_t k) {
-    if constexpr (PT == OMR_PIXELS_FLOAT)
-        return (double)__uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
-    else if constexpr (PT == OMR_PIXELS_INT32) return (double)(int32_t)(k ^ 0x80000000u);
-    else return (double)k;
-}
 
-// grid: (64, n_active) x 256 threads; wave w of block b finds T[c], c = 4b + w, by a 64-ary
-// search of the key domain (every lane evaluates q at one of 64 evenly spaced keys, a ballot
-// narrows the interval 64-fold: <= 6 rounds instead of 33 bisection steps).
-// thr[a][0] = q(max key) | q(NaN) << 8; thr[a][c] = T[c] (0xFFFFFFFF when no key reaches c).
-template <int PT>
-__global__ void __launch_bounds__(256) k_build_thresh(const RenderPlan* __restrict__ plan,
-                                                      uint32_t* __restrict__ thr) {
-    const int a = blockIdx.y;
-    const ChanParam& p = plan->ch[a];
-    if (p.mode != kModeThresh) return;
-    const int cds = plan->cd_start, cde = plan->cd_end;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    constexpr uint32_t klo = KeyDomain<PT>::lo, khi = KeyDomain<PT>::hi;
-    if (c == 0) {
-        if (lane == 0) {
-            const uint32_t cmax = eval_q(key_value<PT>(khi), p, cds, cde);
-            const uint32_t qnan = PT == OMR_PIXELS_FLOAT ? eval_q(__builtin_nan(""), p, cds, cde) : 0u;
-            thr[a * 256] = cmax | (qnan << 8);
-        }
-        return;
-    }
-    uint64_t lo = klo, hi = (uint64_t)khi + 1;      // answer in [lo, hi]; hi = "none"
-    while (lo < hi) {                               // wave-uniform
-        const uint64_t n = hi - lo, step = (n + 63) / 64;
-        const uint64_t m = lo + lane * step;
-        const bool pred = m < hi && eval_q(key_value<PT>((uint32_t)m), p, cds, cde) >= c;
-        const uint64_t mask = __ballot(pred);
-        if (mask == 0) {
-            lo = lo + ((n - 1) / step) * step + 1;      // past the last probed key
-        } else {
-            const uint64_t j = (uint64_t)(__ffsll((unsigned long long)mask) - 1);
-            if (j == 0) hi = lo;
-            else { hi = lo + j * step; lo = lo + (j - 1) * step + 1; }
-        }
-    }
-    if (lane == 0) thr[a * 256 + c] = lo > khi ? 0xFFFFFFFFu : (uint32_t)lo;
-}
+// thr[a][0] = q(max key) | q(NaN) << 8; thr[a][c] = T[c] (0xFFFFFFFF when no key reaches c): built
+// on the host (host_thresholds) and staged with the plan.
 
 // Buckets over the key range where a kModeThresh channel's code varies: bucket b covers 2^shift
 // keys from origin + b·2^shift; its entry is (#T <= its first key) | (#T in the rest of it) << 8,
@@ -630,6 +572,7 @@ struct PreparedPlan {
     size_t plan_bytes = 0;
     int n_lut = 0;
     size_t lut_bytes = 0;
+    std::vector<uint8_t> lut_host;   // the kModeLut16 byte LUTs (lut_bytes), built on the host
 };
 
 static double host_family_map(const ChanParam& p, double x) { return family_map_code(p.family, x, p.k, p.ws, p.we); }
@@ -655,9 +598,7 @@ static int32_t ceil_to_i32(double v) {
 // log / poly / exp when ws > 0 and k > 0 (x^k, ln x, e^(x^k) increase on x > 0); for the
 // window-normalised exp (OMR_SEM_EXP_NORMALIZED) when k > 0 (its input is in [0, 1)).  Noise
 // reduction only widens the two constant ends.  Codes must stay inside one byte without wrap.
-static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixel_type) {
-    if (pixel_type != OMR_PIXELS_FLOAT && pixel_type != OMR_PIXELS_INT32 && pixel_type != OMR_PIXELS_UINT32)
-        return false;
+static bool monotone_q(const ChanParam& p, const omr_quantum_def& q) {
     if (q.cd_start < 0 || q.cd_end > 255 || q.cd_start > q.cd_end) return false;
     if (!std::isfinite(p.ws) || !std::isfinite(p.we) || !(p.ws < p.we)) return false;
     if (p.nr && !std::isfinite(p.dec)) return false;
@@ -673,6 +614,210 @@ static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixe
     if (!is_log && !(p.k > 0 && std::isfinite(p.k))) return false;
     if (p.family == kFamExpNorm) return true;
     return p.ws > 0;
+}
+
+static bool thresh_ok(const ChanParam& p, const omr_quantum_def& q, int32_t pixel_type) {
+    if (pixel_type != OMR_PIXELS_FLOAT && pixel_type != OMR_PIXELS_INT32 && pixel_type != OMR_PIXELS_UINT32)
+        return false;
+    return monotone_q(p, q);
+}
+
+// ---- kModeThresh code thresholds, on the host (round 5).  T[c] = the smallest key whose q is
+// >= c, found with eval_q run on the host: the family map then goes through the host libm (the
+// same log / pow / exp the CPU restatement calls), so the thresholds -- and hence every code K2
+// produces for a Thresh channel -- are exactly the restatement's, where the device libm left a
+// code boundary one ulp off now and then (+-1 code value, two of them on a composite component
+// two channels feed).  Per code a galloping search from an estimate (the family map inverted at
+// the code's rounding boundary) brackets T[c] within a few keys, then bisection: ~8 q evaluations
+// per code instead of 32, and the estimate only steers the search, so the result does not depend
+// on it.  Results are cached per (pixel type, codomain, family, window, coefficient, NR).
+static double host_key_value(int32_t pt, uint32_t k) {
+    if (pt == OMR_PIXELS_FLOAT) {
+        const uint32_t b = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+        float f;
+        std::memcpy(&f, &b, 4);
+        return (double)f;
+    }
+    if (pt == OMR_PIXELS_INT32) return (double)(int32_t)(k ^ 0x80000000u);
+    return (double)k;
+}
+
+// The key of the representable pixel value nearest x (an estimate only; NaN -> 0).
+static uint64_t host_key_of(int32_t pt, double x) {
+    if (x != x) return 0;
+    if (pt == OMR_PIXELS_FLOAT) {
+        const float f = (float)x;
+        uint32_t b;
+        std::memcpy(&b, &f, 4);
+        return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    }
+    if (pt == OMR_PIXELS_INT32) {
+        const double c = std::min(2147483647.0, std::max(-2147483648.0, std::floor(x)));
+        return (uint32_t)(int32_t)c ^ 0x80000000u;
+    }
+    return (uint32_t)std::min(4294967295.0, std::max(0.0, std::floor(x)));
+}
+
+// Inverse of the family map (estimate of the x where f(x) = y).
+static double host_family_inverse(const ChanParam& p, double y) {
+    switch (p.family) {
+    case kFamPoly: return std::pow(y, 1.0 / p.k);
+    case kFamLog:
+    case kFamLogRaw: return std::exp(y);
+    case kFamExp: return std::pow(std::log(y), 1.0 / p.k);
+    case kFamExpNorm: return p.ws + (p.we - p.ws) * std::pow(std::log(y), 1.0 / p.k);
+    default: return y;
+    }
+}
+
+// Smallest k in [L, R] with ge(k), given ge(R) and a guess h in [L, R]: gallop away from h until
+// the answer is bracketed, then bisect.  Exact for any monotone ge whatever h is.
+template <typename Ge>
+static uint64_t first_true(uint64_t L, uint64_t R, uint64_t h, Ge ge) {
+    if (ge(h)) {
+        R = h;
+        for (uint64_t step = 1; R - L >= step; step <<= 1) {
+            const uint64_t m = R - step;
+            if (ge(m)) R = m;
+            else { L = m + 1; break; }
+        }
+    } else {
+        L = h + 1;
+        for (uint64_t step = 1; L + step - 1 < R; step <<= 1) {
+            const uint64_t m = L + step - 1;
+            if (ge(m)) { R = m; break; }
+            L = m + 1;
+        }
+    }
+    while (L < R) {
+        const uint64_t m = L + (R - L) / 2;
+        if (ge(m)) R = m;
+        else L = m + 1;
+    }
+    return L;
+}
+
+// Estimate of the pixel value where q reaches code c: the first-stage value r the code needs,
+// then f(x) = ys + (r - 0.5) / a0 inverted, clamped into the window.
+static double code_estimate(const ChanParam& p, uint32_t c, int cds) {
+    double r = (double)c;
+    if (p.second) r = std::ceil(((double)c - 0.5 - (double)cds) / p.a1);
+    double xe = host_family_inverse(p, p.ys + (r - 0.5) / p.a0);
+    if (!(xe >= p.ws)) xe = p.ws;                    // NaN included
+    if (!(xe <= p.we)) xe = p.we;
+    return xe;
+}
+
+static void host_thresholds_compute(const ChanParam& p, int32_t pt, int cds, int cde, uint32_t* T) {
+    const uint32_t klo = pt == OMR_PIXELS_FLOAT ? 0x007FFFFFu : 0u;
+    const uint32_t khi = pt == OMR_PIXELS_FLOAT ? 0xFF800000u : 0xFFFFFFFFu;
+    auto q = [&](uint64_t k) { return eval_q(host_key_value(pt, (uint32_t)k), p, cds, cde); };
+    const uint32_t cmax = q(khi);
+    const uint32_t qnan = pt == OMR_PIXELS_FLOAT ? eval_q(std::nan(""), p, cds, cde) : 0u;
+    T[0] = cmax | (qnan << 8);
+    uint64_t lower = klo;                            // T[c] >= T[c - 1]: q is monotone
+    for (uint32_t c = 1; c < 256; ++c) {
+        if (c > cmax) {                              // no key reaches c
+            T[c] = 0xFFFFFFFFu;
+            continue;
+        }
+        const uint64_t h = std::min<uint64_t>(std::max<uint64_t>(host_key_of(pt, code_estimate(p, c, cds)), lower), khi);
+        lower = first_true(lower, khi, h, [&](uint64_t k) { return q(k) >= c; });
+        T[c] = (uint32_t)lower;
+    }
+}
+
+// The byte LUT of a kModeLut16 channel over its domain [gmin, gmax] (the Quantization_8_16_bit
+// LUT), with quantize_eval on the host: for a monotone q through its 255 code thresholds (a few
+// thousand evaluations instead of 65,536 for a u16 domain), otherwise entry by entry.  Cached
+// (most recent 16 domains up to 2^17 entries).
+static void host_quant_lut_compute(const ChanParam& p, int cds, int cde, bool mono, uint8_t* out) {
+    const int64_t gmin = p.gmin, gmax = p.gmax, n = gmax - gmin + 1;
+    auto q = [&](int64_t x) { return (uint32_t)quantize_eval((double)x, p, cds, cde); };
+    if (!mono) {
+        for (int64_t i = 0; i < n; ++i) out[i] = (uint8_t)q(gmin + i);
+        return;
+    }
+    const uint32_t cmax = q(gmax);
+    int64_t T[256];
+    uint64_t lower = 0;                              // offsets from gmin
+    for (uint32_t c = 1; c <= cmax; ++c) {
+        double xe = std::ceil(code_estimate(p, c, cds));
+        if (!(xe >= (double)gmin)) xe = (double)gmin;
+        if (!(xe <= (double)gmax)) xe = (double)gmax;
+        const uint64_t h = std::max<uint64_t>((uint64_t)((int64_t)xe - gmin), lower);
+        lower = first_true(lower, (uint64_t)(n - 1), h, [&](uint64_t k) { return q(gmin + (int64_t)k) >= c; });
+        T[c] = (int64_t)lower;
+    }
+    uint32_t c = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        while (c < cmax && T[c + 1] <= i) ++c;
+        out[i] = (uint8_t)c;
+    }
+}
+
+static void host_quant_lut(const ChanParam& p, int cds, int cde, bool mono, uint8_t* out) {
+    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
+    struct Key {
+        int32_t cds, cde, family, nr, gmin, gmax, lo, hi, second, mono;
+        double ws, we, k, ys, a0, a1, dec;
+    };
+    Key key;
+    std::memset(&key, 0, sizeof(key));
+    key.cds = cds; key.cde = cde; key.family = p.family; key.nr = p.nr; key.gmin = p.gmin; key.gmax = p.gmax;
+    key.lo = p.lo; key.hi = p.hi; key.second = p.second; key.mono = mono;
+    key.ws = p.ws; key.we = p.we; key.k = p.k; key.ys = p.ys; key.a0 = p.a0; key.a1 = p.a1; key.dec = p.dec;
+    struct Entry { Key k; std::vector<uint8_t> lut; };
+    static std::mutex mu;
+    static std::vector<Entry> cache;                 // most recent last
+    const bool cacheable = n <= (1 << 17);
+    if (cacheable) {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = cache.size(); i-- > 0;)
+            if (std::memcmp(&cache[i].k, &key, sizeof(Key)) == 0) {
+                std::memcpy(out, cache[i].lut.data(), (size_t)n);
+                if (i + 1 != cache.size()) std::swap(cache[i], cache.back());
+                return;
+            }
+    }
+    host_quant_lut_compute(p, cds, cde, mono, out);
+    if (!cacheable) return;
+    Entry e{key, std::vector<uint8_t>(out, out + n)};
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.push_back(std::move(e));
+}
+
+static void host_thresholds(const ChanParam& p, int32_t pt, int cds, int cde, uint32_t* T) {
+    struct Key {
+        int32_t pt, cds, cde, family, nr, pad;
+        double ws, we, k, ys, a0, a1, dec;
+        int32_t second, pad2;
+    };
+    Key key;
+    std::memset(&key, 0, sizeof(key));
+    key.pt = pt; key.cds = cds; key.cde = cde; key.family = p.family; key.nr = p.nr;
+    key.ws = p.ws; key.we = p.we; key.k = p.k; key.ys = p.ys; key.a0 = p.a0; key.a1 = p.a1; key.dec = p.dec;
+    key.second = p.second;
+    struct Entry { Key k; uint32_t T[256]; };
+    static std::mutex mu;
+    static std::vector<Entry> cache;                 // most recent last, at most 64 entries
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (size_t i = cache.size(); i-- > 0;)
+            if (std::memcmp(&cache[i].k, &key, sizeof(Key)) == 0) {
+                std::memcpy(T, cache[i].T, sizeof(cache[i].T));
+                if (i + 1 != cache.size()) std::swap(cache[i], cache.back());
+                return;
+            }
+    }
+    Entry e;
+    e.k = key;
+    host_thresholds_compute(p, pt, cds, cde, e.T);
+    std::memcpy(T, e.T, sizeof(e.T));
+    std::lock_guard<std::mutex> lk(mu);
+    if (cache.size() >= 64) cache.erase(cache.begin());
+    cache.push_back(e);
 }
 
 static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch,
@@ -742,6 +887,12 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
             p.gmax = (int32_t)gmax;
             if (bpp == 1) {
                 p.mode = kModeTable8;
+                for (int t = 0; t < 256; ++t) {            // q of every raw byte in the domain
+                    const int value = pixel_type == OMR_PIXELS_INT8 ? (int)(int8_t)(uint8_t)t : t;
+                    p.qtab[t] = value < p.gmin || value > p.gmax
+                                    ? 0
+                                    : (uint8_t)quantize_eval((double)value, p, q->cd_start, q->cd_end);
+                }
             } else {
                 const bool fast = b.family == OMR_FAMILY_LINEAR && !p.nr && std::isfinite(p.ws) &&
                                   std::isfinite(p.a0) && std::fabs(p.a0) < 1e300 && !p.second &&
@@ -771,6 +922,15 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
             if (P.ch[i].mode == kModeThresh) P.ch[i].mode = kModeEval;
     pp.plan_bytes = offsetof(RenderPlan, ch) + sizeof(ChanParam) * (size_t)(na > 0 ? na : 1);
     pp.lut_bytes = lut_off;
+    pp.lut_host.clear();
+    if (pp.n_lut > 0) {
+        pp.lut_host.assign(lut_off, 0);
+        const bool int_bounds = (P.sem & OMR_SEM_WINDOW_INT_BOUNDS) != 0;   // x in [(int)ws, ws): may wrap
+        for (int i = 0; i < na; ++i)
+            if (P.ch[i].mode == kModeLut16)
+                host_quant_lut(P.ch[i], q->cd_start, q->cd_end, !int_bounds && monotone_q(P.ch[i], *q),
+                               pp.lut_host.data() + P.ch[i].lut_off);
+    }
     return OMR_OK;
 }
 
@@ -1008,13 +1168,28 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
     uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
     uint8_t* d_luts = ws + L.lut_off;
+    const int na = pp.plan.n_active;
+    bool use_thresh = false;
+    for (int i = 0; i < na; ++i) use_thresh |= pp.plan.ch[i].mode == kModeThresh;
+    uint32_t* d_thresh = reinterpret_cast<uint32_t*>(ws + L.thresh_off);
+    uint16_t* d_buckets = reinterpret_cast<uint16_t*>(ws + L.bucket_off);
+    std::vector<uint32_t> thr;
+    if (use_thresh) {                               // the code thresholds, on the host (exact)
+        thr.assign((size_t)na * 256, 0u);
+        for (int i = 0; i < na; ++i)
+            if (pp.plan.ch[i].mode == kModeThresh)
+                host_thresholds(pp.plan.ch[i], pixel_type, pp.plan.cd_start, pp.plan.cd_end, thr.data() + 256 * i);
+    }
+    const bool thr_with_plan = use_thresh && !(ptr_src && ptr_bytes);   // one staging launch for both
     // LUT offsets are relative to the LUT region; make them workspace-relative for K2.
     for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off += L.lut_off;
-    omr_status st = stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, const_cast<const void**>(d_plane_ptrs),
-                               ptr_src, ptr_src ? ptr_bytes : 0);
+    omr_status st = thr_with_plan
+                        ? stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, d_thresh, thr.data(), thr.size() * 4)
+                        : stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, const_cast<const void**>(d_plane_ptrs),
+                                     ptr_src, ptr_src ? ptr_bytes : 0);
     for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off -= L.lut_off;
     if (st != OMR_OK) return st;
-    const int na = pp.plan.n_active;
+    if (use_thresh && !thr_with_plan && (st = stage_h2d(ctx, d_thresh, thr.data(), thr.size() * 4))) return st;
     const int bpp = bytes_per_pixel(pixel_type);
     const int vec = aligned ? (bpp <= 2 ? 8 : 16 / bpp) : 1;
     const uint64_t cpr = (uint64_t)width / vec;
@@ -1030,23 +1205,9 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
                                pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
             OMR_HIP(ctx, hipGetLastError());
         }
-        if (pp.n_lut > 0) {
-            hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan, ws);
-            OMR_HIP(ctx, hipGetLastError());
-        }
+        if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     }
-    bool use_thresh = false;
-    for (int i = 0; i < na; ++i) use_thresh |= pp.plan.ch[i].mode == kModeThresh;
-    uint32_t* d_thresh = reinterpret_cast<uint32_t*>(ws + L.thresh_off);
-    uint16_t* d_buckets = reinterpret_cast<uint16_t*>(ws + L.bucket_off);
     if (use_thresh) {
-        const dim3 g(64, na);
-        switch (pixel_type) {
-        case OMR_PIXELS_FLOAT: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_FLOAT>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
-        case OMR_PIXELS_INT32: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_INT32>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
-        default: hipLaunchKernelGGL(k_build_thresh<OMR_PIXELS_UINT32>, g, dim3(256), 0, ctx->stream, d_plan, d_thresh); break;
-        }
-        OMR_HIP(ctx, hipGetLastError());
         hipLaunchKernelGGL(k_build_buckets, dim3(kBuckets / 256, na), dim3(256), 0, ctx->stream, d_plan, d_thresh,
                            d_buckets);
         OMR_HIP(ctx, hipGetLastError());
@@ -1205,11 +1366,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
                            fp->pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
         OMR_HIP(ctx, hipGetLastError());
     }
-    if (pp.n_lut > 0) {
-        hipLaunchKernelGGL(k_build_lut, dim3(256, na), dim3(256), 0, ctx->stream, d_plan,
-                           static_cast<uint8_t*>(ctx->ws));
-        OMR_HIP(ctx, hipGetLastError());
-    }
+    if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     std::memset(&F, 0, sizeof(F));
     double tlo, thi;
     type_bounds(fp->pixel_type, tlo, thi);

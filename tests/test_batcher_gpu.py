@@ -397,6 +397,78 @@ def test_projection_job_errors_fail_alone(romio_stack):
     pb.close()
 
 
+def test_projection_bad_t_never_cached(romio_stack):
+    """A projection job at a t outside [0, sizeT) fails at wait in every round it is submitted:
+    the stack cache never records a slot for a stack that was not uploaded (a second request for
+    the same t must not read that slot as a hit), and a good job of the same image still renders."""
+    path, px = romio_stack
+    pb = PixelBuffer(path, PX_, PY_, PZ_, PC_, PT_, _lib.PIXELS_UINT16)
+    ch = c2_channels(3)
+    with Batcher(0, max_batch=8, max_wait_us=1000) as b:
+        for _ in range(2):                                   # two separate dispatch rounds
+            t_bad = b.submit(pb, O.make_qdef("rgb"), ch, 0, PT_ + 1, 0, 0, 16, 16, fmt="argb",
+                             projection="intmax")
+            with pytest.raises(_lib.OmrError) as e:
+                b.wait(t_bad)
+            assert e.value.status == _lib.INVALID_ARGUMENT
+        got = b.wait(b.submit(pb, O.make_qdef("rgb"), ch, 0, 1, 0, 0, 16, 16, fmt="argb", projection="intmax"))
+    stt, exp = _oracle_projected(px, ch, "rgb", 1, _lib.PROJECTION_MAX, 0, PZ_ - 1)
+    np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(PY_, PX_), exp)
+    pb.close()
+
+
+def test_tile_outside_image_fails_alone(romio):
+    """One out-of-bounds tile (x + width > sizeX, or z / t past the image) in a group fails only its
+    own job; the group's other tiles render against the oracle."""
+    path, px = romio
+    pb = PixelBuffer(path, X, Y, Z, C, T, _lib.PIXELS_UINT16)
+    qd, ch = O.make_qdef("rgb"), c2_channels(3)
+    with Batcher(0, max_batch=64, max_wait_us=50000) as b:
+        t_ok = b.submit(pb, qd, ch, 0, 0, 256, 0, TW, TH, fmt="argb")
+        t_x = b.submit(pb, qd, ch, 0, 0, X - 100, 0, TW, TH, fmt="argb")
+        t_z = b.submit(pb, qd, ch, Z, 0, 0, 0, TW, TH, fmt="argb")
+        t_t = b.submit(pb, qd, ch, 0, T, 0, 0, TW, TH, fmt="argb")
+        for t in (t_x, t_z, t_t):
+            with pytest.raises(_lib.OmrError) as e:
+                b.wait(t)
+            assert e.value.status == _lib.INVALID_ARGUMENT
+        got = b.wait(t_ok)
+    np.testing.assert_array_equal(np.frombuffer(got, np.uint32).reshape(TH, TW),
+                                  _oracle_argb(px, ch, "rgb", 0, 256, 0, False))
+    pb.close()
+
+
+def test_mask_jobs_bad_dims_empty_and_wide_fail_alone():
+    """Masks the batch answers 404 take no output room (a 100000 x 100000 mask of 4 bytes must not
+    size a 10 GB host buffer); an empty mask is not deduplicated with a 1-byte zero mask; a mask
+    row too wide for the batched filter fails alone; the good masks of the round still encode."""
+    import io
+    from PIL import Image
+    good = (bytes([0x55, 0xAA] * 8), 16, 8, (255, 0, 0, 255))
+    with Batcher(0, max_batch=64, max_wait_us=50000) as b:
+        b.set_semantics(_lib.SEM_MASK_PIXEL_FLIP)
+        t_huge = b.submit_mask(b"\x01\x02\x03\x04", 100000, 100000, (255, 0, 0, 255))
+        t_empty = b.submit_mask(b"", 8, 1, (255, 0, 0, 255))
+        t_zero = b.submit_mask(b"\x00", 8, 1, (255, 0, 0, 255))
+        t_wide = b.submit_mask(bytes((100001 + 7) // 8), 100001, 1, (0, 255, 0, 255))
+        t_good = b.submit_mask(*good)
+        with pytest.raises(_lib.OmrError) as e:
+            b.wait(t_huge)
+        assert e.value.status == _lib.NOT_FOUND
+        with pytest.raises(_lib.OmrError) as e:
+            b.wait(t_empty)
+        assert e.value.status == _lib.NOT_FOUND
+        zero = b.wait(t_zero)
+        with pytest.raises(_lib.OmrError):
+            b.wait(t_wide)
+        png = b.wait(t_good)
+    im = Image.open(io.BytesIO(zero))
+    assert im.size == (8, 1) and list(im.getdata()) == [0] * 8
+    im = Image.open(io.BytesIO(png))
+    bits = np.unpackbits(np.frombuffer(good[0], np.uint8))[:16 * 8]
+    np.testing.assert_array_equal(np.array(im).reshape(-1), bits)
+
+
 def test_pool_projection_and_mask_jobs(romio_stack, romio):
     """A 2-entry pool serving tile, projection and shape-mask jobs from concurrent workers: every
     result against the CPU restatement, both batchers used."""

@@ -181,8 +181,10 @@ def test_semantics_reject_unknown_flags(sem_ctx):
 #   2 chunks per lane), the fused render -> JPEG (F1; integer types: byte-identical to the unfused
 #   GPU render + JPEG, and to the restatement's JPEG when the family is linear), and the
 #   projection glue (K3 + K2 and K3R; integer types), plus the float threshold / Eval modes.
-# Transcendental families are held to +-1 code value per component (device log/pow/exp vs glibc,
-# DESIGN.md §2); linear ones are bit-exact.
+# Round 5: every quantization table (8/16-bit LUTs, the float / 32-bit code thresholds) is built on
+# the host with the host libm, so integer types and threshold-mode float channels are bit-exact for
+# every family; only Eval-mode channels (double pixels, or a q not provably monotone) evaluate
+# log/pow/exp on the device and keep the +-1 code-value bar.
 
 PRIMARY = [(255, 0, 0, 255), (0, 255, 0, 255), (0, 0, 255, 255)]
 
@@ -208,8 +210,11 @@ def _k3r_context():
 
 def _every_path(ctx, flags, chans, planes, pt, w, h, tol, k3r_ctx=None, jpeg=True):
     """Renders `planes` (numpy, native order) under `flags` through every kernel path and checks
-    each against the restatement.  Returns the one-tile ARGB."""
+    each against the restatement.  Returns the one-tile ARGB.  8/16-bit integer types are held
+    bit-exact whatever `tol` says: their quantization tables come from the host (round 5)."""
     import torch
+    if _lib.BYTES_PER_PIXEL[pt] <= 2:
+        tol = 0
     ctx.set_semantics(flags)
     q = make_qdef("rgb")
     with O.semantics(flags):
@@ -262,6 +267,8 @@ def _files(d_out, offs, lens, n):
 
 def _glue_paths(ctx, k3r, flags, chans, stacks, pt, w, h, z, tol):
     import torch
+    if _lib.BYTES_PER_PIXEL[pt] <= 2:
+        tol = 0                                 # host-built quantization tables: exact
     for c in (ctx, k3r):
         c.set_semantics(flags)
         q = make_qdef("rgb")
