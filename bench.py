@@ -732,26 +732,50 @@ def png_section(torch, ctx, data):
     stat = torch.empty(B, dtype=torch.int32, device=data.device)
     ctx.synchronize()
     batched = {}
+    raw = (3 * TILE + 1) * TILE                         # filtered stream bytes per tile
     for n in (64, 256):
         if n > B:
             continue
         def step():
             ctx.encode_png_batch_device(argb, n, TILE, TILE, d_out, offs, lens, stat)
-        t_end = time.perf_counter() + SECTION_PREWARM_S
-        while time.perf_counter() < t_end:
-            step()
-            ctx.synchronize()
         reps = max(4, 1024 // n)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            step()
-        ctx.synchronize()
-        el = time.perf_counter() - t0
-        ln = lens[:n].cpu().numpy()
+        el, avg = _timed(torch, ctx, step, reps, 2)
+        ln = lens[:n].cpu().numpy().astype(np.int64)
         assert int((stat[:n] != 0).sum().item()) == 0, "PNG batch status"
-        batched[f"tiles_per_call_{n}"] = {"tiles_per_s": round(n * reps / el, 1),
-                                          "ms_per_call": round(1e3 * el / reps, 4),
-                                          "mean_png_bytes": int(ln.mean())}
+        files = int(ln.sum())
+        ms = el * 1e3 / reps
+        leg = {"tiles_per_s": round(n * reps / el, 1), "ms_per_call": round(ms, 4), "mean_png_bytes": int(ln.mean())}
+        # Per-stage roofline from HIP events around each stage's launches (kinds 20-26,
+        # omr_png.hip launch_png_batch).  Algorithmic bytes per call: the filter reads the ARGB
+        # tiles and writes the filtered streams; the histogram pass and the encoder read the
+        # streams (the encoder also writes the deflate words, ~ the files); emit reads the words
+        # and writes the files; CRC reads the files.  HBM-bound stages against 8 TB/s.
+        stages = {20: ("filter (D1)", n * TILE * TILE * 4 + n * raw),
+                  21: ("histogram parse (P2)", n * raw),
+                  22: ("huffman tables (P3)", 0),
+                  23: ("encode (P4: parse + code + look-back)", n * raw + files),
+                  24: ("fixup + meta + offsets", 0),
+                  25: ("emit (P8)", 2 * files),
+                  26: ("crc (P9)", files)}
+        per = {}
+        for k, (name, alg) in stages.items():
+            if k not in avg:
+                continue
+            t = avg[k]
+            e = {"stage": name, "avg_ms": round(t, 5)}
+            if alg:
+                gbs = alg / (t * 1e-3) / 1e9
+                e.update({"algorithmic_bytes": alg, "achieved_gbs": round(gbs, 1),
+                          "frac": round(gbs / HBM_PEAK_GBS, 4)})
+            per[str(k)] = e
+        alg_all = n * TILE * TILE * 4 + files
+        stage_ms = sum(avg.get(k, 0.0) for k in stages)
+        leg["roofline"] = {"bound": "hbm", "scope": "whole pipeline: ARGB tiles in + PNG files out per call",
+                           "achieved": round(alg_all / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(alg_all / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "algorithmic_bytes_per_call": alg_all, "sum_of_stage_ms": round(stage_ms, 5),
+                           "stages": per}
+        batched[f"tiles_per_call_{n}"] = leg
     res["batched"] = batched
     if "tiles_per_call_256" in batched:
         res["batched_vs_single"] = round(batched["tiles_per_call_256"]["tiles_per_s"] / res["single_tile_per_s"], 2)

@@ -172,6 +172,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     if (const char* v = std::getenv("OMR_K2_NT_STORE")) c->k2_nt_store = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_K3R")) c->k3r = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_PNG_DEVICE_D3")) c->png_device_d3 = std::atoi(v) != 0;
+    if (const char* v = std::getenv("OMR_PNG_SINGLE_BATCHED")) c->png_single_batched = std::atoi(v) != 0;
     if (const char* v = std::getenv("OMR_F1_F32")) c->f1_f32 = std::atoi(v) != 0;
     // B4a / B6 grids for 0.4 B per pixel (C2 q 0.9 streams are 0.37; longer ones loop): same-box A/B
     // 210.2k (1.0 B/px, the round-3 sizing) -> 213.5k C2 tiles/s fused (profiles/r04/ab_jpeg_est_groups.txt)

@@ -120,6 +120,7 @@ struct Ctx {
     // PNG D3 (Huffman tables) on the device (env OMR_PNG_DEVICE_D3=1): no mid-encode host round
     // trip, but the single-workgroup build measured slower than the host's
     bool png_device_d3 = false;
+    bool png_single_batched = true;   // single PNG / mask requests through the batched pipeline (n = 1)
     // x^(8*256*j) mod P (CRC-32) for the batched PNG's segment combine: [0, 4096) j = lo, then
     // [4096, 6144) j = hi * 4096; built on the device on first use (omr_png.hip)
     uint32_t* d_crc_pow = nullptr;

@@ -604,14 +604,107 @@ __device__ __forceinline__ uint32_t eq_mask(const uint32_t (&x)[8], const uint32
     return m;
 }
 
-// One lane per kSeg-byte segment; the workgroup first stages its 4 KiB of filtered stream plus
-// the look-back window (one image row, <= 31 KiB) in LDS.  Greedy LZ77 over the distances image
-// rows repeat at (1, bpp, 2*bpp, one row up), matches inside the segment: for each distance d a
-// 32-bit mask of "byte == byte d back" is built with dword compares, and the match length at q is
-// the run of ones from bit q -- the parse itself runs in registers.  The first candidate with the
-// longest match wins (same tokens as a byte-by-byte compare loop).  Parse block `blk` of one image:
-// flt is the image's filtered stream (16-byte aligned), tokens / ntok its segments' token slots
-// (tok_at) and counts, lhist / dhist its symbol histograms.
+// D2 in three pieces, shared by the single-image parse (tokens stored), the batched histogram
+// pass and the batched encoder (both re-parse instead of storing tokens, round 5):
+//   lz_stage         the workgroup stages its kParseLanes * kSeg bytes of filtered stream plus the
+//                    look-back window (one image row, <= 31 KiB) in LDS
+//   lz_seg_prepare   one lane per kSeg-byte segment: for each candidate distance (1, bpp, 2*bpp,
+//                    one row up) a 32-bit mask of "byte == byte d back", built with dword compares
+//   lz_seg_tokens    greedy LZ77 from the masks: the match length at q is the run of ones from bit
+//                    q; the first candidate with the longest match wins (the tokens of a byte-by-
+//                    byte compare loop); every token goes to tok(t, position, candidate or -1)
+// flt is the image's filtered stream (16-byte aligned); the staged window covers [wbeg, bend).
+__device__ __forceinline__ void lz_stage(const uint8_t* __restrict__ flt, int64_t raw, int64_t blk, int32_t back,
+                                         uint8_t* s_win, int64_t& wbeg, int64_t& bend) {
+    const int64_t bbeg = blk * kParseLanes * kSeg;
+    bend = min(raw, bbeg + (int64_t)kParseLanes * kSeg);
+    wbeg = max((int64_t)0, bbeg - back);                        // back is a multiple of 16
+    const int64_t n16 = (bend - wbeg) / 16;
+    const uint4* g16 = reinterpret_cast<const uint4*>(flt + wbeg);
+    for (int64_t i = threadIdx.x; i < n16; i += blockDim.x) reinterpret_cast<uint4*>(s_win)[i] = g16[i];
+    for (int64_t i = wbeg + n16 * 16 + threadIdx.x; i < bend; i += blockDim.x) s_win[i - wbeg] = flt[i];
+}
+
+struct LzSeg {
+    uint32_t m[4];      // equal-byte masks per candidate distance
+    uint32_t dl[4];     // the candidate distances
+    int nd, n;          // candidates, segment bytes
+    int64_t beg;        // stream offset of the segment
+};
+
+__device__ __forceinline__ void lz_seg_prepare(const uint8_t* s_win, int64_t wbeg, int64_t s, int64_t raw,
+                                               int64_t rowlen, int bpp, int32_t back, LzSeg& L) {
+    const uint8_t* f = s_win - wbeg;            // f[p] for p in [wbeg, bend)
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_win);
+    const int64_t beg = s * kSeg;
+    L.beg = beg;
+    const int n = (int)(min(raw, beg + kSeg) - beg);
+    L.n = n;
+    const uint32_t nmask = n >= 32 ? 0xFFFFFFFFu : (1u << n) - 1u;
+    uint32_t x[8];
+    {
+        const uint4* o = reinterpret_cast<const uint4*>(s_win + (beg - wbeg));   // 16-byte aligned
+        const uint4 u0 = o[0], u1 = o[1];
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+    }
+    // candidates in the compare order of the byte-wise parse: 1, bpp, 2 bpp (not for bpp 1,
+    // where bpp repeats distance 1), one row up
+    L.nd = bpp == 1 ? 2 : 4;
+    L.dl[0] = 1u;
+    L.dl[1] = bpp == 1 ? (uint32_t)rowlen : (uint32_t)bpp;
+    L.dl[2] = (uint32_t)(2 * bpp);
+    L.dl[3] = (uint32_t)rowlen;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        L.m[k] = 0;
+        if (k >= L.nd) continue;
+        const int64_t d = L.dl[k];
+        if (d > back) continue;                              // past the staged look-back
+        if (beg - d >= wbeg) {
+            L.m[k] = eq_mask(x, sw, beg - d - wbeg) & nmask;
+        } else {                                             // the window's first bytes
+            uint32_t mm = 0;
+            for (int q = 0; q < n; ++q)
+                if (beg + q - d >= wbeg && f[beg + q] == f[beg + q - d]) mm |= 1u << q;
+            L.m[k] = mm;
+        }
+    }
+}
+
+template <typename Tok>
+__device__ __forceinline__ void lz_seg_tokens(const LzSeg& L, const uint8_t* s_win, int64_t wbeg,
+                                              const DeflateTabs& T, Tok&& tok) {
+    const uint8_t* f = s_win - wbeg;
+    int p = 0;
+    while (p < L.n) {
+        int best = 0, bk = 0;
+        uint32_t bd = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k >= L.nd) break;
+            const uint32_t v = L.m[k] >> p;
+            const int l = v == 0xFFFFFFFFu ? 32 : __builtin_ctz(~v);   // run of equal bytes from p
+            if (l > best) { best = l; bd = L.dl[k]; bk = k; }
+        }
+        if (best >= 3) {
+            tok(pack_match(T, (uint32_t)best, bd), p, bk);
+            p += best;
+        } else {
+            tok((uint32_t)f[L.beg + p], p, -1);
+            ++p;
+        }
+    }
+}
+
+__device__ __forceinline__ void lz_load_tabs(DeflateTabs& T) {
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(&c_dfl);
+    uint8_t* dst = reinterpret_cast<uint8_t*>(&T);
+    for (int i = threadIdx.x; i < (int)sizeof(DeflateTabs); i += blockDim.x) dst[i] = src[i];
+}
+
+// Parse block `blk` of one image with the tokens stored (the single-image pipeline): tokens / ntok
+// its segments' token slots (tok_at) and counts, lhist / dhist its symbol histograms.
 __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw, int64_t rowlen, int bpp,
                                    int64_t nseg, int64_t blk, int32_t back, uint32_t* __restrict__ tokens,
                                    uint16_t* __restrict__ ntok, uint32_t* __restrict__ lhist,
@@ -620,77 +713,24 @@ __device__ void png_lz_parse_block(const uint8_t* __restrict__ flt, int64_t raw,
     __shared__ DeflateTabs T;
     for (int i = threadIdx.x; i < 286; i += kParseLanes) lh[i] = 0;
     if (threadIdx.x < 30) dh[threadIdx.x] = 0;
-    {
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(&c_dfl);
-        uint8_t* dst = reinterpret_cast<uint8_t*>(&T);
-        for (int i = threadIdx.x; i < (int)sizeof(DeflateTabs); i += kParseLanes) dst[i] = src[i];
-    }
-    const int64_t bbeg = blk * kParseLanes * kSeg;
-    const int64_t bend = min(raw, bbeg + (int64_t)kParseLanes * kSeg);
-    const int64_t wbeg = max((int64_t)0, bbeg - back);          // back is a multiple of 16
-    const int64_t n16 = (bend - wbeg) / 16;
-    const uint4* g16 = reinterpret_cast<const uint4*>(flt + wbeg);
-    for (int64_t i = threadIdx.x; i < n16; i += kParseLanes) reinterpret_cast<uint4*>(s_win)[i] = g16[i];
-    for (int64_t i = wbeg + n16 * 16 + threadIdx.x; i < bend; i += kParseLanes) s_win[i - wbeg] = flt[i];
+    lz_load_tabs(T);
+    int64_t wbeg, bend;
+    lz_stage(flt, raw, blk, back, s_win, wbeg, bend);
     __syncthreads();
     const int64_t s = blk * kParseLanes + threadIdx.x;
     if (s < nseg) {
-        const uint8_t* f = s_win - wbeg;            // f[p] for p in [wbeg, bend)
-        const uint32_t* sw = reinterpret_cast<const uint32_t*>(s_win);
-        const int64_t beg = s * kSeg;
-        const int n = (int)(min(raw, beg + kSeg) - beg);
-        const uint32_t nmask = n >= 32 ? 0xFFFFFFFFu : (1u << n) - 1u;
-        uint32_t x[8];
-        {
-            const uint4* o = reinterpret_cast<const uint4*>(s_win + (beg - wbeg));   // 16-byte aligned
-            const uint4 u0 = o[0], u1 = o[1];
-            x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
-            x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
-        }
-        // candidates in the compare order of the byte-wise parse: 1, bpp, 2 bpp (not for bpp 1,
-        // where bpp repeats distance 1), one row up
-        const int nd = bpp == 1 ? 2 : 4;
-        const uint32_t dl[4] = {1u, bpp == 1 ? (uint32_t)rowlen : (uint32_t)bpp,
-                                (uint32_t)(2 * bpp), (uint32_t)rowlen};
-        uint32_t m[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k >= nd) break;
-            const int64_t d = dl[k];
-            if (d > back) continue;                              // past the staged look-back
-            if (beg - d >= wbeg) {
-                m[k] = eq_mask(x, sw, beg - d - wbeg) & nmask;
-            } else {                                             // the window's first bytes
-                uint32_t mm = 0;
-                for (int q = 0; q < n; ++q)
-                    if (beg + q - d >= wbeg && f[beg + q] == f[beg + q - d]) mm |= 1u << q;
-                m[k] = mm;
-            }
-        }
-        int nt = 0, p = 0;
-        while (p < n) {
-            int best = 0;
-            uint32_t bd = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (k >= nd) break;
-                const uint32_t v = m[k] >> p;
-                const int l = v == 0xFFFFFFFFu ? 32 : __builtin_ctz(~v);   // run of equal bytes from p
-                if (l > best) { best = l; bd = dl[k]; }
-            }
-            if (best >= 3) {
-                const uint32_t t = pack_match(T, (uint32_t)best, bd);
-                tokens[tok_at(s, nt++)] = t;
+        LzSeg L;
+        lz_seg_prepare(s_win, wbeg, s, raw, rowlen, bpp, back, L);
+        int nt = 0;
+        lz_seg_tokens(L, s_win, wbeg, T, [&](uint32_t t, int, int) {
+            tokens[tok_at(s, nt++)] = t;
+            if (t & 0x80000000u) {
                 atomicAdd(&lh[257 + (t & 31)], 1u);
                 atomicAdd(&dh[(t >> 5) & 31], 1u);
-                p += best;
             } else {
-                const uint32_t x0 = f[beg + p];
-                tokens[tok_at(s, nt++)] = x0;
-                atomicAdd(&lh[x0], 1u);
-                ++p;
+                atomicAdd(&lh[t], 1u);
             }
-        }
+        });
         ntok[s] = (uint16_t)nt;
     }
     __syncthreads();
@@ -1422,17 +1462,21 @@ static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H
 // through one launch per stage, every grid spanning all images, and the N files packed in device
 // memory with per-image status (the batch form of the per-request ImageIO.write calls,
 // ImageRegionRequestHandler.java:597-599, and of every mask, ShapeMaskRequestHandler.java:185-203):
-//   P1 k_pngb_filter   one workgroup per image row (D1)
-//   P2 k_pngb_parse    one lane per 32-byte segment, 128 per workgroup (D2); per-image histograms
+//   P1 k_pngb_filter   one wave per band of image rows (wave form, RGB tiles), else one
+//                      workgroup per 4 rows (D1)
+//   P2 k_pngb_parse    one lane per 32-byte segment, 128 per workgroup (D2): the per-image symbol
+//                      histograms and a 12-byte parse trace per segment (round 5: no token buffer)
 //   P3 k_pngb_tables   one workgroup per image: length-limited Huffman code + block header (D3
 //                      on the device: no host round trip; N workgroups run side by side)
-//   P4 k_pngb_bits     one lane per segment: its bits, the in-group exclusive scan, group sums
-//   P5 k_pngb_scan     one workgroup per image: group bit offsets, stream length, stored vs
-//                      dynamic, Adler-32 from the row partials, boundary words zeroed, header +
-//                      EOB ORed in
+//   P4 k_pngb_encode   one workgroup per parse block, in ticket order: the tokens again from the
+//                      traces and the stream bytes, each lane's code bits, the block's bit offset by decoupled look-back over the
+//                      image's earlier blocks, codes assembled in LDS, whole words stored, the
+//                      block's two partial words kept aside (round 5: replaces token stores, a
+//                      bits pass and a write pass that moved ~4x the stream in tokens)
+//   P5 k_pngb_fixup    one lane per block: the words blocks share, ORed from the kept parts
+//   P5b k_pngb_meta    one workgroup per image: stream length, stored vs dynamic, Adler-32 from
+//                      the row partials
 //   P6 k_pngb_offsets  one workgroup: files' offsets in the output (16-byte aligned), status
-//   P7 k_pngb_write    one workgroup per 256 segments: codes assembled in LDS, interior words
-//                      stored, the two boundary words ORed
 //   P8 k_pngb_emit     16 output bytes per lane: prefix chunks, IDAT header, zlib stream (deflate
 //                      words funnel-shifted, or stored blocks of the filtered stream), Adler,
 //                      IEND — aligned 16-byte stores
@@ -1441,7 +1485,6 @@ static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H
 //   P10 k_pngb_finish  one lane per image: the CRC bytes
 // =====================================================================================
 constexpr int kPngbGroup = 256;                 // segments per P4/P7 group
-constexpr int kPngbGroupWords = kPngbGroup * kSeg * 16 / 32 + 2;   // <= 16 bits per stream byte
 constexpr int kPngbEmitBytes = 16 * 256;        // output bytes per P8 workgroup
 constexpr int kPngbCrcBytes = 256 * 256;        // CRC range bytes per P9 workgroup
 constexpr int kPngbMaxSide = 4096;
@@ -1478,11 +1521,17 @@ struct PngBatch {
     const int32_t* eblk0;
     const int32_t* cblk0;
     uint8_t* flt;
-    uint32_t* tokens;                           // [segments][kSeg]
-    uint16_t* ntok;                             // [segments]
-    uint32_t* segb;                             // [segments] bit offset within the group
-    uint32_t* gsum;                             // [groups] bits of the group
-    uint32_t* goff;                             // [groups] bit offset of the group in its stream
+    unsigned long long* lb_state;               // [parse blocks] look-back words (flag | bit offset)
+    uint32_t* lb_err;                           // [n] a look-back gave up (the image fails, no hang)
+    uint32_t* lb_ticket;                        // [n] P4 block order per image
+    int32_t lb_skip, pad4;                      // measurement only (OMR_PNG_LB_SKIP=1): no look-back, wrong output
+    uint32_t* blk_b0;                           // [parse blocks] first bit of the block in its stream
+    uint32_t* blk_b1;                           // [parse blocks] one past its last bit
+    uint32_t* blk_cf;                           // [parse blocks] its first (partial) word
+    uint32_t* blk_cl;                           // [parse blocks] its last (partial) word
+    int32_t total_pblk, pad3;
+    int64_t total_segs;
+    uint32_t* trace;                            // [3][segments] parse traces (S, M, D)
     uint32_t* hist;                             // [n][316]
     DflTables* tab;                             // [n]
     PngMeta* meta;                              // [n]
@@ -1551,58 +1600,99 @@ __global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
 // png_filter_rows.
 constexpr int kFilterBandRows = 8;
 
+// Residual f (wave-uniform) of 4 row bytes: png_residuals' entry f alone.
+__device__ __forceinline__ uint32_t png_residual(int f, uint32_t X, uint32_t A, uint32_t B, uint32_t C) {
+    switch (f) {
+    case 0: return X;
+    case 1: return sub8(X, A);
+    case 2: return sub8(X, B);
+    case 3: return sub8(X, (A & B) + (((A ^ B) & 0xFEFEFEFEu) >> 1));
+    default: {
+        uint32_t P = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int a = (int)byte_at(A, k), b = (int)byte_at(B, k), c = (int)byte_at(C, k);
+            const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
+            const int pr = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+            P |= (uint32_t)pr << (8 * k);
+        }
+        return sub8(X, P);
+    }
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS per wave: two rows (this one and the one above) of 3 * 64 * M dwords behind a zero dword
+// (the left neighbour of the row's first dword).
+template <int M> __host__ __device__ constexpr int fw_row_dwords() { return 3 * 64 * M + 1; }
+template <int M> __host__ __device__ constexpr size_t fw_lds_bytes() { return (size_t)4 * 2 * fw_row_dwords<M>() * 4; }
+
 template <int M>
 __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_fw[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + wv;
     const int i = (int)(wid / B.fw_bands);
     if (i >= B.n) return;
     const PngImg& I = B.img[i];
     const int y0 = (int)(wid - (int64_t)i * B.fw_bands) * kFilterBandRows;
     const int y1 = min(I.H, y0 + kFilterBandRows);
-    const int W = I.W, nq = W >> 2, rb = 3 * W;
+    const int W = I.W, nq = W >> 2, nd = 3 * nq, rb = 3 * W;
     const uint32_t* __restrict__ argb = I.argb;
     uint8_t* __restrict__ flt = B.flt + I.flt;
     const int64_t rowlen = I.rowlen, raw = I.raw;
-    uint32_t pv[M][3], cv[M][3];
-    auto load_row = [&](int y, uint32_t (&d)[M][3]) {
+    constexpr int S = fw_row_dwords<M>();
+    uint32_t* bufA = s_fw + wv * 2 * S;
+    uint32_t* bufB = bufA + S;
+    if (lane == 0) { bufA[0] = 0u; bufB[0] = 0u; }
+    auto load_raw = [&](int y, uint4 (&v)[M]) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             const int q = lane + 64 * m;
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (y >= 0 && q < nq) v = reinterpret_cast<const uint4*>(argb + (int64_t)y * W)[q];
-            d[m][0] = __builtin_amdgcn_perm(v.y, v.x, 0x06000102u);       // r0 g0 b0 r1
-            d[m][1] = __builtin_amdgcn_perm(v.z, v.y, 0x05060001u);       // g1 b1 r2 g2
-            d[m][2] = __builtin_amdgcn_perm(v.w, v.z, 0x04050600u);       // b2 r3 g3 b3
+            v[m] = make_uint4(0, 0, 0, 0);
+            if (y >= 0 && q < nq) v[m] = reinterpret_cast<const uint4*>(argb + (int64_t)y * W)[q];
         }
     };
-    load_row(y0 - 1, pv);
-    unsigned long long s1 = 0, s2 = 0;
-    for (int y = y0; y < y1; ++y) {
-        load_row(y, cv);
-        uint32_t rr[5][M][3];
-        uint32_t sm[5] = {0, 0, 0, 0, 0};
+    auto put_row = [&](const uint4 (&v)[M], uint32_t* row) {   // RGB dwords of the row at row[1 + j]
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-            // the dword left of this quad: the previous quad's third dword (0 left of the row)
-            const uint32_t wx = m ? __shfl(cv[m - 1][2], 63, 64) : 0u;
-            const uint32_t wp = m ? __shfl(pv[m - 1][2], 63, 64) : 0u;
-            uint32_t lx = __shfl_up(cv[m][2], 1, 64), lp = __shfl_up(pv[m][2], 1, 64);
-            lx = lane ? lx : wx;
-            lp = lane ? lp : wp;
-            const bool live = lane + 64 * m < nq;
+            const int q = lane + 64 * m;
+            if (q < nq) {
+                row[1 + 3 * q] = __builtin_amdgcn_perm(v[m].y, v[m].x, 0x06000102u);       // r0 g0 b0 r1
+                row[2 + 3 * q] = __builtin_amdgcn_perm(v[m].z, v[m].y, 0x05060001u);       // g1 b1 r2 g2
+                row[3 + 3 * q] = __builtin_amdgcn_perm(v[m].w, v[m].z, 0x04050600u);       // b2 r3 g3 b3
+            }
+        }
+    };
+    uint4 nxt[M];
+    load_raw(y0 - 1, nxt);
+    uint32_t* prev = bufA;
+    uint32_t* cur = bufB;
+    put_row(nxt, prev);
+    load_raw(y0, nxt);
+    unsigned long long s1 = 0, s2 = 0;
+    for (int y = y0; y < y1; ++y) {
+        put_row(nxt, cur);
+        if (y + 1 < y1) load_raw(y + 1, nxt);                 // the next row's loads fly meanwhile
+        wave_lds_sync();
+        // pass 1: the five |residual| sums; lane l takes row dwords j = l + 64 t (conflict-free LDS)
+        uint32_t sm[5] = {0, 0, 0, 0, 0};
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const uint32_t X = cv[m][k], Bv = pv[m][k];
-                const uint32_t Av = __builtin_amdgcn_alignbyte(X, k ? cv[m][k - 1] : lx, 1);
-                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, k ? pv[m][k - 1] : lp, 1);
+        for (int t = 0; t < 3 * M; ++t) {
+            const int j = lane + 64 * t;
+            if (j < nd) {
+                const uint32_t X = cur[1 + j], Bv = prev[1 + j];
+                const uint32_t Av = __builtin_amdgcn_alignbyte(X, cur[j], 1);
+                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, prev[j], 1);
                 uint32_t r[5];
                 png_residuals(X, Av, Bv, Cv, r);
 #pragma unroll
-                for (int f = 0; f < 5; ++f) {
-                    rr[f][m][k] = r[f];
-                    sm[f] = live ? abs_sum8(r[f], sm[f]) : sm[f];
-                }
+                for (int f = 0; f < 5; ++f) sm[f] = abs_sum8(r[f], sm[f]);
             }
         }
         int f = 0;
@@ -1612,40 +1702,44 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
             uint32_t v = sm[k];
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (v < best) { best = v; f = k; }                 // wave-uniform
+            if (v < best) { best = v; f = k; }                 // wave-uniform; lowest filter on ties
+        }
+        // pass 2: the chosen residual row
+        uint32_t c[3 * M];
+#pragma unroll
+        for (int t = 0; t < 3 * M; ++t) {
+            const int j = lane + 64 * t;
+            c[t] = 0u;
+            if (j < nd) {
+                const uint32_t X = cur[1 + j], Bv = prev[1 + j];
+                const uint32_t Av = __builtin_amdgcn_alignbyte(X, cur[j], 1);
+                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, prev[j], 1);
+                c[t] = png_residual(f, X, Av, Bv, Cv);
+            }
         }
         const int64_t ypos = (int64_t)y * rowlen;              // the row's offset in the stream
         const int64_t row0 = I.flt + ypos;                     // ... and in B.flt (16-aligned base)
-        const int u = (int)((-row0 - 1) & 3);                  // residual byte at an aligned address
-        uint32_t c[M][3];
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-                c[m][k] = f == 0 ? rr[0][m][k] : f == 1 ? rr[1][m][k] : f == 2 ? rr[2][m][k]
-                        : f == 3 ? rr[3][m][k] : rr[4][m][k];
-        uint32_t* gw = reinterpret_cast<uint32_t*>(B.flt + row0 + u + 1);   // aligned: out dword J
+        const int u = (int)((-row0 - 1) & 3);                  // residual byte u sits at an aligned address
+        uint32_t* gw = reinterpret_cast<uint32_t*>(B.flt + row0 + u + 1);   // out dword J
         const int jfull = (rb - u) >> 2;                       // out dwords J < jfull lie inside the row
+        const unsigned long long rbase = (unsigned long long)(raw - ypos - 1);
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const int q = lane + 64 * m;
-            uint32_t nx = __shfl_down(c[m][0], 1, 64);          // the next quad's first dword
-            const uint32_t wn = m + 1 < M ? __shfl(c[m + 1][0], 0, 64) : 0u;
-            nx = lane == 63 ? wn : nx;
-            if (q < nq) {
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const int J = 3 * q + k;
-                    const uint32_t w = c[m][k];
-                    const uint32_t hi = k < 2 ? c[m][k + 1] : (q + 1 < nq ? nx : 0u);
-                    if (J < jfull) gw[J] = __builtin_amdgcn_alignbyte(hi, w, u);
-                    const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
-                    s1 += sv;
-                    s2 += (unsigned long long)(raw - ypos - 4 * J - 1) * sv - __builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
-                    // bytes outside the whole out dwords: the row's first u, the last (rb - u) & 3
+        for (int t = 0; t < 3 * M; ++t) {
+            const int j = lane + 64 * t;
+            const uint32_t dn = __shfl_down(c[t], 1, 64);        // residual dword j + 1
+            const uint32_t wn = t + 1 < 3 * M ? __shfl(c[t + 1], 0, 64) : 0u;
+            const uint32_t hi = lane == 63 ? wn : dn;
+            if (j < nd) {
+                const uint32_t w = c[t];
+                if (j < jfull) gw[j] = __builtin_amdgcn_alignbyte(hi, w, u);
+                const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
+                s1 += sv;
+                s2 += (rbase - 4ull * j) * sv - __builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
+                // bytes outside the whole out dwords: the row's first u, its last (rb - u) & 3
+                if (4 * j < u || 4 * j + 3 >= u + 4 * jfull) {
                     for (int b = 0; b < 4; ++b) {
-                        const int t = 4 * J + b;
-                        if (t < u || t >= u + 4 * jfull) flt[ypos + 1 + t] = (uint8_t)byte_at(w, b);
+                        const int tt = 4 * j + b;
+                        if (tt < u || tt >= u + 4 * jfull) flt[ypos + 1 + tt] = (uint8_t)byte_at(w, b);
                     }
                 }
             }
@@ -1655,10 +1749,10 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
             s1 += (unsigned long long)f;
             s2 += (unsigned long long)(raw - ypos) * (unsigned long long)f;
         }
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-#pragma unroll
-            for (int k = 0; k < 3; ++k) pv[m][k] = cv[m][k];
+        wave_lds_sync();                                       // every lane is done with `prev`
+        uint32_t* tmp = prev;
+        prev = cur;
+        cur = tmp;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1669,14 +1763,72 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
     if (lane < 2 * (y1 - y0)) rs[lane] = lane == 0 ? s1 : lane == 1 ? s2 : 0ull;
 }
 
+// P2: the parse of one block: the image's symbol histograms (four LDS copies, lane & 3, so the
+// common literals' atomics spread over four addresses) and each segment's parse trace -- token
+// starts S, match starts M, the matches' candidate indices D (2 bits each, <= 10 per segment) --
+// so that P4 codes the segment without parsing it again.
+constexpr int kHistCopies = 4;
+
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
+    __shared__ uint32_t lh[kHistCopies][286 + 30];
+    __shared__ DeflateTabs T;
     const int i = pngb_image(B, B.pblk0, B.pblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
+    for (int k = threadIdx.x; k < kHistCopies * 316; k += kParseLanes) (&lh[0][0])[k] = 0;
+    lz_load_tabs(T);
+    int64_t wbeg, bend;
+    lz_stage(B.flt + I.flt, I.raw, blk, I.back, s_win, wbeg, bend);
+    __syncthreads();
+    const int64_t s = blk * kParseLanes + threadIdx.x;
+    if (s < I.nseg) {
+        uint32_t* h = lh[threadIdx.x & (kHistCopies - 1)];
+        LzSeg L;
+        lz_seg_prepare(s_win, wbeg, s, I.raw, I.rowlen, I.bpp, I.back, L);
+        uint32_t S = 0, M = 0, D = 0;
+        int nm = 0;
+        lz_seg_tokens(L, s_win, wbeg, T, [&](uint32_t t, int p, int k) {
+            S |= 1u << p;
+            if (t & 0x80000000u) {
+                M |= 1u << p;
+                D |= (uint32_t)k << (2 * nm++);
+                atomicAdd(&h[257 + (t & 31)], 1u);
+                atomicAdd(&h[286 + ((t >> 5) & 31)], 1u);
+            } else {
+                atomicAdd(&h[t], 1u);
+            }
+        });
+        const int64_t gs = I.seg0 + s;
+        B.trace[gs] = S;
+        B.trace[B.total_segs + gs] = M;
+        B.trace[2 * B.total_segs + gs] = D;
+    }
+    __syncthreads();
     uint32_t* h = B.hist + (size_t)i * 316;
-    png_lz_parse_block(B.flt + I.flt, I.raw, I.rowlen, I.bpp, I.nseg, blk, I.back, B.tokens + I.tok0,
-                       B.ntok + I.seg0, h, h + 286, s_win);
+    for (int k = threadIdx.x; k < 316; k += kParseLanes) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int c = 0; c < kHistCopies; ++c) v += lh[c][k];
+        if (v) atomicAdd(&h[k], v);
+    }
+}
+
+// The tokens of a segment from its parse trace (P2): t as lz_seg_tokens produced them.
+template <typename Tok>
+__device__ __forceinline__ void trace_tokens(uint32_t S, uint32_t M, uint32_t D, int n, const uint8_t* seg,
+                                             const uint32_t (&dl)[4], const DeflateTabs& T, Tok&& tok) {
+    while (S) {
+        const int p = __builtin_ctz(S);
+        S &= S - 1;
+        const int q = S ? __builtin_ctz(S) : n;
+        if ((M >> p) & 1u) {
+            tok(pack_match(T, (uint32_t)(q - p), dl[D & 3u]));
+            D >>= 2;
+        } else {
+            tok((uint32_t)seg[p]);
+        }
+    }
 }
 
 __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
@@ -1709,60 +1861,172 @@ __device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s
     return off + x - v;
 }
 
-// P4: one lane per segment (256 per workgroup = one group, never straddling images).
-__global__ void __launch_bounds__(kPngbGroup) k_pngb_bits(PngBatch B) {
+// P4: one workgroup per parse block.  Workgroups take blocks in ticket order (an atomic counter),
+// so every block an encoder waits on belongs to a workgroup that started earlier: the look-back
+// cannot deadlock whatever order the hardware dispatches in.
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 1ull << 63;
+constexpr int kEncWords = kPngbGroup * kSeg * 16 / 32 + 96 + 4;   // <= 16 bits per byte + header
+constexpr uint32_t kLbSpinMax = 1u << 22;
+
+__global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_seg[kPngbGroup * kSeg];   // the block's stream bytes
+    __shared__ DeflateTabs T;
     __shared__ uint8_t llen[286], dlen[30];
+    __shared__ uint16_t lcode[286], dcode[30];
+    __shared__ uint32_t sw[kEncWords];
     __shared__ uint32_t s_wave[kPngbGroup / 64];
+    __shared__ uint32_t s_tk, s_b0, s_b1;
+    // the image from the workgroup index, the block within it from the image's ticket counter
     const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
     const PngImg& I = B.img[i];
-    const int64_t gl = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.grp_per : I.grp0);
-    const DflTables* T = B.tab + i;
-    for (int k = threadIdx.x; k < 286; k += kPngbGroup) llen[k] = T->llen[k];
-    if (threadIdx.x < 30) dlen[threadIdx.x] = T->dlen[threadIdx.x];
+    const int64_t gfirst = B.uniform ? (int64_t)i * B.grp_per : I.grp0;
+    if (threadIdx.x == 0) s_tk = B.lb_skip ? (uint32_t)(blockIdx.x - gfirst) : atomicAdd(&B.lb_ticket[i], 1u);
     __syncthreads();
-    const int64_t ls = gl * kPngbGroup + threadIdx.x;     // segment within the image
-    uint32_t b = 0;
-    if (ls < I.nseg) {
-        const int64_t s = I.seg0 + ls;
-        const uint32_t* tok = B.tokens + I.tok0;
-        const int nt = B.ntok[s];
-        for (int k = 0; k < nt; ++k) b += token_bits(tok[tok_at(ls, k)], llen, dlen);
+    const int64_t blk = s_tk;
+    const int64_t g = gfirst + blk;                             // this workgroup's block
+    const DflTables* Tb = B.tab + i;
+    for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = Tb->llen[k]; lcode[k] = Tb->lcode[k]; }
+    if (threadIdx.x < 30) { dlen[threadIdx.x] = Tb->dlen[threadIdx.x]; dcode[threadIdx.x] = Tb->dcode[threadIdx.x]; }
+    for (int k = threadIdx.x; k < kEncWords; k += kPngbGroup) sw[k] = 0;
+    lz_load_tabs(T);
+    {
+        const int64_t bbeg = blk * kPngbGroup * kSeg, bend = min(I.raw, bbeg + (int64_t)kPngbGroup * kSeg);
+        const uint8_t* src = B.flt + I.flt + bbeg;              // 16-byte aligned
+        const int64_t nbytes = bend - bbeg, n16 = nbytes / 16;
+        for (int64_t k = threadIdx.x; k < n16; k += kPngbGroup)
+            reinterpret_cast<uint4*>(s_seg)[k] = reinterpret_cast<const uint4*>(src)[k];
+        for (int64_t k = n16 * 16 + threadIdx.x; k < nbytes; k += kPngbGroup) s_seg[k] = src[k];
+    }
+    __syncthreads();
+    const int64_t s = blk * kPngbGroup + threadIdx.x;
+    const bool live = s < I.nseg;
+    const bool last = s == I.nseg - 1;                          // the EOB code follows its tokens
+    uint32_t S = 0, M = 0, D = 0;
+    int n = 0;
+    const uint32_t dl[4] = {1u, I.bpp == 1 ? (uint32_t)I.rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
+                            (uint32_t)I.rowlen};               // lz_seg_prepare's candidates
+    const uint8_t* seg = s_seg + kSeg * threadIdx.x;
+    uint32_t nb = 0;
+    if (live) {
+        const int64_t gs = I.seg0 + s;
+        S = B.trace[gs];
+        M = B.trace[B.total_segs + gs];
+        D = B.trace[2 * B.total_segs + gs];
+        n = (int)min((int64_t)kSeg, I.raw - s * kSeg);
+        trace_tokens(S, M, D, n, seg, dl, T, [&](uint32_t t) { nb += token_bits(t, llen, dlen); });
+        if (last) nb += llen[256];
     }
     uint32_t total;
-    const uint32_t ex = pngb_block_excl_scan(b, s_wave, total);
-    if (ls < I.nseg) B.segb[I.seg0 + ls] = ex;
-    if (threadIdx.x == 0) B.gsum[blockIdx.x] = total;
+    const uint32_t ex = pngb_block_excl_scan(nb, s_wave, total);
+    const uint32_t hb = Tb->hdr[95];
+    // The block's bit range: publish the aggregate, then look back with the first wave -- lane l
+    // reads the state of block g - 1 - l (64 predecessors per round trip); the nearest inclusive
+    // prefix ends the walk, the aggregates in front of it add up.
+    // The state words carry flag and value in one 8-byte granule (the data is the flag): relaxed
+    // agent-scope stores and loads, no release / acquire fence -- an agent-scope release writes the
+    // XCD's L2 back on this multi-XCD part (~us per block; MI355X_MICROARCH.md, visibility).
+    if (threadIdx.x < 64) {
+        typedef __attribute__((address_space(1))) unsigned long long gu64;
+        gu64* st = (gu64*)(B.lb_state);
+        const int lane = threadIdx.x;
+        uint32_t b0 = 0;
+        if (blk > 0 && !B.lb_skip) {
+            if (lane == 0) __hip_atomic_store(&st[g], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t jend = g;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t j = jend - 1 - lane;
+                const unsigned long long v =
+                    j >= gfirst ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+                const uint64_t incl = __ballot((v & kLbIncl) != 0);
+                const uint64_t wait = __ballot((v & (kLbIncl | kLbAgg)) == 0);
+                const int f = incl ? __ffsll((unsigned long long)incl) - 1 : 64;   // nearest inclusive lane
+                const uint64_t upto = f == 64 ? ~0ull : (2ull << f) - 1ull;       // lanes 0..f
+                if (wait & upto) {                              // a predecessor has not published yet
+                    if (++spins > kLbSpinMax) {
+                        if (lane == 0) atomicOr(&B.lb_err[i], 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t x = (((upto >> lane) & 1ull) != 0) ? (uint32_t)v : 0u;
+                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+                b0 += x;
+                if (f < 64) break;
+                jend -= 64;
+            }
+        }
+        const uint32_t b1 = (blk == 0 ? hb : b0) + total;
+        if (lane == 0) {
+            __hip_atomic_store(&st[g], kLbIncl | b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_b0 = b0;
+            s_b1 = b1;
+        }
+    }
+    __syncthreads();
+    const uint32_t b0 = s_b0, b1 = s_b1, w0 = b0 >> 5;
+    if (blk == 0 && threadIdx.x == 0)
+        for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&sw[k], Tb->hdr[k]);
+    if (live) {
+        const uint32_t pos = (blk == 0 ? hb : b0) + ex - 32 * w0;   // bit position in sw
+        uint64_t acc = 0;
+        int nacc = (int)(pos & 31);
+        uint32_t wpos = pos >> 5;
+        auto put = [&](uint32_t v, int n) {                    // LSB-first into a 64-bit accumulator
+            acc |= (uint64_t)(v & ((1u << n) - 1)) << nacc;
+            nacc += n;
+            if (nacc >= 32) {
+                atomicOr(&sw[wpos], (uint32_t)acc);
+                ++wpos;
+                acc >>= 32;
+                nacc -= 32;
+            }
+        };
+        trace_tokens(S, M, D, n, seg, dl, T, [&](uint32_t t) { put_token(t, lcode, llen, dcode, dlen, put); });
+        if (last) put(lcode[256], llen[256]);
+        if (nacc > 0) atomicOr(&sw[wpos], (uint32_t)acc);
+    }
+    __syncthreads();
+    // whole words inside [b0, b1) go out; the first and last (shared with the neighbouring
+    // blocks) are kept for P5
+    const uint32_t w1 = (b1 - 1) >> 5;
+    uint32_t* w = B.words + I.words;
+    for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup)
+        if (b0 <= 32 * k && b1 >= 32 * k + 32) w[k] = sw[k - w0];
+    if (threadIdx.x == 0) {
+        B.blk_b0[g] = b0;
+        B.blk_b1[g] = b1;
+        B.blk_cf[g] = sw[0];
+        B.blk_cl[g] = w1 != w0 ? sw[w1 - w0] : 0u;
+    }
 }
 
-// P5: one workgroup per image.
-__global__ void __launch_bounds__(256) k_pngb_scan(PngBatch B) {
-    __shared__ uint32_t s_wave[4];
+// P5: the words two or more blocks share.  Block g handles the partial word its stream ends in,
+// when it is the first block touching that word, ORing the first words of the blocks that
+// follow while they start inside it.
+__global__ void __launch_bounds__(256) k_pngb_fixup(PngBatch B) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= B.total_grp) return;
+    const int i = pngb_image(B, B.grp0, B.grp_per, g);
+    const PngImg& I = B.img[i];
+    const int64_t gend = (B.uniform ? (int64_t)i * B.grp_per : I.grp0) + (I.nseg + kPngbGroup - 1) / kPngbGroup;
+    const uint32_t b0 = B.blk_b0[g], b1 = B.blk_b1[g], w0 = b0 >> 5, w1 = (b1 - 1) >> 5;
+    if ((b1 & 31) == 0 || !(w1 > w0 || (b0 & 31) == 0)) return;
+    uint32_t v = w1 == w0 ? B.blk_cf[g] : B.blk_cl[g];
+    for (int64_t j = g + 1; j < gend && B.blk_b0[j] < 32 * (w1 + 1); ++j) v |= B.blk_cf[j];
+    B.words[I.words + w1] = v;
+}
+
+// P5b: one workgroup per image: stream length, stored vs dynamic, Adler-32.
+__global__ void __launch_bounds__(256) k_pngb_meta(PngBatch B) {
     __shared__ unsigned long long s_ad[2][4];
-    __shared__ uint32_t s_carry;
     const int i = blockIdx.x;
     const PngImg& I = B.img[i];
-    const DflTables* T = B.tab + i;
-    const int ng = (int)((I.nseg + kPngbGroup - 1) / kPngbGroup);
-    const uint32_t hb = T->hdr[95];
-    if (threadIdx.x == 0) s_carry = hb;
-    __syncthreads();
-    for (int g0 = 0; g0 < ng; g0 += 256) {              // group offsets: header bits + exclusive scan
-        const int g = g0 + threadIdx.x;
-        const uint32_t v = g < ng ? B.gsum[I.grp0 + g] : 0u;
-        uint32_t tot;
-        const uint32_t ex = pngb_block_excl_scan(v, s_wave, tot);
-        const uint32_t base = s_carry;
-        if (g < ng) B.goff[I.grp0 + g] = base + ex;
-        __syncthreads();
-        if (threadIdx.x == 0) s_carry = base + tot;
-        __syncthreads();
-    }
-    const uint32_t eob = s_carry;                      // header + codes
-    const uint32_t eob_n = T->llen[256];
-    const int64_t dbytes = ((int64_t)eob + eob_n + 7) / 8;
-    const int64_t zdyn = 2 + dbytes + 4, zstored = 2 + 5 * I.nblk + I.raw + 4;
+    const int64_t glast = (B.uniform ? (int64_t)i * B.grp_per : I.grp0) + (I.nseg + kPngbGroup - 1) / kPngbGroup - 1;
+    const uint32_t total = B.blk_b1[glast];                    // header + codes + EOB
+    const int64_t zdyn = 2 + ((int64_t)total + 7) / 8 + 4, zstored = 2 + 5 * I.nblk + I.raw + 4;
     const bool stored = zdyn >= zstored;
-    // Adler-32 of the filtered stream from the row partials (the same bytes either way)
     unsigned long long s1 = 0, s2 = 0;
     for (int y = threadIdx.x; y < I.H; y += 256) {
         s1 += B.row_sums[2 * ((int64_t)I.row0 + y)];
@@ -1773,30 +2037,12 @@ __global__ void __launch_bounds__(256) k_pngb_scan(PngBatch B) {
         s2 += __shfl_down(s2, o, 64);
     }
     if ((threadIdx.x & 63) == 0) { s_ad[0][threadIdx.x >> 6] = s1; s_ad[1][threadIdx.x >> 6] = s2; }
-    uint32_t* w = B.words + I.words;
-    if (!stored) {                                     // zero the words the groups OR into
-        for (int g = threadIdx.x; g < ng; g += 256) {
-            const uint32_t o = B.goff[I.grp0 + g], n = B.gsum[I.grp0 + g];
-            w[o >> 5] = 0;
-            if (n) w[(o + n - 1) >> 5] = 0;
-        }
-        for (uint32_t k = threadIdx.x; k <= (hb >> 5); k += 256) w[k] = 0;
-        if (threadIdx.x == 0) {
-            w[eob >> 5] = 0;
-            w[(eob + eob_n - 1) >> 5] = 0;
-        }
-    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (!stored) {
-            for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&w[k], T->hdr[k]);
-            const uint32_t v = T->lcode[256], sh = eob & 31;
-            atomicOr(&w[eob >> 5], v << sh);
-            if (sh + eob_n > 32) atomicOr(&w[(eob >> 5) + 1], v >> (32 - sh));
-        }
         const unsigned long long a1 = s_ad[0][0] + s_ad[0][1] + s_ad[0][2] + s_ad[0][3];
         const unsigned long long a2 = s_ad[1][0] + s_ad[1][1] + s_ad[1][2] + s_ad[1][3];
         const uint64_t a = (1 + a1) % 65521, b = ((uint64_t)I.raw % 65521 + a2 % 65521) % 65521;
+        const uint32_t hb = B.tab[i].hdr[95];
         PngMeta& M = B.meta[i];
         M.zlen = stored ? zstored : zdyn;
         M.file_len = I.pre_len + 8 + M.zlen + 4 + 12;
@@ -1804,9 +2050,9 @@ __global__ void __launch_bounds__(256) k_pngb_scan(PngBatch B) {
         M.adler = (uint32_t)((b << 16) | a);
         M.crc = 0;
         M.hbits = hb;
-        M.tot_bits = eob - hb;
+        M.tot_bits = total - hb;
         M.stored = stored ? 1 : 0;
-        M.status = OMR_OK;
+        M.status = B.lb_err[i] ? OMR_INTERNAL : OMR_OK;
     }
 }
 
@@ -1819,7 +2065,8 @@ __global__ void __launch_bounds__(1024) k_pngb_offsets(PngBatch B) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int i0 = 0; i0 < B.n; i0 += 1024) {
         const int i = i0 + threadIdx.x;
-        const unsigned long long v = i < B.n ? ((unsigned long long)B.meta[i].file_len + 15ull) & ~15ull : 0ull;
+        const bool ok = i < B.n && B.meta[i].status == OMR_OK;   // a failed image takes no slot
+        const unsigned long long v = ok ? ((unsigned long long)B.meta[i].file_len + 15ull) & ~15ull : 0ull;
         unsigned long long x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1841,9 +2088,9 @@ __global__ void __launch_bounds__(1024) k_pngb_offsets(PngBatch B) {
         const unsigned long long base = s_carry, ex = base + (wid ? s_wave[wid - 1] : 0ull) + x - v;
         if (i < B.n) {
             PngMeta& M = B.meta[i];
-            const bool fits = ex + v <= B.out_cap;       // the whole 16-byte slot (P8 stores 16 B)
+            const bool fits = ok && ex + v <= B.out_cap; // the whole 16-byte slot (P8 stores 16 B)
             M.off = fits ? (int64_t)ex : -1;
-            M.status = fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
+            M.status = !ok ? M.status : fits ? OMR_OK : OMR_BUFFER_TOO_SMALL;
             if (B.d_offsets) B.d_offsets[i] = fits ? ex : 0ull;
             if (B.d_lengths) B.d_lengths[i] = fits ? (uint32_t)M.file_len : 0u;
             if (B.d_status) B.d_status[i] = M.status;
@@ -1851,57 +2098,6 @@ __global__ void __launch_bounds__(1024) k_pngb_offsets(PngBatch B) {
         __syncthreads();
         if (threadIdx.x == 0) s_carry = base + s_wave[15];
         __syncthreads();
-    }
-}
-
-// P7: one workgroup per group of 256 segments: the group's codes are one contiguous run of the
-// stream, assembled in LDS (ds_or: neighbouring lanes share boundary words) and copied out; the
-// run's first and last words are ORed into memory (shared with the neighbouring groups, the
-// header or the EOB, zeroed by P5), interior words stored.
-__global__ void __launch_bounds__(kPngbGroup) k_pngb_write(PngBatch B) {
-    __shared__ uint8_t llen[286], dlen[30];
-    __shared__ uint16_t lcode[286], dcode[30];
-    __shared__ uint32_t sw[kPngbGroupWords];
-    const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
-    const PngImg& I = B.img[i];
-    if (B.meta[i].stored) return;
-    const int64_t gl = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.grp_per : I.grp0);
-    const DflTables* T = B.tab + i;
-    for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = T->llen[k]; lcode[k] = T->lcode[k]; }
-    if (threadIdx.x < 30) { dlen[threadIdx.x] = T->dlen[threadIdx.x]; dcode[threadIdx.x] = T->dcode[threadIdx.x]; }
-    for (int k = threadIdx.x; k < kPngbGroupWords; k += kPngbGroup) sw[k] = 0;
-    __syncthreads();
-    const uint32_t gbase = B.goff[blockIdx.x], gbits = B.gsum[blockIdx.x];
-    const int64_t ls = gl * kPngbGroup + threadIdx.x;
-    if (ls < I.nseg) {
-        const int64_t s = I.seg0 + ls;
-        const uint32_t* tok = B.tokens + I.tok0;
-        const int nt = B.ntok[s];
-        const uint32_t pos = (gbase & 31) + B.segb[s];     // bit position in sw
-        uint64_t acc = 0;
-        int nacc = (int)(pos & 31);
-        uint32_t wpos = pos >> 5;
-        auto put = [&](uint32_t v, int n) {                // LSB-first into a 64-bit accumulator
-            acc |= (uint64_t)(v & ((1u << n) - 1)) << nacc;
-            nacc += n;
-            if (nacc >= 32) {
-                atomicOr(&sw[wpos], (uint32_t)acc);
-                ++wpos;
-                acc >>= 32;
-                nacc -= 32;
-            }
-        };
-        for (int k = 0; k < nt; ++k) put_token(tok[tok_at(ls, k)], lcode, llen, dcode, dlen, put);
-        if (nacc > 0) atomicOr(&sw[wpos], (uint32_t)acc);
-    }
-    __syncthreads();
-    if (!gbits) return;
-    uint32_t* w = B.words + I.words;
-    const uint32_t w0 = gbase >> 5, w1 = (gbase + gbits - 1) >> 5;
-    for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup) {
-        const uint32_t v = sw[k - w0];
-        if (k == w0 || k == w1) atomicOr(&w[k], v);
-        else w[k] = v;
     }
 }
 
@@ -2049,20 +2245,34 @@ __global__ void __launch_bounds__(256) k_pngb_crc(PngBatch B) {
     const int64_t s0 = n - kCrcStrip * (g + 1);           // strip start, relative to the range
     if (s0 + kCrcStrip <= 0) return;                      // wave-uniform: past the range's start
     const uint8_t* base = B.out + M.off + I.pre_len + 4;
+    // the strip's words are read as aligned dwords (one coalesced 256-byte read per wave and step)
+    // and realigned with the next lane's dword (lane 63: lane 0's of the next step)
+    const uintptr_t sa = reinterpret_cast<uintptr_t>(base) + (uintptr_t)s0;   // may lie below base
+    const uint32_t* aw = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+    const int sh = (int)(sa & 3);
+    const int64_t arel = s0 - sh;                         // range offset of aw[0]
     uint32_t q = 0;
-    for (int j = 0; j < 64; ++j) {
-        const int64_t rel = s0 + 256 * j + 4 * lane;
-        uint32_t w = 0;
-        if (rel >= 0) {
-            w = load_u32_any(base + rel);
-        } else if (rel > -4) {
-            w = load_u32_any(base + rel) & (0xFFFFFFFFu << (8 * (int)(-rel)));   // bytes before the range: 0
+#pragma unroll 1
+    for (int j0 = 0; j0 < 64; j0 += 16) {
+        uint32_t cw[17];
+#pragma unroll
+        for (int t = 0; t < 17; ++t) {                    // 17 loads in flight; bytes outside the range read 0
+            const int64_t r = arel + 256 * (j0 + t) + 4 * lane;
+            cw[t] = (r > -4 && r < n) ? aw[64 * (j0 + t) + lane] : 0u;
         }
-        const uint32_t x = q ^ w;
-        if (j < 63) {
-            q = sb[0][x & 255] ^ sb[1][(x >> 8) & 255] ^ sb[2][(x >> 16) & 255] ^ sb[3][x >> 24];
-        } else {
-            q = sl[0][x & 255] ^ sl[1][(x >> 8) & 255] ^ sl[2][(x >> 16) & 255] ^ sl[3][x >> 24];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t dn = __shfl_down(cw[t], 1, 64);
+            const uint32_t wn = __shfl(cw[t + 1], 0, 64);
+            uint32_t w = __builtin_amdgcn_alignbyte(lane == 63 ? wn : dn, cw[t], sh);
+            const int64_t rel = s0 + 256 * (j0 + t) + 4 * lane;   // range offset of the word
+            if (rel < 0) w = rel <= -4 ? 0u : w & (0xFFFFFFFFu << (8 * (int)(-rel)));   // bytes before the range: 0
+            const uint32_t x = q ^ w;
+            if (j0 + t < 63) {
+                q = sb[0][x & 255] ^ sb[1][(x >> 8) & 255] ^ sb[2][(x >> 16) & 255] ^ sb[3][x >> 24];
+            } else {
+                q = sl[0][x & 255] ^ sl[1][(x >> 8) & 255] ^ sl[2][(x >> 16) & 255] ^ sl[3][x >> 24];
+            }
         }
     }
     uint32_t v = q ? multmodp(c_braid.lane[lane], q) : 0u;
@@ -2135,7 +2345,8 @@ struct PngBatchPlan {
     int64_t rows = 0, rblk = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
     size_t rows_lds = 16, parse_lds = 16;
     bool uniform = true;
-    size_t o_img, o_first, o_flt, o_tok, o_ntok, o_segb, o_gsum, o_goff, o_hist, o_tab, o_meta, o_rows, o_words;
+    size_t o_img, o_first, o_flt, o_lb, o_blk, o_trace, o_hist, o_tab, o_meta, o_rows, o_words;
+    size_t lb_bytes = 0;                        // look-back words + error flags + ticket (zeroed per call)
     size_t scratch = 0;
 };
 
@@ -2199,11 +2410,10 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
     L.o_img = take(sizeof(PngImg) * n);
     L.o_first = take(sizeof(int32_t) * 5 * n);
     L.o_flt = take((size_t)L.flt);
-    L.o_tok = take((size_t)L.toks * 4);
-    L.o_ntok = take((size_t)L.segs * 2);
-    L.o_segb = take((size_t)L.segs * 4);
-    L.o_gsum = take((size_t)L.grp * 4);
-    L.o_goff = take((size_t)L.grp * 4);
+    L.lb_bytes = align_up((size_t)L.grp * 8 + (size_t)n * 8, 16);   // P4 blocks = groups of kPngbGroup segments
+    L.o_lb = take(L.lb_bytes);
+    L.o_blk = take((size_t)L.grp * 16);
+    L.o_trace = take((size_t)L.segs * 12);
     L.o_hist = take((size_t)n * 316 * 4);
     L.o_tab = take(sizeof(DflTables) * n);
     L.o_meta = take(sizeof(PngMeta) * n);
@@ -2231,10 +2441,9 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     const size_t rows_lds = L.rows_lds, parse_lds = L.parse_lds;
     const bool uniform = L.uniform;
     auto at = [&](size_t rel) { return ws_off + rel; };
-    const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt), o_tok = at(L.o_tok),
-                 o_ntok = at(L.o_ntok), o_segb = at(L.o_segb), o_gsum = at(L.o_gsum), o_goff = at(L.o_goff),
-                 o_hist = at(L.o_hist), o_tab = at(L.o_tab), o_meta = at(L.o_meta), o_rows = at(L.o_rows),
-                 o_words = at(L.o_words);
+    const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt), o_lb = at(L.o_lb),
+                 o_blk = at(L.o_blk), o_hist = at(L.o_hist), o_tab = at(L.o_tab), o_meta = at(L.o_meta),
+                 o_rows = at(L.o_rows), o_words = at(L.o_words);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     PngBatch Bt{};
     Bt.img = reinterpret_cast<const PngImg*>(ws + o_img);
@@ -2253,11 +2462,20 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     Bt.eblk0 = fd + 3 * (size_t)n;
     Bt.cblk0 = fd + 4 * (size_t)n;
     Bt.flt = ws + o_flt;
-    Bt.tokens = reinterpret_cast<uint32_t*>(ws + o_tok);
-    Bt.ntok = reinterpret_cast<uint16_t*>(ws + o_ntok);
-    Bt.segb = reinterpret_cast<uint32_t*>(ws + o_segb);
-    Bt.gsum = reinterpret_cast<uint32_t*>(ws + o_gsum);
-    Bt.goff = reinterpret_cast<uint32_t*>(ws + o_goff);
+    Bt.lb_state = reinterpret_cast<unsigned long long*>(ws + o_lb);
+    Bt.lb_err = reinterpret_cast<uint32_t*>(ws + o_lb + (size_t)grp * 8);
+    Bt.lb_ticket = Bt.lb_err + n;
+    {
+        const char* e = std::getenv("OMR_PNG_LB_SKIP");
+        Bt.lb_skip = e && *e == '1';
+    }
+    Bt.blk_b0 = reinterpret_cast<uint32_t*>(ws + o_blk);
+    Bt.blk_b1 = Bt.blk_b0 + grp;
+    Bt.blk_cf = Bt.blk_b1 + grp;
+    Bt.blk_cl = Bt.blk_cf + grp;
+    Bt.total_pblk = (int32_t)pblk;
+    Bt.total_segs = L.segs;
+    Bt.trace = reinterpret_cast<uint32_t*>(ws + at(L.o_trace));
     Bt.hist = reinterpret_cast<uint32_t*>(ws + o_hist);
     Bt.tab = reinterpret_cast<DflTables*>(ws + o_tab);
     Bt.meta = reinterpret_cast<PngMeta*>(ws + o_meta);
@@ -2273,43 +2491,124 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
                     sizeof(int32_t) * 5 * n);
     if (st) return st;
     OMR_HIP(ctx, hipMemsetAsync(ws + o_hist, 0, (size_t)n * 316 * 4, ctx->stream));
+    OMR_HIP(ctx, hipMemsetAsync(ws + o_lb, 0, L.lb_bytes, ctx->stream));
     if (rows_lds > (size_t)60 * 1024)
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_filter),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds + 1024));
-    if (parse_lds > (size_t)60 * 1024)
+    if (parse_lds > (size_t)40 * 1024) {
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_parse),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)parse_lds + 2048));
+    }
     hipStream_t s = ctx->stream;
     // D1: the wave form for uniform batches of RGB tiles up to 1024 wide (OMR_PNG_FILTER_WAVE=0: the
     // workgroup form, for measurement)
-    static const bool wave_filter = [] {
-        const char* e = std::getenv("OMR_PNG_FILTER_WAVE");
-        return !(e && *e == '0');
-    }();
+    const char* fw_env = std::getenv("OMR_PNG_FILTER_WAVE");        // read per call: tests A/B it
+    const bool wave_filter = !(fw_env && *fw_env == '0');
     const int W0 = im[0].W, H0 = im[0].H;
     const int fw_m = (W0 / 4 + 63) / 64;
-    if (wave_filter && uniform && im[0].kind == kRgb && W0 % 4 == 0 && W0 <= 1024) {
-        Bt.fw_bands = (H0 + kFilterBandRows - 1) / kFilterBandRows;
-        const unsigned blocks = (unsigned)(((int64_t)n * Bt.fw_bands + 3) / 4);
-        switch (fw_m) {
-        case 1: hipLaunchKernelGGL(k_pngb_filter_wave<1>, dim3(blocks), dim3(256), 0, s, Bt); break;
-        case 2: hipLaunchKernelGGL(k_pngb_filter_wave<2>, dim3(blocks), dim3(256), 0, s, Bt); break;
-        case 3: hipLaunchKernelGGL(k_pngb_filter_wave<3>, dim3(blocks), dim3(256), 0, s, Bt); break;
-        default: hipLaunchKernelGGL(k_pngb_filter_wave<4>, dim3(blocks), dim3(256), 0, s, Bt); break;
+    // kernel timing (omr_ctx_enable_kernel_timing): kinds 20.. per stage, for bench.py's roofline
+    // of the batched PNG pipeline
+    {
+        KernelTimer t_filter(ctx, 20);
+        if (wave_filter && uniform && im[0].kind == kRgb && W0 % 4 == 0 && W0 <= 1024) {
+            Bt.fw_bands = (H0 + kFilterBandRows - 1) / kFilterBandRows;
+            const unsigned blocks = (unsigned)(((int64_t)n * Bt.fw_bands + 3) / 4);
+            switch (fw_m) {
+            case 1: hipLaunchKernelGGL(k_pngb_filter_wave<1>, dim3(blocks), dim3(256), fw_lds_bytes<1>(), s, Bt); break;
+            case 2: hipLaunchKernelGGL(k_pngb_filter_wave<2>, dim3(blocks), dim3(256), fw_lds_bytes<2>(), s, Bt); break;
+            case 3: hipLaunchKernelGGL(k_pngb_filter_wave<3>, dim3(blocks), dim3(256), fw_lds_bytes<3>(), s, Bt); break;
+            default: hipLaunchKernelGGL(k_pngb_filter_wave<4>, dim3(blocks), dim3(256), fw_lds_bytes<4>(), s, Bt); break;
+            }
+        } else {
+            hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
         }
-    } else {
-        hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
     }
-    hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
-    hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
-    hipLaunchKernelGGL(k_pngb_bits, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
-    hipLaunchKernelGGL(k_pngb_scan, dim3((unsigned)n), dim3(256), 0, s, Bt);
-    hipLaunchKernelGGL(k_pngb_offsets, dim3(1), dim3(1024), 0, s, Bt);
-    hipLaunchKernelGGL(k_pngb_write, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
-    hipLaunchKernelGGL(k_pngb_emit, dim3((unsigned)eblk), dim3(256), 0, s, Bt);
+    {
+        KernelTimer t(ctx, 21);
+        hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
+    }
+    {
+        KernelTimer t(ctx, 22);
+        hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
+    }
+    {
+        KernelTimer t(ctx, 23);
+        hipLaunchKernelGGL(k_pngb_encode, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
+    }
+    {
+        KernelTimer t(ctx, 24);
+        hipLaunchKernelGGL(k_pngb_fixup, dim3((unsigned)((grp + 255) / 256)), dim3(256), 0, s, Bt);
+        hipLaunchKernelGGL(k_pngb_meta, dim3((unsigned)n), dim3(256), 0, s, Bt);
+        hipLaunchKernelGGL(k_pngb_offsets, dim3(1), dim3(1024), 0, s, Bt);
+    }
+    {
+        KernelTimer t(ctx, 25);
+        hipLaunchKernelGGL(k_pngb_emit, dim3((unsigned)eblk), dim3(256), 0, s, Bt);
+    }
+    KernelTimer t_crc(ctx, 26);
     hipLaunchKernelGGL(k_pngb_crc, dim3((unsigned)cblk), dim3(256), 0, s, Bt);
     hipLaunchKernelGGL(k_pngb_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Bt);
     OMR_HIP(ctx, hipGetLastError());
+    return OMR_OK;
+}
+
+// One image through the batched pipeline (n = 1; round 5): the single-request entry points use the
+// same kernels as the batch -- device Huffman tables, no token buffers, one sync -- so a tile's
+// file is the batch's byte for byte.  Workspace from `base`: [file slot][meta][batch scratch].
+__global__ void __launch_bounds__(256) k_png_file_to_host(const uint8_t* __restrict__ src,
+                                                          const uint32_t* __restrict__ d_len,
+                                                          const int32_t* __restrict__ d_stat, uint8_t* __restrict__ host) {
+    const uint32_t len = *d_stat == OMR_OK ? *d_len : 0u;
+    const uint64_t i = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i == 0) {
+        reinterpret_cast<uint32_t*>(host)[0] = len;
+        reinterpret_cast<int32_t*>(host)[1] = *d_stat;
+    }
+    if (i >= len) return;
+    uint8_t* dst = host + 16;
+    if (i + 16 <= len) {
+        *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+        for (uint64_t j = i; j < len; ++j) dst[j] = src[j];
+    }
+}
+
+struct PngSingleLayout {
+    size_t o_out, o_meta, o_scr, fcap, total;
+};
+
+static omr_status png_single_layout(Ctx* ctx, const PngImgHost& im, size_t base, PngBatchPlan& L, PngSingleLayout& S) {
+    omr_status st = plan_png_batch(ctx, &im, 1, L);
+    if (st) return st;
+    S.fcap = align_up(omr_png_max_bytes(im.W, im.H, im.kind == kRgb ? 3 : 1), 256);
+    S.o_out = align_up(base, 256);
+    S.o_meta = S.o_out + S.fcap;
+    S.o_scr = S.o_meta + 256;
+    S.total = S.o_scr + L.scratch;
+    return OMR_OK;
+}
+
+// The caller has sized the workspace to S.total (a host-input caller stages its pixels below base).
+static omr_status png_single_batched(Ctx* ctx, PngImgHost im, PngBatchPlan& L, const PngSingleLayout& S,
+                                     uint8_t* out, size_t cap, size_t* out_len) {
+    uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(ws + S.o_meta);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(ws + S.o_meta + 8);
+    int32_t* d_st = reinterpret_cast<int32_t*>(ws + S.o_meta + 12);
+    omr_status st = launch_png_batch(ctx, L, &im, 1, S.o_scr, ws + S.o_out, S.fcap, d_off, d_len, d_st);
+    if (st) return st;
+    st = ensure_host_out(ctx, S.fcap + 16);
+    if (st) return st;
+    hipLaunchKernelGGL(k_png_file_to_host, dim3((unsigned)((S.fcap + 16 * 256 - 1) / (16 * 256))), dim3(256), 0,
+                       ctx->stream, ws + S.o_out, d_len, d_st, ctx->h_out);
+    OMR_HIP(ctx, hipGetLastError());
+    OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t len = reinterpret_cast<volatile uint32_t*>(ctx->h_out)[0];
+    const int32_t fst = reinterpret_cast<volatile int32_t*>(ctx->h_out)[1];
+    if (fst != OMR_OK || len == 0) return fail(ctx, fst ? fst : OMR_INTERNAL, "PNG: the encode failed on the device");
+    if (out_len) *out_len = len;
+    if (!out || cap < len) return fail(ctx, OMR_BUFFER_TOO_SMALL, "PNG output buffer too small");
+    std::memcpy(out, ctx->h_out + 16, len);
     return OMR_OK;
 }
 
@@ -2330,6 +2629,14 @@ omr_status omr_encode_png_device(omr_ctx* ctx, const uint32_t* d_argb, int32_t w
     if (!ctx) return OMR_INVALID_ARGUMENT;
     if (width <= 0 || height <= 0 || !d_argb) return fail(ctx, OMR_INVALID_ARGUMENT, "bad PNG input");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
+    if (width <= kPngbMaxSide && height <= kPngbMaxSide && ctx->png_single_batched) {
+        const PngImgHost im{d_argb, nullptr, kRgb, width, height, 0, 0, {0, 0, 0, 0}};
+        PngBatchPlan L;
+        PngSingleLayout S;
+        omr_status st = png_single_layout(ctx, im, 0, L, S);
+        if (!st) st = ensure_workspace(ctx, S.total);
+        return st ? st : png_single_batched(ctx, im, L, S, out, cap, out_len);
+    }
     omr_status st = ensure_workspace(ctx, png_scratch(kRgb, width, height));
     if (st) return st;
     return encode_png_ws(ctx, kRgb, d_argb, nullptr, width, height, 0, 0, nullptr, 0, out, cap, out_len);
@@ -2341,6 +2648,17 @@ omr_status omr_encode_png(omr_ctx* ctx, const uint32_t* argb, int32_t width, int
     if (width <= 0 || height <= 0 || !argb) return fail(ctx, OMR_INVALID_ARGUMENT, "bad PNG input");
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const size_t img = align_up((size_t)width * height * 4, 256);
+    if (width <= kPngbMaxSide && height <= kPngbMaxSide && ctx->png_single_batched) {
+        PngImgHost im{nullptr, nullptr, kRgb, width, height, 0, 0, {0, 0, 0, 0}};
+        PngBatchPlan L;
+        PngSingleLayout S;
+        omr_status st = png_single_layout(ctx, im, img, L, S);
+        if (!st) st = ensure_workspace(ctx, S.total);          // before the pixels are staged
+        if (st) return st;
+        im.argb = static_cast<const uint32_t*>(ctx->ws);
+        OMR_HIP(ctx, hipMemcpyAsync(ctx->ws, argb, (size_t)width * height * 4, hipMemcpyHostToDevice, ctx->stream));
+        return png_single_batched(ctx, im, L, S, out, cap, out_len);
+    }
     omr_status st = ensure_workspace(ctx, img + png_scratch(kRgb, width, height));
     if (st) return st;
     uint32_t* d = static_cast<uint32_t*>(ctx->ws);
@@ -2521,6 +2839,22 @@ omr_status omr_render_shape_mask_png(omr_ctx* ctx, const uint8_t* bits, size_t n
     }
     OMR_HIP(ctx, hipSetDevice(ctx->device));
     const int kind = width % 8 == 0 ? kIdx1 : kIdx8;   // bitsPerPixel 1 or 8 (:174-178)
+    const PngPlan P1 = png_plan(kind, width, height);
+    if (ctx->png_single_batched && P1.raw <= ((int64_t)1 << 27) &&
+        align_up((size_t)png_filter_lds(P1.rowlen - 1) + 16, 16) <= (size_t)kPngFilterLdsMax + 64) {
+        // the batch of one (the mask bits go to the workspace below base; packed flip done above)
+        const size_t nbits = align_up((size_t)((npx + 7) / 8), 256);
+        PngImgHost im{nullptr, nullptr, kind, width, height, flip_h ? 1 : 0, flip_v ? 1 : 0,
+                      {rgba[0], rgba[1], rgba[2], rgba[3]}};
+        PngBatchPlan L;
+        PngSingleLayout S;
+        omr_status st = png_single_layout(ctx, im, nbits, L, S);
+        if (!st) st = ensure_workspace(ctx, S.total);
+        if (st) return st;
+        im.bits = static_cast<const uint8_t*>(ctx->ws);
+        OMR_HIP(ctx, hipMemcpyAsync(ctx->ws, bits, (size_t)((npx + 7) / 8), hipMemcpyHostToDevice, ctx->stream));
+        return png_single_batched(ctx, im, L, S, out, cap, out_len);
+    }
     const size_t nb = align_up(n_bytes, 256);
     omr_status st = ensure_workspace(ctx, nb + png_scratch(kind, width, height));
     if (st) return st;

@@ -246,3 +246,63 @@ def test_mask_batch_capacity(pixel_flip):
     res = ctx.render_shape_mask_png_batch(masks, cap=2 * ((one + 15) // 16 * 16) + 15)
     assert [r[0] for r in res] == [0, 0, _lib.BUFFER_TOO_SMALL]
     assert res[0][1] == full[0][1] and res[1][1] == full[1][1]
+
+
+@pytest.mark.parametrize("kind,n,w,h", [("image", 3, 1024, 40), ("noise", 2, 1024, 9), ("image", 5, 512, 33),
+                                        ("image", 4, 100, 17), ("image", 2, 764, 21), ("flat", 3, 8, 5)])
+def test_png_batch_wave_filter_matches_workgroup_filter(ctx, kind, n, w, h, monkeypatch):
+    """D1's wave form (uniform RGB batches, W % 4 == 0, W <= 1024) writes the same filtered rows,
+    the same filter bytes and the same Adler partials as the workgroup form: the files are
+    byte-identical (OMR_PNG_FILTER_WAVE=0 selects the workgroup form, read per call)."""
+    argb = tiles(kind, n, w, h, 7 * w + h + n)
+    monkeypatch.setenv("OMR_PNG_FILTER_WAVE", "0")
+    ref = encode_batch(ctx, argb)
+    monkeypatch.setenv("OMR_PNG_FILTER_WAVE", "1")
+    got = encode_batch(ctx, argb)
+    for i in range(n):
+        assert got[i][0] == 0 and ref[i][0] == 0
+        assert got[i][2] == ref[i][2], f"tile {i}: wave-form file differs"
+        np.testing.assert_array_equal(np.asarray(decode(got[i][2])), rgb_of(argb[i]))
+
+
+def test_png_batch_wave_filter_rendered_c2(ctx, monkeypatch):
+    """The bench's tiles (C2 rendered on the GPU, 1024^2): wave-form and workgroup-form D1 give
+    byte-identical files."""
+    import torch
+    from omr.synthetic import c2_channels, tile_u16
+    import oracle_lib as O
+    w = h = 1024
+    outs = []
+    for t in range(2):
+        planes = [p.astype(">u2") for p in tile_u16(t, 4, h, w)]
+        st, argb = O.render(c2_channels(4), planes, _lib.PIXELS_UINT16, w, h, big_endian=True)
+        outs.append(argb)
+    argb = np.stack(outs)
+    monkeypatch.setenv("OMR_PNG_FILTER_WAVE", "0")
+    ref = encode_batch(ctx, argb)
+    monkeypatch.setenv("OMR_PNG_FILTER_WAVE", "1")
+    got = encode_batch(ctx, argb)
+    for i in range(2):
+        assert got[i][2] == ref[i][2], f"tile {i}: wave-form file differs"
+
+
+def test_single_request_paths_batched_and_legacy(monkeypatch):
+    """Single PNG / mask requests run the batched pipeline with n = 1 (round 5); the legacy
+    single-image pipeline (OMR_PNG_SINGLE_BATCHED=0, read at context creation; still the path
+    for images beyond 4096 px) gives the same pixels."""
+    import omr
+    argb = tiles("image", 1, 300, 77, 5)[0]
+    rng = np.random.default_rng(3)
+    bits = rng.integers(0, 256, (37 * 21 + 7) // 8, dtype=np.uint8).tobytes()
+    outs = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("OMR_PNG_SINGLE_BATCHED", flag)
+        c = omr.Context(0)
+        try:
+            outs[flag] = (c.encode_png(argb, 300, 77), c.render_shape_mask_png(bits, 37, 21, (9, 8, 7, 200), True, False))
+        finally:
+            c.close()
+    for k in (0, 1):
+        np.testing.assert_array_equal(np.asarray(decode(outs["1"][k]).convert("RGBA")),
+                                      np.asarray(decode(outs["0"][k]).convert("RGBA")))
+    np.testing.assert_array_equal(np.asarray(decode(outs["1"][0])), rgb_of(argb))

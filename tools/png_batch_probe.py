@@ -55,6 +55,16 @@ def main():
         ln = lens[:n].cpu().numpy()
         res[f"batch{n}"] = {"ms_per_call": round(1e3 * el / iters, 4), "tiles_per_s": round(n * iters / el, 1),
                             "mean_file_bytes": int(ln.mean()), "status_ok": int((stat[:n] == 0).sum().item())}
+        ctx.kernel_timings()                            # per-stage HIP events (kinds 20-26)
+        ctx.enable_kernel_timing(True)
+        for _ in range(4):
+            step()
+        ctx.synchronize()
+        ctx.enable_kernel_timing(False)
+        acc = {}
+        for ms, kind in ctx.kernel_timings():
+            acc.setdefault(int(kind), []).append(ms)
+        res[f"batch{n}"]["stage_ms"] = {k: round(sum(v) / len(v), 4) for k, v in sorted(acc.items())}
     # single-tile path (host D3, one sync per tile)
     t0 = time.perf_counter()
     k = 32
