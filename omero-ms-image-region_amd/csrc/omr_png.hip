@@ -676,8 +676,20 @@ template <typename Tok>
 __device__ __forceinline__ void lz_seg_tokens(const LzSeg& L, const uint8_t* s_win, int64_t wbeg,
                                               const DeflateTabs& T, Tok&& tok) {
     const uint8_t* f = s_win - wbeg;
+    // positions where some candidate's run of equal bytes reaches 3: the only places a match can
+    // start; the bytes in between are literals and skip the candidate evaluation
+    uint32_t A = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (k >= L.nd) break;
+        A |= L.m[k] & (L.m[k] >> 1) & (L.m[k] >> 2);
+    }
     int p = 0;
     while (p < L.n) {
+        const uint32_t ap = p < 32 ? A >> p : 0u;
+        const int q = ap ? p + __builtin_ctz(ap) : L.n;        // the next match start (or the end)
+        for (; p < q; ++p) tok((uint32_t)f[L.beg + p], p, -1);
+        if (p >= L.n) break;
         int best = 0, bk = 0;
         uint32_t bd = 0;
 #pragma unroll
@@ -1468,11 +1480,13 @@ static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H
 //                      histograms and a 12-byte parse trace per segment (round 5: no token buffer)
 //   P3 k_pngb_tables   one workgroup per image: length-limited Huffman code + block header (D3
 //                      on the device: no host round trip; N workgroups run side by side)
-//   P4 k_pngb_encode   one workgroup per parse block, in ticket order: the tokens again from the
-//                      traces and the stream bytes, each lane's code bits, the block's bit offset by decoupled look-back over the
-//                      image's earlier blocks, codes assembled in LDS, whole words stored, the
-//                      block's two partial words kept aside (round 5: replaces token stores, a
-//                      bits pass and a write pass that moved ~4x the stream in tokens)
+//   P3b k_pngb_block_offsets  one workgroup per image: every parse block's code bits from its
+//                      symbol counts x the code lengths, scanned into bit offsets
+//   P4 k_pngb_encode   one workgroup per 256 segments: the tokens again from the traces and the
+//                      stream bytes, each lane's code bits and in-group offset, codes assembled
+//                      in LDS, whole words stored, the group's two partial words kept aside
+//                      (round 5: replaces token stores and a bits / scan / write sequence that
+//                      moved ~4x the stream in tokens)
 //   P5 k_pngb_fixup    one lane per block: the words blocks share, ORed from the kept parts
 //   P5b k_pngb_meta    one workgroup per image: stream length, stored vs dynamic, Adler-32 from
 //                      the row partials
@@ -1521,10 +1535,9 @@ struct PngBatch {
     const int32_t* eblk0;
     const int32_t* cblk0;
     uint8_t* flt;
-    unsigned long long* lb_state;               // [parse blocks] look-back words (flag | bit offset)
-    uint32_t* lb_err;                           // [n] a look-back gave up (the image fails, no hang)
-    uint32_t* lb_ticket;                        // [n] P4 block order per image
-    int32_t lb_skip, pad4;                      // measurement only (OMR_PNG_LB_SKIP=1): no look-back, wrong output
+    uint16_t* bh;                               // [parse blocks][316] symbol counts of each parse block
+    uint32_t* poff;                             // [parse blocks] bit offset of each parse block's codes
+    uint32_t* img_bits;                         // [n] stream bits: header + codes + EOB
     uint32_t* blk_b0;                           // [parse blocks] first bit of the block in its stream
     uint32_t* blk_b1;                           // [parse blocks] one past its last bit
     uint32_t* blk_cf;                           // [parse blocks] its first (partial) word
@@ -1763,6 +1776,32 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
     if (lane < 2 * (y1 - y0)) rs[lane] = lane == 0 ? s1 : lane == 1 ? s2 : 0ull;
 }
 
+__device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t w = lane < nw ? s_wave[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;
+    }
+    __syncthreads();
+    const uint32_t off = wid ? s_wave[wid - 1] : 0;
+    total = s_wave[nw - 1];
+    __syncthreads();
+    return off + x - v;
+}
+
 // P2: the parse of one block: the image's symbol histograms (four LDS copies, lane & 3, so the
 // common literals' atomics spread over four addresses) and each segment's parse trace -- token
 // starts S, match starts M, the matches' candidate indices D (2 bits each, <= 10 per segment) --
@@ -1806,12 +1845,58 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     }
     __syncthreads();
     uint32_t* h = B.hist + (size_t)i * 316;
+    uint16_t* bh = B.bh + (size_t)blockIdx.x * 316;            // <= 4096 tokens per block: u16
     for (int k = threadIdx.x; k < 316; k += kParseLanes) {
         uint32_t v = 0;
 #pragma unroll
         for (int c = 0; c < kHistCopies; ++c) v += lh[c][k];
+        bh[k] = (uint16_t)v;
         if (v) atomicAdd(&h[k], v);
     }
+}
+
+// P3b: one workgroup per image, after the code is known: each parse block's code bits are its
+// symbol counts times the code lengths (extra bits included), an exclusive scan over the image's
+// blocks from the header's end gives every block's first bit -- so P4 needs no inter-block
+// communication at all.
+__global__ void __launch_bounds__(256) k_pngb_block_offsets(PngBatch B) {
+    __shared__ uint32_t cost[316];
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_carry;
+    const int i = blockIdx.x;
+    const PngImg& I = B.img[i];
+    const DflTables* T = B.tab + i;
+    for (int k = threadIdx.x; k < 316; k += 256) {
+        uint32_t c;
+        if (k < 257) c = T->llen[k];
+        else if (k < 286) c = T->llen[k] + len_xbits_of(k - 257);
+        else c = T->dlen[k - 286] + dist_xbits_of(k - 286);
+        cost[k] = c;
+    }
+    const uint32_t hb = T->hdr[95];
+    if (threadIdx.x == 0) s_carry = hb;
+    __syncthreads();
+    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
+    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
+    for (int j0 = 0; j0 < npb; j0 += 256) {
+        const int j = j0 + threadIdx.x;
+        uint32_t bits = 0;
+        if (j < npb) {
+            const uint32_t* c2 = reinterpret_cast<const uint32_t*>(B.bh + (size_t)(p0 + j) * 316);   // 4-aligned
+            for (int k = 0; k < 158; ++k) {
+                const uint32_t v = c2[k];
+                bits += (v & 0xFFFFu) * cost[2 * k] + (v >> 16) * cost[2 * k + 1];
+            }
+        }
+        uint32_t tot;
+        const uint32_t ex = pngb_block_excl_scan(bits, s_wave, tot);
+        const uint32_t base = s_carry;
+        if (j < npb) B.poff[p0 + j] = base + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = base + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) B.img_bits[i] = s_carry + T->llen[256];   // + EOB
 }
 
 // The tokens of a segment from its parse trace (P2): t as lz_seg_tokens produced them.
@@ -1835,38 +1920,10 @@ __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
     png_build_tables(B.hist + (size_t)blockIdx.x * 316, B.tab + blockIdx.x);
 }
 
-__device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[wid] = x;
-    __syncthreads();
-    if (wid == 0) {
-        uint32_t w = lane < nw ? s_wave[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(w, o, 64);
-            if (lane >= o) w += y;
-        }
-        if (lane < nw) s_wave[lane] = w;
-    }
-    __syncthreads();
-    const uint32_t off = wid ? s_wave[wid - 1] : 0;
-    total = s_wave[nw - 1];
-    __syncthreads();
-    return off + x - v;
-}
-
-// P4: one workgroup per parse block.  Workgroups take blocks in ticket order (an atomic counter),
-// so every block an encoder waits on belongs to a workgroup that started earlier: the look-back
-// cannot deadlock whatever order the hardware dispatches in.
-constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 1ull << 63;
+// P4: one workgroup per group of kPngbGroup segments (two parse blocks): its bit range comes
+// from P3b, so groups run independently.
 constexpr int kEncWords = kPngbGroup * kSeg * 16 / 32 + 96 + 4;   // <= 16 bits per byte + header
-constexpr uint32_t kLbSpinMax = 1u << 22;
+static_assert(kPngbGroup == 2 * kParseLanes, "P4 groups are two parse blocks");
 
 __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     __shared__ __attribute__((aligned(16))) uint8_t s_seg[kPngbGroup * kSeg];   // the block's stream bytes
@@ -1875,15 +1932,11 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     __shared__ uint16_t lcode[286], dcode[30];
     __shared__ uint32_t sw[kEncWords];
     __shared__ uint32_t s_wave[kPngbGroup / 64];
-    __shared__ uint32_t s_tk, s_b0, s_b1;
-    // the image from the workgroup index, the block within it from the image's ticket counter
     const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const int64_t gfirst = B.uniform ? (int64_t)i * B.grp_per : I.grp0;
-    if (threadIdx.x == 0) s_tk = B.lb_skip ? (uint32_t)(blockIdx.x - gfirst) : atomicAdd(&B.lb_ticket[i], 1u);
-    __syncthreads();
-    const int64_t blk = s_tk;
-    const int64_t g = gfirst + blk;                             // this workgroup's block
+    const int64_t blk = (int64_t)blockIdx.x - gfirst;
+    const int64_t g = blockIdx.x;                               // this workgroup's group
     const DflTables* Tb = B.tab + i;
     for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = Tb->llen[k]; lcode[k] = Tb->lcode[k]; }
     if (threadIdx.x < 30) { dlen[threadIdx.x] = Tb->dlen[threadIdx.x]; dcode[threadIdx.x] = Tb->dcode[threadIdx.x]; }
@@ -1919,57 +1972,19 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     uint32_t total;
     const uint32_t ex = pngb_block_excl_scan(nb, s_wave, total);
     const uint32_t hb = Tb->hdr[95];
-    // The block's bit range: publish the aggregate, then look back with the first wave -- lane l
-    // reads the state of block g - 1 - l (64 predecessors per round trip); the nearest inclusive
-    // prefix ends the walk, the aggregates in front of it add up.
-    // The state words carry flag and value in one 8-byte granule (the data is the flag): relaxed
-    // agent-scope stores and loads, no release / acquire fence -- an agent-scope release writes the
-    // XCD's L2 back on this multi-XCD part (~us per block; MI355X_MICROARCH.md, visibility).
-    if (threadIdx.x < 64) {
-        typedef __attribute__((address_space(1))) unsigned long long gu64;
-        gu64* st = (gu64*)(B.lb_state);
-        const int lane = threadIdx.x;
-        uint32_t b0 = 0;
-        if (blk > 0 && !B.lb_skip) {
-            if (lane == 0) __hip_atomic_store(&st[g], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t jend = g;
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t j = jend - 1 - lane;
-                const unsigned long long v =
-                    j >= gfirst ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-                const uint64_t incl = __ballot((v & kLbIncl) != 0);
-                const uint64_t wait = __ballot((v & (kLbIncl | kLbAgg)) == 0);
-                const int f = incl ? __ffsll((unsigned long long)incl) - 1 : 64;   // nearest inclusive lane
-                const uint64_t upto = f == 64 ? ~0ull : (2ull << f) - 1ull;       // lanes 0..f
-                if (wait & upto) {                              // a predecessor has not published yet
-                    if (++spins > kLbSpinMax) {
-                        if (lane == 0) atomicOr(&B.lb_err[i], 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                uint32_t x = (((upto >> lane) & 1ull) != 0) ? (uint32_t)v : 0u;
-                for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-                b0 += x;
-                if (f < 64) break;
-                jend -= 64;
-            }
-        }
-        const uint32_t b1 = (blk == 0 ? hb : b0) + total;
-        if (lane == 0) {
-            __hip_atomic_store(&st[g], kLbIncl | b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_b0 = b0;
-            s_b1 = b1;
-        }
-    }
-    __syncthreads();
-    const uint32_t b0 = s_b0, b1 = s_b1, w0 = b0 >> 5;
+    // the group's bit range from P3b: its first parse block's offset (the header opens group 0)
+    // to the next group's (or the stream's end)
+    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
+    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
+    const uint32_t c0 = B.poff[p0 + 2 * blk];                   // first code bit of the group
+    const uint32_t b0 = blk == 0 ? 0u : c0;
+    const uint32_t b1 = 2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i];
+    (void)total;                                                // == b1 - c0 (the same codes)
+    const uint32_t w0 = b0 >> 5;
     if (blk == 0 && threadIdx.x == 0)
         for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&sw[k], Tb->hdr[k]);
     if (live) {
-        const uint32_t pos = (blk == 0 ? hb : b0) + ex - 32 * w0;   // bit position in sw
+        const uint32_t pos = c0 + ex - 32 * w0;                 // bit position in sw
         uint64_t acc = 0;
         int nacc = (int)(pos & 31);
         uint32_t wpos = pos >> 5;
@@ -2024,7 +2039,8 @@ __global__ void __launch_bounds__(256) k_pngb_meta(PngBatch B) {
     const int i = blockIdx.x;
     const PngImg& I = B.img[i];
     const int64_t glast = (B.uniform ? (int64_t)i * B.grp_per : I.grp0) + (I.nseg + kPngbGroup - 1) / kPngbGroup - 1;
-    const uint32_t total = B.blk_b1[glast];                    // header + codes + EOB
+    const uint32_t total = B.img_bits[i];                      // header + codes + EOB
+    (void)glast;
     const int64_t zdyn = 2 + ((int64_t)total + 7) / 8 + 4, zstored = 2 + 5 * I.nblk + I.raw + 4;
     const bool stored = zdyn >= zstored;
     unsigned long long s1 = 0, s2 = 0;
@@ -2052,7 +2068,7 @@ __global__ void __launch_bounds__(256) k_pngb_meta(PngBatch B) {
         M.hbits = hb;
         M.tot_bits = total - hb;
         M.stored = stored ? 1 : 0;
-        M.status = B.lb_err[i] ? OMR_INTERNAL : OMR_OK;
+        M.status = OMR_OK;
     }
 }
 
@@ -2345,8 +2361,7 @@ struct PngBatchPlan {
     int64_t rows = 0, rblk = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
     size_t rows_lds = 16, parse_lds = 16;
     bool uniform = true;
-    size_t o_img, o_first, o_flt, o_lb, o_blk, o_trace, o_hist, o_tab, o_meta, o_rows, o_words;
-    size_t lb_bytes = 0;                        // look-back words + error flags + ticket (zeroed per call)
+    size_t o_img, o_first, o_flt, o_bh, o_poff, o_blk, o_trace, o_hist, o_tab, o_meta, o_rows, o_words;
     size_t scratch = 0;
 };
 
@@ -2410,8 +2425,8 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
     L.o_img = take(sizeof(PngImg) * n);
     L.o_first = take(sizeof(int32_t) * 5 * n);
     L.o_flt = take((size_t)L.flt);
-    L.lb_bytes = align_up((size_t)L.grp * 8 + (size_t)n * 8, 16);   // P4 blocks = groups of kPngbGroup segments
-    L.o_lb = take(L.lb_bytes);
+    L.o_bh = take((size_t)L.pblk * 316 * 2);
+    L.o_poff = take((size_t)L.pblk * 4 + (size_t)n * 4);
     L.o_blk = take((size_t)L.grp * 16);
     L.o_trace = take((size_t)L.segs * 12);
     L.o_hist = take((size_t)n * 316 * 4);
@@ -2441,7 +2456,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     const size_t rows_lds = L.rows_lds, parse_lds = L.parse_lds;
     const bool uniform = L.uniform;
     auto at = [&](size_t rel) { return ws_off + rel; };
-    const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt), o_lb = at(L.o_lb),
+    const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt),
                  o_blk = at(L.o_blk), o_hist = at(L.o_hist), o_tab = at(L.o_tab), o_meta = at(L.o_meta),
                  o_rows = at(L.o_rows), o_words = at(L.o_words);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
@@ -2462,13 +2477,9 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     Bt.eblk0 = fd + 3 * (size_t)n;
     Bt.cblk0 = fd + 4 * (size_t)n;
     Bt.flt = ws + o_flt;
-    Bt.lb_state = reinterpret_cast<unsigned long long*>(ws + o_lb);
-    Bt.lb_err = reinterpret_cast<uint32_t*>(ws + o_lb + (size_t)grp * 8);
-    Bt.lb_ticket = Bt.lb_err + n;
-    {
-        const char* e = std::getenv("OMR_PNG_LB_SKIP");
-        Bt.lb_skip = e && *e == '1';
-    }
+    Bt.bh = reinterpret_cast<uint16_t*>(ws + at(L.o_bh));
+    Bt.poff = reinterpret_cast<uint32_t*>(ws + at(L.o_poff));
+    Bt.img_bits = Bt.poff + pblk;
     Bt.blk_b0 = reinterpret_cast<uint32_t*>(ws + o_blk);
     Bt.blk_b1 = Bt.blk_b0 + grp;
     Bt.blk_cf = Bt.blk_b1 + grp;
@@ -2491,7 +2502,6 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
                     sizeof(int32_t) * 5 * n);
     if (st) return st;
     OMR_HIP(ctx, hipMemsetAsync(ws + o_hist, 0, (size_t)n * 316 * 4, ctx->stream));
-    OMR_HIP(ctx, hipMemsetAsync(ws + o_lb, 0, L.lb_bytes, ctx->stream));
     if (rows_lds > (size_t)60 * 1024)
         OMR_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(k_pngb_filter),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds + 1024));
@@ -2530,6 +2540,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     {
         KernelTimer t(ctx, 22);
         hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
+        hipLaunchKernelGGL(k_pngb_block_offsets, dim3((unsigned)n), dim3(256), 0, s, Bt);
     }
     {
         KernelTimer t(ctx, 23);
