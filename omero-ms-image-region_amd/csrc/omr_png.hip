@@ -1736,6 +1736,7 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
         uint32_t* gw = reinterpret_cast<uint32_t*>(B.flt + row0 + u + 1);   // out dword J
         const int jfull = (rb - u) >> 2;                       // out dwords J < jfull lie inside the row
         const unsigned long long rbase = (unsigned long long)(raw - ypos - 1);
+        uint32_t a1 = 0, aj = 0, ad = 0;                      // this row's Adler partials in 32 bits
 #pragma unroll
         for (int t = 0; t < 3 * M; ++t) {
             const int j = lane + 64 * t;
@@ -1746,8 +1747,9 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
                 const uint32_t w = c[t];
                 if (j < jfull) gw[j] = __builtin_amdgcn_alignbyte(hi, w, u);
                 const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
-                s1 += sv;
-                s2 += (rbase - 4ull * j) * sv - __builtin_amdgcn_udot4(w, 0x03020100u, 0u, false);
+                a1 += sv;
+                aj += (uint32_t)j * sv;                        // <= 767 * 12 * 1020 per lane and row
+                ad = __builtin_amdgcn_udot4(w, 0x03020100u, ad, false);
                 // bytes outside the whole out dwords: the row's first u, its last (rb - u) & 3
                 if (4 * j < u || 4 * j + 3 >= u + 4 * jfull) {
                     for (int b = 0; b < 4; ++b) {
@@ -1757,6 +1759,8 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
                 }
             }
         }
+        s1 += a1;                                              // sum (raw - pos) * byte over the row
+        s2 += rbase * a1 - 4ull * aj - ad;
         if (lane == 0) {
             flt[ypos] = (uint8_t)f;
             s1 += (unsigned long long)f;
@@ -1802,20 +1806,20 @@ __device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s
     return off + x - v;
 }
 
-// P2: the parse of one block: the image's symbol histograms (four LDS copies, lane & 3, so the
-// common literals' atomics spread over four addresses) and each segment's parse trace -- token
+// P2: the parse of one block: the image's symbol histograms (eight LDS copies, lane & 7, two
+// 16-bit counts per dword, so the common literals' atomics spread over eight addresses) and each segment's parse trace -- token
 // starts S, match starts M, the matches' candidate indices D (2 bits each, <= 10 per segment) --
 // so that P4 codes the segment without parsing it again.
-constexpr int kHistCopies = 4;
+constexpr int kHistCopies = 8;                 // copies of the block histogram (lane & 7), u16 pairs
 
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
-    __shared__ uint32_t lh[kHistCopies][286 + 30];
+    __shared__ uint32_t lh[kHistCopies][158];              // bin b: half (b & 1) of dword b >> 1
     __shared__ DeflateTabs T;
     const int i = pngb_image(B, B.pblk0, B.pblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
-    for (int k = threadIdx.x; k < kHistCopies * 316; k += kParseLanes) (&lh[0][0])[k] = 0;
+    for (int k = threadIdx.x; k < kHistCopies * 158; k += kParseLanes) (&lh[0][0])[k] = 0;
     lz_load_tabs(T);
     int64_t wbeg, bend;
     lz_stage(B.flt + I.flt, I.raw, blk, I.back, s_win, wbeg, bend);
@@ -1832,10 +1836,11 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
             if (t & 0x80000000u) {
                 M |= 1u << p;
                 D |= (uint32_t)k << (2 * nm++);
-                atomicAdd(&h[257 + (t & 31)], 1u);
-                atomicAdd(&h[286 + ((t >> 5) & 31)], 1u);
+                const uint32_t a = 257 + (t & 31), b = 286 + ((t >> 5) & 31);
+                atomicAdd(&h[a >> 1], 1u << (16 * (a & 1)));
+                atomicAdd(&h[b >> 1], 1u << (16 * (b & 1)));
             } else {
-                atomicAdd(&h[t], 1u);
+                atomicAdd(&h[t >> 1], 1u << (16 * (t & 1)));
             }
         });
         const int64_t gs = I.seg0 + s;
@@ -1849,7 +1854,7 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     for (int k = threadIdx.x; k < 316; k += kParseLanes) {
         uint32_t v = 0;
 #pragma unroll
-        for (int c = 0; c < kHistCopies; ++c) v += lh[c][k];
+        for (int c = 0; c < kHistCopies; ++c) v += (lh[c][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
         bh[k] = (uint16_t)v;
         if (v) atomicAdd(&h[k], v);
     }
@@ -1938,9 +1943,17 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     const int64_t blk = (int64_t)blockIdx.x - gfirst;
     const int64_t g = blockIdx.x;                               // this workgroup's group
     const DflTables* Tb = B.tab + i;
+    // the group's bit range from P3b: its first parse block's offset (the header opens group 0)
+    // to the next group's (or the stream's end)
+    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
+    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
+    const uint32_t c0 = B.poff[p0 + 2 * blk];                   // first code bit of the group
+    const uint32_t b0 = blk == 0 ? 0u : c0;
+    const uint32_t b1 = 2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i];
+    const uint32_t w0 = b0 >> 5, w1 = (b1 - 1) >> 5;
     for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = Tb->llen[k]; lcode[k] = Tb->lcode[k]; }
     if (threadIdx.x < 30) { dlen[threadIdx.x] = Tb->dlen[threadIdx.x]; dcode[threadIdx.x] = Tb->dcode[threadIdx.x]; }
-    for (int k = threadIdx.x; k < kEncWords; k += kPngbGroup) sw[k] = 0;
+    for (uint32_t k = threadIdx.x; k <= min(w1 - w0, (uint32_t)kEncWords - 1); k += kPngbGroup) sw[k] = 0;
     lz_load_tabs(T);
     {
         const int64_t bbeg = blk * kPngbGroup * kSeg, bend = min(I.raw, bbeg + (int64_t)kPngbGroup * kSeg);
@@ -1972,15 +1985,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     uint32_t total;
     const uint32_t ex = pngb_block_excl_scan(nb, s_wave, total);
     const uint32_t hb = Tb->hdr[95];
-    // the group's bit range from P3b: its first parse block's offset (the header opens group 0)
-    // to the next group's (or the stream's end)
-    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
-    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
-    const uint32_t c0 = B.poff[p0 + 2 * blk];                   // first code bit of the group
-    const uint32_t b0 = blk == 0 ? 0u : c0;
-    const uint32_t b1 = 2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i];
     (void)total;                                                // == b1 - c0 (the same codes)
-    const uint32_t w0 = b0 >> 5;
     if (blk == 0 && threadIdx.x == 0)
         for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&sw[k], Tb->hdr[k]);
     if (live) {
@@ -2005,7 +2010,6 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     __syncthreads();
     // whole words inside [b0, b1) go out; the first and last (shared with the neighbouring
     // blocks) are kept for P5
-    const uint32_t w1 = (b1 - 1) >> 5;
     uint32_t* w = B.words + I.words;
     for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup)
         if (b0 <= 32 * k && b1 >= 32 * k + 32) w[k] = sw[k - w0];
