@@ -22,6 +22,7 @@ TAG=${1:?tag}; shift
 O=gpurun_out/$TAG; mkdir -p $O
 R=$PWD
 export TMPDIR=/tmp
+export C5_TILES=${C5_TILES:-64} JPEG_PROBE_TILES=${JPEG_PROBE_TILES:-256}   # the bench's launch sizes
 
 run() {   # run <seconds> <log> <cmd...>: one GPU step under its own limit; stop the script on failure
     local t=$1 log=$2; shift 2
