@@ -320,6 +320,43 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32")
 
 
+PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "png_sq.json")
+# batched PNG stages (omr_png.hip launch_png_batch timer kinds) -> the kernels they launch
+PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse",),
+                     22: ("k_pngb_tables", "k_pngb_block_offsets"), 23: ("k_pngb_encode",),
+                     24: ("k_pngb_fixup", "k_pngb_meta", "k_pngb_offsets"), 25: ("k_pngb_emit",),
+                     26: ("k_pngb_crc", "k_pngb_finish")}
+
+
+def png_valu_roofline(stage_ms):
+    """VALU issue of each batched PNG stage (256 C2 tiles per call): SQ_INSTS_VALU per launch from
+    the committed SQ passes (tools/gpu.sh sq=png -> tools/sq_json.py -> profiles/r05/png_sq.json,
+    the same probe workload) x 2 issue cycles, over the stage's measured time; peak = every SIMD
+    issuing every cycle.  Next to the stage's HBM frac it says which bound the stage is nearer."""
+    try:
+        with open(PNG_SQ) as fh:
+            doc = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    ks = doc.get("kernels", {})
+    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S,
+           "source": os.path.relpath(PNG_SQ, os.path.dirname(os.path.abspath(__file__)))}
+    for kind, names in PNG_STAGE_KERNELS.items():
+        ms = stage_ms.get(kind)
+        rows = [v for k, v in ks.items() if any(k.endswith("::" + nm) for nm in names)]
+        if not ms or not rows:
+            continue
+        valu = sum(r["counters"].get("SQ_INSTS_VALU", 0.0) for r in rows)
+        conf = sum(r["counters"].get("SQ_LDS_BANK_CONFLICT", 0.0) for r in rows)
+        lds = sum(r["counters"].get("SQ_LDS_IDX_ACTIVE", 0.0) for r in rows)
+        ach = VALU_CYCLES * valu / (ms * 1e-3)
+        out[str(kind)] = {"kernels": list(names), "valu_instr_per_launch": valu,
+                          "achieved": round(ach, 1), "frac": round(ach / VALU_PEAK_ISSUE_CYCLES_PER_S, 4),
+                          "lds_bank_conflict_share": round(conf / lds, 3) if lds else None,
+                          "avg_ms": round(ms, 5)}
+    return out
+
+
 JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04u2.json")
 JPEG_FUSED_KERNELS = ("k_jpeg_render_fdct", "k_jpeg_block_bits", "k_jpeg_group_scan", "k_jpeg_huff_thread",
                       "k_jpeg_tile_scan", "k_jpeg_stuff_count", "k_jpeg_stuff_batch")
@@ -750,13 +787,13 @@ def png_section(torch, ctx, data):
         leg = {"tiles_per_s": round(n * reps / el, 1), "ms_per_call": round(ms, 4), "mean_png_bytes": int(ln.mean())}
         # Per-stage roofline from HIP events around each stage's launches (kinds 20-26,
         # omr_png.hip launch_png_batch).  Algorithmic bytes per call: the filter reads the ARGB
-        # tiles and writes the filtered streams; the histogram pass and the encoder read the
-        # streams (the encoder also writes the deflate words, ~ the files); emit reads the words
-        # and writes the files; CRC reads the files.  HBM-bound stages against 8 TB/s.
-        stages = {20: ("filter (D1)", n * TILE * TILE * 4 + n * raw),
-                  21: ("histogram parse (P2)", n * raw),
-                  22: ("huffman tables (P3)", 0),
-                  23: ("encode (P4: parse + code + look-back)", n * raw + files),
+        # tiles and writes the filtered streams; the parse and the encoder read the streams (the
+        # encoder also writes the deflate words, ~ the files); emit reads the words and writes the
+        # files; CRC reads the files.  HBM-bound stages against 8 TB/s.
+        stages = {20: ("filter (P1)", n * TILE * TILE * 4 + n * raw),
+                  21: ("LZ77 parse + histograms (P2)", n * raw),
+                  22: ("huffman tables + block offsets (P3, P3b)", 0),
+                  23: ("encode (P4: codes from the parse traces)", n * raw + files),
                   24: ("fixup + meta + offsets", 0),
                   25: ("emit (P8)", 2 * files),
                   26: ("crc (P9)", files)}
@@ -778,6 +815,10 @@ def png_section(torch, ctx, data):
                            "frac": round(alg_all / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "algorithmic_bytes_per_call": alg_all, "sum_of_stage_ms": round(stage_ms, 5),
                            "stages": per}
+        if n == 256:
+            vr = png_valu_roofline(avg)
+            if vr:
+                leg["valu_roofline"] = vr
         batched[f"tiles_per_call_{n}"] = leg
     res["batched"] = batched
     if "tiles_per_call_256" in batched:

@@ -350,22 +350,40 @@ __device__ __forceinline__ uint32_t sub8(uint32_t x, uint32_t y) {
     return ((x | 0x80808080u) - (y & 0x7F7F7F7Fu)) ^ ((x ^ ~y) & 0x80808080u);
 }
 
+// Paeth predictors of two bytes held as 16-bit halves (values 0..255), packed 16-bit arithmetic
+// (v_pk_*): pa = |b - c|, pb = |a - c|, pc = |a + b - 2c|; a when pa <= min(pb, pc), else b when
+// pb <= pc, else c -- the PNG rule, selected by the sign masks of two differences.
+typedef short omr_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t paeth_pairs(uint32_t a, uint32_t b, uint32_t c) {
+    const omr_s16x2 va = __builtin_bit_cast(omr_s16x2, a), vb = __builtin_bit_cast(omr_s16x2, b),
+                    vc = __builtin_bit_cast(omr_s16x2, c);
+    const omr_s16x2 d1 = vb - vc, d2 = va - vc;
+    const omr_s16x2 pa = __builtin_elementwise_abs(d1), pb = __builtin_elementwise_abs(d2),
+                    pc = __builtin_elementwise_abs(d1 + d2);
+    const omr_s16x2 m = __builtin_elementwise_min(pb, pc);
+    const uint32_t na = __builtin_bit_cast(uint32_t, (omr_s16x2)((m - pa) >> 15));   // ~0: not a
+    const uint32_t nb = __builtin_bit_cast(uint32_t, (omr_s16x2)((pc - pb) >> 15));  // ~0: c over b
+    const uint32_t bc = (nb & c) | (~nb & b);
+    return (na & bc) | (~na & a);
+}
+
+// Paeth predictor of 4 row bytes (even and odd bytes as two 16-bit pairs); checked against the
+// per-byte rule on every (a, b, c) byte triple.
+__device__ __forceinline__ uint32_t paeth4(uint32_t A, uint32_t B, uint32_t C) {
+    constexpr uint32_t M = 0x00FF00FFu;
+    const uint32_t e = paeth_pairs(A & M, B & M, C & M);
+    const uint32_t o = paeth_pairs((A >> 8) & M, (B >> 8) & M, (C >> 8) & M);
+    return e | (o << 8);
+}
+
 // The five PNG filter residuals of 4 row bytes: dword X of this row, B of the row above, A / C the
-// same bytes bpp to the left.  None / Sub / Up / Average in SWAR, Paeth per byte.
+// same bytes bpp to the left.  None / Sub / Up / Average in SWAR, Paeth on 16-bit pairs.
 __device__ __forceinline__ void png_residuals(uint32_t X, uint32_t A, uint32_t B, uint32_t C, uint32_t (&r)[5]) {
     r[0] = X;
     r[1] = sub8(X, A);
     r[2] = sub8(X, B);
     r[3] = sub8(X, (A & B) + (((A ^ B) & 0xFEFEFEFEu) >> 1));    // floor((a + b) / 2) per byte
-    uint32_t P = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int a = (int)byte_at(A, k), b = (int)byte_at(B, k), c = (int)byte_at(C, k);
-        const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
-        const int pr = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-        P |= (uint32_t)pr << (8 * k);
-    }
-    r[4] = sub8(X, P);
+    r[4] = sub8(X, paeth4(A, B, C));
 }
 
 // Sum over the 4 bytes of |(int8) byte| (libpng's minimum-sum heuristic): |(r ^ 0x80) - 0x80| per
@@ -592,14 +610,19 @@ __device__ __forceinline__ uint32_t eq_mask(const uint32_t (&x)[8], const uint32
     uint32_t m = 0;
     uint32_t lo = q[0];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t hi = q[i + 1];
-        const uint32_t y = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        lo = hi;
-        const uint32_t e = x[i] ^ y;                          // zero bytes: equal
-        const uint32_t z = ~(((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e | 0x7F7F7F7Fu);   // 0x80 per zero byte
-        const uint32_t nib = ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
-        m |= nib << (4 * i);
+    for (int i = 0; i < 8; i += 2) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t hi = q[i + k + 1];
+            const uint32_t y = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+            const uint32_t e = x[i + k] ^ y;                  // zero bytes: equal
+            const uint32_t z = ~(((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e | 0x7F7F7F7Fu);   // 0x80 per zero byte
+            // the four flags (bytes of 0 / 1) weighted 1, 2, 4, 8 (<< 4 for the second dword) by one dot4
+            acc = __builtin_amdgcn_udot4((z >> 7) & 0x01010101u, k ? 0x80402010u : 0x08040201u, acc, false);
+        }
+        m |= acc << (4 * i);
     }
     return m;
 }
@@ -709,10 +732,11 @@ __device__ __forceinline__ void lz_seg_tokens(const LzSeg& L, const uint8_t* s_w
     }
 }
 
+static_assert(sizeof(DeflateTabs) % 2 == 0 && alignof(DeflateTabs) == 2, "DeflateTabs copies as u16");
 __device__ __forceinline__ void lz_load_tabs(DeflateTabs& T) {
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(&c_dfl);
-    uint8_t* dst = reinterpret_cast<uint8_t*>(&T);
-    for (int i = threadIdx.x; i < (int)sizeof(DeflateTabs); i += blockDim.x) dst[i] = src[i];
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(&c_dfl);
+    uint16_t* dst = reinterpret_cast<uint16_t*>(&T);
+    for (int i = threadIdx.x; i < (int)(sizeof(DeflateTabs) / 2); i += blockDim.x) dst[i] = src[i];
 }
 
 // Parse block `blk` of one image with the tokens stored (the single-image pipeline): tokens / ntok
@@ -1470,32 +1494,33 @@ static omr_status encode_png_ws(Ctx* ctx, int kind, const uint32_t* d_argb, cons
 static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H).total; }
 
 // =====================================================================================
-// Batched PNG (round 4): N images — rendered RGB tiles of one size, or shape masks of any size —
+// Batched PNG (rounds 4-5): N images — rendered RGB tiles of one size, or shape masks of any size —
 // through one launch per stage, every grid spanning all images, and the N files packed in device
 // memory with per-image status (the batch form of the per-request ImageIO.write calls,
 // ImageRegionRequestHandler.java:597-599, and of every mask, ShapeMaskRequestHandler.java:185-203):
 //   P1 k_pngb_filter   one wave per band of image rows (wave form, RGB tiles), else one
 //                      workgroup per 4 rows (D1)
-//   P2 k_pngb_parse    one lane per 32-byte segment, 128 per workgroup (D2): the per-image symbol
-//                      histograms and a 12-byte parse trace per segment (round 5: no token buffer)
+//   P2 k_pngb_parse    one lane per 32-byte segment, 128 per workgroup (D2): candidate masks in
+//                      registers from global loads, greedy parse over the match starts, a 12-byte
+//                      parse trace per segment (no token buffer), per-block symbol counts and
+//                      the per-image histograms
 //   P3 k_pngb_tables   one workgroup per image: length-limited Huffman code + block header (D3
 //                      on the device: no host round trip; N workgroups run side by side)
 //   P3b k_pngb_block_offsets  one workgroup per image: every parse block's code bits from its
 //                      symbol counts x the code lengths, scanned into bit offsets
 //   P4 k_pngb_encode   one workgroup per 256 segments: the tokens again from the traces and the
-//                      stream bytes, each lane's code bits and in-group offset, codes assembled
-//                      in LDS, whole words stored, the group's two partial words kept aside
-//                      (round 5: replaces token stores and a bits / scan / write sequence that
-//                      moved ~4x the stream in tokens)
-//   P5 k_pngb_fixup    one lane per block: the words blocks share, ORed from the kept parts
+//                      stream bytes, each lane's codes into its LDS column, an in-group scan,
+//                      the columns shifted into the group's words, whole words stored, the
+//                      group's two partial words kept aside
+//   P5 k_pngb_fixup    one lane per group: the words groups share, ORed from the kept parts
 //   P5b k_pngb_meta    one workgroup per image: stream length, stored vs dynamic, Adler-32 from
 //                      the row partials
 //   P6 k_pngb_offsets  one workgroup: files' offsets in the output (16-byte aligned), status
 //   P8 k_pngb_emit     16 output bytes per lane: prefix chunks, IDAT header, zlib stream (deflate
 //                      words funnel-shifted, or stored blocks of the filtered stream), Adler,
 //                      IEND — aligned 16-byte stores
-//   P9 k_pngb_crc      one lane per 256-byte segment counted from the end of the CRC range:
-//                      segment CRC x x^(8*256*j) from a power table, XOR-combined per image
+//   P9 k_pngb_crc      braided CRC-32: one wave per 16 KiB strip, coalesced dword loads, the
+//                      strips combined by x^(8n) powers
 //   P10 k_pngb_finish  one lane per image: the CRC bytes
 // =====================================================================================
 constexpr int kPngbGroup = 256;                 // segments per P4/P7 group
@@ -1620,17 +1645,7 @@ __device__ __forceinline__ uint32_t png_residual(int f, uint32_t X, uint32_t A, 
     case 1: return sub8(X, A);
     case 2: return sub8(X, B);
     case 3: return sub8(X, (A & B) + (((A ^ B) & 0xFEFEFEFEu) >> 1));
-    default: {
-        uint32_t P = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int a = (int)byte_at(A, k), b = (int)byte_at(B, k), c = (int)byte_at(C, k);
-            const int pa = abs(b - c), pb = abs(a - c), pc = abs(a + b - 2 * c);
-            const int pr = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-            P |= (uint32_t)pr << (8 * k);
-        }
-        return sub8(X, P);
-    }
+    default: return sub8(X, paeth4(A, B, C));
     }
 }
 
@@ -1810,54 +1825,193 @@ __device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s
 // 16-bit counts per dword, so the common literals' atomics spread over eight addresses) and each segment's parse trace -- token
 // starts S, match starts M, the matches' candidate indices D (2 bits each, <= 10 per segment) --
 // so that P4 codes the segment without parsing it again.
-constexpr int kHistCopies = 8;                 // copies of the block histogram (lane & 7), u16 pairs
+// P2 (round 5): no LDS staging.  A lane's 32 stream bytes, the 8 before them and the 36 one row
+// up come from global memory (consecutive lanes read consecutive segments: coalesced; the row
+// above was read by a block one row back, an L2 hit), and every candidate's "byte == byte d back"
+// mask is built in registers.  The greedy parse then visits only match starts (positions where
+// some candidate's run reaches 3: there a match always starts); everything between is literals,
+// counted by a static walk over the 32 bytes.  Symbol counts go to lane-private u8 counters in
+// LDS -- [bin / 4][lane & 31]: a lane's adds hit its own bank, no conflicts; at most 4 lanes x 32
+// symbols share a counter, so u8 never wraps.
+constexpr int kHistRows = 316 / 4 + 1;          // dwords of four u8 counters per copy
+
+__device__ __forceinline__ uint32_t eq_mask_q(const uint32_t (&x)[8], const uint32_t (&q)[9], int sh) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t y = __builtin_amdgcn_alignbyte(q[i + k + 1], q[i + k], sh);
+            const uint32_t e = x[i + k] ^ y;                  // zero bytes: equal
+            const uint32_t z = ~(((e & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | e | 0x7F7F7F7Fu);   // 0x80 per zero byte
+            acc = __builtin_amdgcn_udot4((z >> 7) & 0x01010101u, k ? 0x80402010u : 0x08040201u, acc, false);
+        }
+        m |= acc << (4 * i);
+    }
+    return m;
+}
+
+// LDS-only workgroup barrier: orders the LDS traffic (the counters) without waiting for the
+// wave's outstanding global stores, which __syncthreads' workgroup fence would.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t s_win[];
-    __shared__ uint32_t lh[kHistCopies][158];              // bin b: half (b & 1) of dword b >> 1
+    __shared__ uint32_t lh[kHistRows * 32];                 // u8 counters [bin / 4][copy]
     __shared__ DeflateTabs T;
     const int i = pngb_image(B, B.pblk0, B.pblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
-    for (int k = threadIdx.x; k < kHistCopies * 158; k += kParseLanes) (&lh[0][0])[k] = 0;
-    lz_load_tabs(T);
-    int64_t wbeg, bend;
-    lz_stage(B.flt + I.flt, I.raw, blk, I.back, s_win, wbeg, bend);
-    __syncthreads();
     const int64_t s = blk * kParseLanes + threadIdx.x;
-    if (s < I.nseg) {
-        uint32_t* h = lh[threadIdx.x & (kHistCopies - 1)];
-        LzSeg L;
-        lz_seg_prepare(s_win, wbeg, s, I.raw, I.rowlen, I.bpp, I.back, L);
-        uint32_t S = 0, M = 0, D = 0;
-        int nm = 0;
-        lz_seg_tokens(L, s_win, wbeg, T, [&](uint32_t t, int p, int k) {
-            S |= 1u << p;
-            if (t & 0x80000000u) {
-                M |= 1u << p;
-                D |= (uint32_t)k << (2 * nm++);
-                const uint32_t a = 257 + (t & 31), b = 286 + ((t >> 5) & 31);
-                atomicAdd(&h[a >> 1], 1u << (16 * (a & 1)));
-                atomicAdd(&h[b >> 1], 1u << (16 * (b & 1)));
-            } else {
-                atomicAdd(&h[t >> 1], 1u << (16 * (t & 1)));
+    const bool live = s < I.nseg;
+    const uint8_t* f = B.flt + I.flt;                       // 16-byte aligned, >= 64 bytes of slack after
+    const int64_t beg = s * kSeg, rowlen = I.rowlen;
+    // every global load first (the segment, the 8 bytes before it, 36 bytes one row up), so one
+    // memory latency covers them and the table copy below
+    uint32_t x[8] = {}, p0 = 0, p1 = 0, up[9] = {};
+    const bool row_ok = live && rowlen <= I.back && beg >= rowlen;
+    if (live) {
+        const uint4* o = reinterpret_cast<const uint4*>(f + beg);
+        const uint4 u0 = o[0], u1 = o[1];
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+        if (beg >= 8) {
+            const uint2 u = *reinterpret_cast<const uint2*>(f + beg - 8);
+            p0 = u.x;
+            p1 = u.y;
+        }
+        if (row_ok) {
+            const uint32_t* ua = reinterpret_cast<const uint32_t*>(f + ((beg - rowlen) & ~(int64_t)3));
+#pragma unroll
+            for (int j = 0; j < 9; ++j) up[j] = ua[j];
+        }
+    }
+    for (int k = threadIdx.x; k < kHistRows * 32; k += kParseLanes) lh[k] = 0;
+    lz_load_tabs(T);
+    uint32_t* const hl = lh + (threadIdx.x & 31);
+    auto count = [&](uint32_t t) {                          // one symbol into this lane's counters
+        atomicAdd(hl + ((t >> 2) << 5), 1u << ((t << 3) & 31u));
+    };
+    uint32_t S = 0, M = 0, D = 0;
+    __syncthreads();
+    if (live) {
+        const int n = (int)min((int64_t)kSeg, I.raw - beg);
+        const uint32_t nmask = n >= 32 ? 0xFFFFFFFFu : (1u << n) - 1u;
+        // candidates in the compare order of the byte-wise parse: 1, bpp, 2 bpp (not for bpp 1,
+        // where bpp repeats distance 1), one row up (bpp <= 4: every candidate but the row is
+        // within 8 bytes)
+        const int nd = I.bpp == 1 ? 2 : 4;
+        const uint32_t dl[4] = {1u, I.bpp == 1 ? (uint32_t)rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
+                                (uint32_t)rowlen};
+        uint32_t m[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            m[k] = 0;
+            if (k >= nd) continue;
+            const int64_t d = dl[k];
+            if (d > I.back) continue;                       // past the single path's look-back
+            if (beg >= d) {
+                uint32_t q[9];
+                const int sh = (int)((-d) & 3);
+                if (d <= 4) {                               // one dword back: p1, then the segment
+                    q[0] = p1;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) q[j + 1] = x[j];
+                } else if (d <= 8) {                        // two dwords back
+                    q[0] = p0;
+                    q[1] = p1;
+#pragma unroll
+                    for (int j = 0; j < 7; ++j) q[j + 2] = x[j];
+                } else {                                    // one row up (d == rowlen)
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) q[j] = up[j];
+                }
+                m[k] = eq_mask_q(x, q, sh) & nmask;
+            } else if (d - beg < n) {                       // the image's first bytes
+                uint32_t mm = 0;
+                for (int q = (int)(d - beg); q < n; ++q)
+                    if (f[beg + q] == f[beg + q - d]) mm |= 1u << q;
+                m[k] = mm;
             }
-        });
+        }
+        uint32_t A = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) A |= m[k] & (m[k] >> 1) & (m[k] >> 2);
+        uint32_t cov = 0;                                   // bytes inside matches
+        int nm = 0, p = 0;
+        while (p < 32) {
+            const uint32_t ap = A >> p;
+            if (!ap) break;
+            p += __builtin_ctz(ap);                         // a match starts here
+            int best = 0, bk = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = m[k] >> p;
+                const int l = v == 0xFFFFFFFFu ? 32 : __builtin_ctz(~v);   // run of equal bytes from p
+                if (l > best) { best = l; bk = k; }
+            }
+            const uint32_t t = pack_match(T, (uint32_t)best, dl[bk]);
+            S |= 1u << p;
+            M |= 1u << p;
+            D |= (uint32_t)bk << (2 * nm++);
+            cov |= (best >= 32 ? 0xFFFFFFFFu : ((1u << best) - 1u)) << p;
+            count(257 + (t & 31));
+            count(286 + ((t >> 5) & 31));
+            p += best;
+        }
+        const uint32_t lit = nmask & ~cov;
+        S |= lit;
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+            if (lit & (1u << q)) count((x[q >> 2] >> (8 * (q & 3))) & 0xFFu);
+    }
+    lds_barrier();
+    // per-block counts: bins 4r..4r+3 summed over the 32 copies of row r (u16 pairs: <= 32 x 128);
+    // the image histogram is summed from them by k_pngb_hist (no per-block global atomics)
+    uint16_t* bh = B.bh + (size_t)blockIdx.x * 316;         // <= 4096 symbols per block: u16
+    for (int r = threadIdx.x; r < kHistRows; r += kParseLanes) {
+        uint32_t ev = 0, od = 0;
+#pragma unroll 8
+        for (int c = 0; c < 32; ++c) {
+            const uint32_t v = lh[r * 32 + ((c + r) & 31)];  // rotated start: rows spread over banks
+            ev += v & 0x00FF00FFu;
+            od += (v >> 8) & 0x00FF00FFu;
+        }
+        const uint32_t cnt[4] = {ev & 0xFFFFu, od & 0xFFFFu, ev >> 16, od >> 16};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = 4 * r + j;
+            if (k < 316) bh[k] = (uint16_t)cnt[j];
+        }
+    }
+    if (live) {
         const int64_t gs = I.seg0 + s;
         B.trace[gs] = S;
         B.trace[B.total_segs + gs] = M;
         B.trace[2 * B.total_segs + gs] = D;
     }
-    __syncthreads();
-    uint32_t* h = B.hist + (size_t)i * 316;
-    uint16_t* bh = B.bh + (size_t)blockIdx.x * 316;            // <= 4096 tokens per block: u16
-    for (int k = threadIdx.x; k < 316; k += kParseLanes) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int c = 0; c < kHistCopies; ++c) v += (lh[c][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-        bh[k] = (uint16_t)v;
-        if (v) atomicAdd(&h[k], v);
-    }
+}
+
+// P2b: the image histograms from the per-block counts: kHistParts workgroups per image, each
+// summing its share of the image's parse blocks (coalesced 632-byte rows), one atomic per bin.
+constexpr int kHistParts = 16;
+__global__ void __launch_bounds__(320) k_pngb_hist(PngBatch B) {
+    const int i = blockIdx.x / kHistParts, part = blockIdx.x % kHistParts;
+    const PngImg& I = B.img[i];
+    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
+    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
+    const int j0 = (int)((int64_t)npb * part / kHistParts), j1 = (int)((int64_t)npb * (part + 1) / kHistParts);
+    const int k = threadIdx.x;
+    if (k >= 316 || j0 >= j1) return;
+    const uint16_t* bh = B.bh + (size_t)p0 * 316 + k;
+    uint32_t v = 0;
+#pragma unroll 8
+    for (int j = j0; j < j1; ++j) v += bh[(size_t)j * 316];
+    if (v) atomicAdd(&B.hist[(size_t)i * 316 + k], v);
 }
 
 // P3b: one workgroup per image, after the code is known: each parse block's code bits are its
@@ -1905,8 +2059,8 @@ __global__ void __launch_bounds__(256) k_pngb_block_offsets(PngBatch B) {
 }
 
 // The tokens of a segment from its parse trace (P2): t as lz_seg_tokens produced them.
-template <typename Tok>
-__device__ __forceinline__ void trace_tokens(uint32_t S, uint32_t M, uint32_t D, int n, const uint8_t* seg,
+template <typename Byte, typename Tok>
+__device__ __forceinline__ void trace_tokens(uint32_t S, uint32_t M, uint32_t D, int n, Byte&& seg,
                                              const uint32_t (&dl)[4], const DeflateTabs& T, Tok&& tok) {
     while (S) {
         const int p = __builtin_ctz(S);
@@ -1916,7 +2070,7 @@ __device__ __forceinline__ void trace_tokens(uint32_t S, uint32_t M, uint32_t D,
             tok(pack_match(T, (uint32_t)(q - p), dl[D & 3u]));
             D >>= 2;
         } else {
-            tok((uint32_t)seg[p]);
+            tok(seg(p));
         }
     }
 }
@@ -1927,15 +2081,37 @@ __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
 
 // P4: one workgroup per group of kPngbGroup segments (two parse blocks): its bit range comes
 // from P3b, so groups run independently.
-constexpr int kEncWords = kPngbGroup * kSeg * 16 / 32 + 96 + 4;   // <= 16 bits per byte + header
+// LDS for 8 bits per stream byte + header; a group whose codes need more (<= 16 bits per byte:
+// high-entropy data) ORs its interior words straight into memory (the slow path).
+constexpr int kEncWords = kPngbGroup * kSeg * 8 / 32 + 96 + 4;
+constexpr int kEncScr = 8;                       // words of codes a lane keeps in LDS (256 bits)
 static_assert(kPngbGroup == 2 * kParseLanes, "P4 groups are two parse blocks");
 
+// The codes of one packed token through put(value, bits), with the code tables packed as
+// code | length << 16: a literal is one put, a match two (its extra bits ride above each code).
+template <typename Put>
+__device__ __forceinline__ void put_token_packed(uint32_t t, const uint32_t* lc, const uint32_t* dc, Put& put) {
+    if (!(t & 0x80000000u)) {
+        const uint32_t e = lc[t];
+        put(e & 0xFFFFu, (int)(e >> 16));
+        return;
+    }
+    const int ls = (int)(t & 31), ds = (int)((t >> 5) & 31);
+    const uint32_t le = lc[257 + ls], de = dc[ds];
+    const int ll = (int)(le >> 16), dn = (int)(de >> 16);
+    put((le & 0xFFFFu) | (((t >> 10) & 31u) << ll), ll + len_xbits_of(ls));          // <= 20 bits
+    put((de & 0xFFFFu) | (((t >> 15) & 0x1FFFu) << dn), dn + dist_xbits_of(ds));     // <= 28 bits
+}
+
 __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_seg[kPngbGroup * kSeg];   // the block's stream bytes
+    // the group's stream bytes, [dword][lane] (pass 1: a lane reads only its own column, each
+    // read on its own bank), then in the same LDS the group's code words (pass 2)
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kEncWords];
+    static_assert(kEncWords * 4 >= kPngbGroup * kSeg, "stream bytes fit the word buffer");
     __shared__ DeflateTabs T;
-    __shared__ uint8_t llen[286], dlen[30];
-    __shared__ uint16_t lcode[286], dcode[30];
-    __shared__ uint32_t sw[kEncWords];
+    __shared__ uint32_t lc[286], dc[30];                        // code | length << 16
+    __shared__ uint32_t scr[kEncScr * kPngbGroup];              // [word][lane]: each lane's codes from bit 0
+    __shared__ uint32_t s_end[2];                               // slow path: the group's first / last word
     __shared__ uint32_t s_wave[kPngbGroup / 64];
     const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
     const PngImg& I = B.img[i];
@@ -1950,74 +2126,147 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     const uint32_t c0 = B.poff[p0 + 2 * blk];                   // first code bit of the group
     const uint32_t b0 = blk == 0 ? 0u : c0;
     const uint32_t b1 = 2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i];
-    const uint32_t w0 = b0 >> 5, w1 = (b1 - 1) >> 5;
-    for (int k = threadIdx.x; k < 286; k += kPngbGroup) { llen[k] = Tb->llen[k]; lcode[k] = Tb->lcode[k]; }
-    if (threadIdx.x < 30) { dlen[threadIdx.x] = Tb->dlen[threadIdx.x]; dcode[threadIdx.x] = Tb->dcode[threadIdx.x]; }
-    for (uint32_t k = threadIdx.x; k <= min(w1 - w0, (uint32_t)kEncWords - 1); k += kPngbGroup) sw[k] = 0;
+    const uint32_t w0 = b0 >> 5, w1 = (b1 - 1) >> 5, nwl = w1 - w0;
+    // stored blocks win for this image (P5b decides the same from the same bits): nothing to code
+    if (2 + ((int64_t)B.img_bits[i] + 7) / 8 + 4 >= 2 + 5 * I.nblk + I.raw + 4) return;
+    uint32_t* w = B.words + I.words;
+    uint32_t* const sw = s_buf;
+    for (int k = threadIdx.x; k < 286; k += kPngbGroup) lc[k] = (uint32_t)Tb->lcode[k] | (uint32_t)Tb->llen[k] << 16;
+    if (threadIdx.x < 30) dc[threadIdx.x] = (uint32_t)Tb->dcode[threadIdx.x] | (uint32_t)Tb->dlen[threadIdx.x] << 16;
+    bool big = false;                                           // set after pass 1, workgroup-uniform
+    // local word li of the group's code run: LDS, or (slow path) its first / last word in LDS and
+    // the rest in memory.  orw for words other lanes (or groups) share; stw for a lane's own.
+    auto orw = [&](uint32_t li, uint32_t v) {
+        if (!big) atomicOr(&sw[li], v);
+        else if (li == 0) atomicOr(&s_end[0], v);
+        else if (li == nwl) atomicOr(&s_end[1], v);
+        else atomicOr(&w[w0 + li], v);
+    };
+    auto stw = [&](uint32_t li, uint32_t v) {
+        if (!big) sw[li] = v;
+        else if (li == 0 || li == nwl) orw(li, v);
+        else w[w0 + li] = v;
+    };
     lz_load_tabs(T);
-    {
-        const int64_t bbeg = blk * kPngbGroup * kSeg, bend = min(I.raw, bbeg + (int64_t)kPngbGroup * kSeg);
-        const uint8_t* src = B.flt + I.flt + bbeg;              // 16-byte aligned
-        const int64_t nbytes = bend - bbeg, n16 = nbytes / 16;
-        for (int64_t k = threadIdx.x; k < n16; k += kPngbGroup)
-            reinterpret_cast<uint4*>(s_seg)[k] = reinterpret_cast<const uint4*>(src)[k];
-        for (int64_t k = n16 * 16 + threadIdx.x; k < nbytes; k += kPngbGroup) s_seg[k] = src[k];
-    }
-    __syncthreads();
     const int64_t s = blk * kPngbGroup + threadIdx.x;
     const bool live = s < I.nseg;
-    const bool last = s == I.nseg - 1;                          // the EOB code follows its tokens
-    uint32_t S = 0, M = 0, D = 0;
-    int n = 0;
-    const uint32_t dl[4] = {1u, I.bpp == 1 ? (uint32_t)I.rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
-                            (uint32_t)I.rowlen};               // lz_seg_prepare's candidates
-    const uint8_t* seg = s_seg + kSeg * threadIdx.x;
-    uint32_t nb = 0;
-    if (live) {
+    uint32_t x[kSeg / 4] = {};                                  // the lane's 32 stream bytes
+    uint32_t S = 0, M = 0, D = 0;                               // its parse trace (P2)
+    if (live) {                                                 // (P2 left >= 64 bytes of slack past each stream)
         const int64_t gs = I.seg0 + s;
         S = B.trace[gs];
         M = B.trace[B.total_segs + gs];
         D = B.trace[2 * B.total_segs + gs];
+        const uint4* o = reinterpret_cast<const uint4*>(B.flt + I.flt + s * kSeg);
+        const uint4 u0 = o[0], u1 = o[1];
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+#pragma unroll
+        for (int k = 0; k < kSeg / 4; ++k) s_buf[k * kPngbGroup + threadIdx.x] = x[k];
+    }
+    __syncthreads();
+    const bool last = s == I.nseg - 1;                          // the EOB code follows its tokens
+    int n = 0;
+    const uint32_t dl[4] = {1u, I.bpp == 1 ? (uint32_t)I.rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
+                            (uint32_t)I.rowlen};               // lz_seg_prepare's candidates
+    auto seg_byte = [&](int p) { return (s_buf[(p >> 2) * kPngbGroup + threadIdx.x] >> (8 * (p & 3))) & 0xFFu; };
+    uint32_t nb = 0;
+    // pass 1: the lane's codes from bit 0 into its scratch column (a lane whose codes pass
+    // kEncScr words only counts them and codes again in pass 2)
+    if (live) {
         n = (int)min((int64_t)kSeg, I.raw - s * kSeg);
-        trace_tokens(S, M, D, n, seg, dl, T, [&](uint32_t t) { nb += token_bits(t, llen, dlen); });
-        if (last) nb += llen[256];
+        uint64_t acc = 0;
+        int nacc = 0;
+        uint32_t nw = 0;
+        auto put = [&](uint32_t v, int bits) {
+            acc |= (uint64_t)v << nacc;
+            nacc += bits;
+            if (nacc >= 32) {
+                if (nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)acc;
+                ++nw;
+                acc >>= 32;
+                nacc -= 32;
+            }
+        };
+        trace_tokens(S, M, D, n, seg_byte, dl, T, [&](uint32_t t) { put_token_packed(t, lc, dc, put); });
+        if (last) put(lc[256] & 0xFFFFu, (int)(lc[256] >> 16));
+        if (nacc > 0 && nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)acc;
+        nb = 32 * nw + (uint32_t)nacc;
+    }
+    // a lane whose codes passed its scratch column codes them again in pass 2, from its stream
+    // bytes kept in that column (the stream buffer becomes the word buffer; the scan's barriers
+    // order these copies before it is zeroed)
+    if (nb > 32u * kEncScr) {
+#pragma unroll
+        for (int k = 0; k < kSeg / 4; ++k) scr[k * kPngbGroup + threadIdx.x] = x[k];
     }
     uint32_t total;
     const uint32_t ex = pngb_block_excl_scan(nb, s_wave, total);
     const uint32_t hb = Tb->hdr[95];
     (void)total;                                                // == b1 - c0 (the same codes)
+    // the slow path when the group's words pass the LDS buffer (> 8 bits per stream byte)
+    big = nwl >= (uint32_t)kEncWords;
+    if (!big) {
+        for (uint32_t k = threadIdx.x; k <= nwl; k += kPngbGroup) sw[k] = 0;
+    } else {                                                    // slow path: interior words in memory
+        if (threadIdx.x < 2) s_end[threadIdx.x] = 0;
+        for (uint32_t k = w0 + 1 + threadIdx.x; k < w1; k += kPngbGroup) w[k] = 0;
+        __threadfence_block();                                  // the zeroed words before any OR
+    }
+    __syncthreads();
     if (blk == 0 && threadIdx.x == 0)
-        for (uint32_t k = 0; k < (hb + 31) / 32; ++k) atomicOr(&sw[k], Tb->hdr[k]);
-    if (live) {
+        for (uint32_t k = 0; k < (hb + 31) / 32; ++k) orw(k, Tb->hdr[k]);
+    if (live && nb) {
         const uint32_t pos = c0 + ex - 32 * w0;                 // bit position in sw
-        uint64_t acc = 0;
-        int nacc = (int)(pos & 31);
-        uint32_t wpos = pos >> 5;
-        auto put = [&](uint32_t v, int n) {                    // LSB-first into a 64-bit accumulator
-            acc |= (uint64_t)(v & ((1u << n) - 1)) << nacc;
-            nacc += n;
-            if (nacc >= 32) {
-                atomicOr(&sw[wpos], (uint32_t)acc);
-                ++wpos;
-                acc >>= 32;
-                nacc -= 32;
+        const uint32_t sh = pos & 31, wb = pos >> 5;
+        if (nb <= 32u * kEncScr) {
+            // pass 2: the scratch column shifted into place; the first and last output words
+            // are shared with the neighbouring lanes, the rest are this lane's alone
+            const uint32_t nsrc = (nb + 31) >> 5, nout = (sh + nb + 31) >> 5;
+            uint32_t prev = 0;
+            for (uint32_t k = 0; k < nout; ++k) {
+                const uint32_t v = k < nsrc ? scr[k * kPngbGroup + threadIdx.x] : 0u;
+                const uint32_t o = sh ? (v << sh) | (prev >> (32 - sh)) : v;
+                prev = v;
+                if (k == 0 || k == nout - 1) orw(wb + k, o);
+                else stw(wb + k, o);
             }
-        };
-        trace_tokens(S, M, D, n, seg, dl, T, [&](uint32_t t) { put_token(t, lcode, llen, dcode, dlen, put); });
-        if (last) put(lcode[256], llen[256]);
-        if (nacc > 0) atomicOr(&sw[wpos], (uint32_t)acc);
+        } else {                                                // long codes: code the tokens again
+            auto byte = [&](int p) { return (scr[(p >> 2) * kPngbGroup + threadIdx.x] >> (8 * (p & 3))) & 0xFFu; };
+            uint64_t acc = 0;
+            int nacc = (int)sh;
+            uint32_t wpos = wb;
+            auto put = [&](uint32_t v, int bits) {
+                acc |= (uint64_t)v << nacc;
+                nacc += bits;
+                if (nacc >= 32) {
+                    orw(wpos, (uint32_t)acc);
+                    ++wpos;
+                    acc >>= 32;
+                    nacc -= 32;
+                }
+            };
+            trace_tokens(S, M, D, n, byte, dl, T, [&](uint32_t t) { put_token_packed(t, lc, dc, put); });
+            if (last) put(lc[256] & 0xFFFFu, (int)(lc[256] >> 16));
+            if (nacc > 0) orw(wpos, (uint32_t)acc);
+        }
     }
     __syncthreads();
     // whole words inside [b0, b1) go out; the first and last (shared with the neighbouring
     // blocks) are kept for P5
-    uint32_t* w = B.words + I.words;
-    for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup)
-        if (b0 <= 32 * k && b1 >= 32 * k + 32) w[k] = sw[k - w0];
+    const uint32_t cf = big ? s_end[0] : sw[0], cl = nwl ? (big ? s_end[1] : sw[nwl]) : 0u;
+    if (!big) {
+        for (uint32_t k = w0 + threadIdx.x; k <= w1; k += kPngbGroup)
+            if (b0 <= 32 * k && b1 >= 32 * k + 32) w[k] = sw[k - w0];
+    } else if (threadIdx.x == 0) {                              // the interior is in memory already
+        if (b0 == 32 * w0) w[w0] = cf;                         // (never both ends inside one word here)
+        if (b1 == 32 * w1 + 32) w[w1] = cl;
+    }
     if (threadIdx.x == 0) {
         B.blk_b0[g] = b0;
         B.blk_b1[g] = b1;
-        B.blk_cf[g] = sw[0];
-        B.blk_cl[g] = w1 != w0 ? sw[w1 - w0] : 0u;
+        B.blk_cf[g] = cf;
+        B.blk_cl[g] = cl;
     }
 }
 
@@ -2030,6 +2279,7 @@ __global__ void __launch_bounds__(256) k_pngb_fixup(PngBatch B) {
     const int i = pngb_image(B, B.grp0, B.grp_per, g);
     const PngImg& I = B.img[i];
     const int64_t gend = (B.uniform ? (int64_t)i * B.grp_per : I.grp0) + (I.nseg + kPngbGroup - 1) / kPngbGroup;
+    if (2 + ((int64_t)B.img_bits[i] + 7) / 8 + 4 >= 2 + 5 * I.nblk + I.raw + 4) return;   // stored: P4 skipped
     const uint32_t b0 = B.blk_b0[g], b1 = B.blk_b1[g], w0 = b0 >> 5, w1 = (b1 - 1) >> 5;
     if ((b1 & 31) == 0 || !(w1 > w0 || (b0 & 31) == 0)) return;
     uint32_t v = w1 == w0 ? B.blk_cf[g] : B.blk_cl[g];
@@ -2421,14 +2671,13 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         L.flt += (int64_t)align_up((size_t)P.raw, 16);
         L.words += (int64_t)align_up((size_t)(P.raw / 2 + 128), 4);     // <= 16 bits per byte + header
         L.rows_lds = std::max(L.rows_lds, align_up((size_t)png_filter_lds(P.rowlen - 1) + 16, 16));
-        L.parse_lds = std::max(L.parse_lds, (size_t)d.back + (size_t)kParseLanes * kSeg);
         if (i && (h.kind != im[0].kind || h.W != im[0].W || h.H != im[0].H)) L.uniform = false;
     }
     size_t o = 0;
     auto take = [&](size_t b) { const size_t r = o; o = align_up(o + b, 256); return r; };
     L.o_img = take(sizeof(PngImg) * n);
     L.o_first = take(sizeof(int32_t) * 5 * n);
-    L.o_flt = take((size_t)L.flt);
+    L.o_flt = take((size_t)L.flt + 64);              // P2 reads up to 48 bytes past an image's stream
     L.o_bh = take((size_t)L.pblk * 316 * 2);
     L.o_poff = take((size_t)L.pblk * 4 + (size_t)n * 4);
     L.o_blk = take((size_t)L.grp * 16);
@@ -2540,6 +2789,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     {
         KernelTimer t(ctx, 21);
         hipLaunchKernelGGL(k_pngb_parse, dim3((unsigned)pblk), dim3(kParseLanes), parse_lds, s, Bt);
+        hipLaunchKernelGGL(k_pngb_hist, dim3((unsigned)(n * kHistParts)), dim3(320), 0, s, Bt);
     }
     {
         KernelTimer t(ctx, 22);

@@ -306,3 +306,46 @@ def test_single_request_paths_batched_and_legacy(monkeypatch):
         np.testing.assert_array_equal(np.asarray(decode(outs["1"][k]).convert("RGBA")),
                                       np.asarray(decode(outs["0"][k]).convert("RGBA")))
     np.testing.assert_array_equal(np.asarray(decode(outs["1"][0])), rgb_of(argb))
+
+
+def test_png_batch_high_entropy_groups_in_a_dynamic_stream(ctx):
+    """A compressible image with a band of noise: the dynamic stream wins overall, while the noise
+    groups need more than 8 bits per byte -- P4's slow path (interior words ORed in memory).  The
+    files decode to the pixels, their IDAT is dynamic, and a stored-winning image (all noise)
+    skips P4 entirely."""
+    rng = np.random.default_rng(77)
+    w, h = 1024, 96
+    a = np.full((h, w), 0xFF204060, np.uint32)
+    a[40:56] = rng.integers(0, 2**32, (16, w), dtype=np.uint64).astype(np.uint32) | 0xFF000000
+    noise = rng.integers(0, 2**32, (h, w), dtype=np.uint64).astype(np.uint32)
+    argb = np.stack([a, noise, a])
+    res = encode_batch(ctx, argb)
+    for i, (st, off, png) in enumerate(res):
+        assert st == 0
+        chunks(png)
+        np.testing.assert_array_equal(np.asarray(decode(png)), rgb_of(argb[i]))
+    assert not idat_is_stored(res[0][2]) and idat_is_stored(res[1][2])
+    assert res[0][2] == res[2][2]
+
+
+def test_png_batch_sparse_noisy_segments(ctx):
+    """A flat image with a short run of noisy pixels in every row: the stream as a whole codes far
+    below 8 bits per byte, but the noisy segments' literals take long codes (> 256 bits per
+    32-byte segment), so P4 codes those lanes again from their stashed bytes inside an LDS-staged
+    group.  Files decode to the pixels and match the single-request path."""
+    rng = np.random.default_rng(11)
+    w, h = 1024, 64
+    a = np.full((h, w), 0xFF204060, np.uint32)
+    for y in range(h):
+        x0 = int(rng.integers(0, w - 16))
+        a[y, x0:x0 + 11] = rng.integers(0, 2**32, 11, dtype=np.uint64).astype(np.uint32) | 0xFF000000
+    b = a.copy()
+    b[::7] = 0xFF000000 | (np.arange(w, dtype=np.uint32) * 2654435761 % 2**24)
+    argb = np.stack([a, b])
+    res = encode_batch(ctx, argb)
+    for i, (st, off, png) in enumerate(res):
+        assert st == 0
+        chunks(png)
+        assert not idat_is_stored(png)
+        np.testing.assert_array_equal(np.asarray(decode(png)), rgb_of(argb[i]))
+        assert png == ctx.encode_png(argb[i], w, h)

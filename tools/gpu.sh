@@ -110,6 +110,7 @@ for step in "$@"; do
                 || { echo "sq $arg pass $i failed"; tail -10 $O/sq_${arg}_$i.err; exit 1; }
         done
         python3 tools/pmc_kernels.py $(find $O/sq_$arg -name '*counter_collection.csv') > $O/sq_$arg.txt || exit 1
+        python3 tools/sq_json.py $O/sq_$arg.txt $O/sq_$arg.json $TAG > /dev/null || exit 1
         find $O/sq_$arg -name '*counter_collection.csv' -delete
         grep -E "==|VALU/wave|WAIT|BANK|IDX" $O/sq_$arg.txt | head -40 ;;
     py)
