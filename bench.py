@@ -862,6 +862,7 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
     el = time.perf_counter() - t0
     res = {"requests": n_req, "clients": clients,
            "one_at_a_time": {"tiles_per_s": round(64 / el, 1), "p50_ms": round(1e3 * float(np.median(lat)), 3)}}
+    res["interactive"] = serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, res["one_at_a_time"])
     legs = [("batcher_max64_wait1000us", lambda: Batcher(ctx.device, max_batch=64, max_wait_us=1000))]
     if pool_devices:
         # omr_pool: one batcher per entry of pool_devices (the node's GPUs; on a one-GPU box the
@@ -903,6 +904,62 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
         leg["dedup_share"] = round(leg["dedup"] / max(1, leg["rendered"] + leg["dedup"]), 3)
         res[name] = {"tiles_per_s": round(n_req / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3), **leg}
     return res
+
+
+def serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, single, per_client=8):
+    """The same tiles with ONE request in flight per client (a viewer asking for the next tile only
+    when the last has arrived): `clients` threads each on its own context rendering its requests
+    directly (the reference's shape: every worker renders its own request) against the batcher
+    taking them all.  With k requests outstanding a request waits behind the others' PCIe
+    transfers (8 MiB per tile in), so p50 grows with k whatever the dispatch; the leg reports both
+    p50s beside the one-at-a-time p50 of a single client."""
+    import threading
+    import numpy as np
+    import omr
+    from omr import Batcher
+    out = {"clients": clients, "requests_per_client": per_client, "in_flight_per_client": 1}
+    ctxs = [omr.Context(ctx.device, torch_order=False) for _ in range(clients)]
+    devs = [torch.empty((TILE, TILE), dtype=torch.int32, device="cuda") for _ in range(clients)]
+    torch.cuda.synchronize()
+
+    def run(job):
+        lats = []
+
+        def client(k):
+            mine = [reqs[(k + clients * j) % len(reqs)] for j in range(per_client)]
+            for r in mine:
+                a = time.perf_counter()
+                job(k, r)
+                lats.append(time.perf_counter() - a)
+        for warm in (True, False):
+            lats.clear()
+            ths = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
+            t0 = time.perf_counter()
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            el = time.perf_counter() - t0
+        return {"tiles_per_s": round(clients * per_client / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3),
+                "p90_ms": round(1e3 * float(np.percentile(lats, 90)), 3)}
+
+    def direct(k, r):
+        ctxs[k].render_pixel_buffer_tiles(qd, chans, pb, [r], TILE, TILE, out=devs[k], bindings=binds)
+        ctxs[k].encode_jpeg_device(devs[k], TILE, TILE, 0.9)
+    try:
+        out["independent_contexts"] = run(direct)
+        with Batcher(ctx.device, max_batch=64, max_wait_us=1000) as b:
+            out["batcher_max64_wait1000us"] = run(
+                lambda k, r: b.wait(b.submit(pb, qd, chans, *r, TILE, TILE, quality=0.9, bindings=binds)))
+            st = b.stats()
+            out["batcher_max64_wait1000us"].update({"rounds": st["batches"], "rendered": st["rendered"],
+                                                    "dedup": st["dedup"]})
+    finally:
+        for c in ctxs:
+            c.close()
+    for k in ("independent_contexts", "batcher_max64_wait1000us"):
+        out[k]["p50_vs_single_client"] = round(out[k]["p50_ms"] / single["p50_ms"], 2)
+    return out
 
 
 def _serve(b, submit_fns, clients):
