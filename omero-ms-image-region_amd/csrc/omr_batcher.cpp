@@ -57,6 +57,8 @@ struct omr_batcher {
     int max_batch = 64;
     int max_wait_us = 500;
     int gap_us = 200;                        // arrival pause that closes a gather (<= max_wait_us)
+    int last_round = 0;                      // jobs the previous round took
+    std::chrono::steady_clock::time_point t_round_end{};
     std::chrono::steady_clock::time_point t_last_submit{};
     omr_ctx* ctx = nullptr;
     std::thread th;
@@ -454,9 +456,16 @@ static void dispatch_loop(omr_batcher* B) {
         // gather: up to max_batch jobs, what arrives within max_wait_us of the oldest one, or --
         // whichever comes first -- until the arrivals pause for gap_us.  The device is idle while
         // the dispatcher gathers, so a burst (a viewer's screenful, the clients answered by the last
-        // round) is taken as soon as it has landed instead of after the whole max_wait_us.
+        // round) is taken as soon as it has landed instead of after the whole max_wait_us.  Right
+        // after a round, as many jobs as it took also close the gather: clients that wait for their
+        // answer before asking again come back together, and their round goes as soon as they are
+        // all in.  After an idle spell (longer than max_wait_us) only the arrival pause counts, so
+        // a fresh burst is still gathered whole (and its duplicates rendered once).
+        const bool follow = B->last_round > 0 &&
+                            B->pending.front()->t_submit - B->t_round_end < std::chrono::microseconds(B->max_wait_us);
         for (;;) {
             if (B->stop || (int)B->pending.size() >= B->max_batch) break;
+            if (follow && (int)B->pending.size() >= B->last_round) break;
             const auto now = std::chrono::steady_clock::now();
             const auto deadline =
                 std::min(B->pending.front()->t_submit + std::chrono::microseconds(B->max_wait_us),
@@ -466,6 +475,7 @@ static void dispatch_loop(omr_batcher* B) {
         }
         std::vector<std::unique_ptr<Job>> take;
         const size_t nt = std::min(B->pending.size(), (size_t)B->max_batch);
+        B->last_round = (int)nt;
         for (size_t i = 0; i < nt; ++i) take.push_back(std::move(B->pending[i]));
         B->pending.erase(B->pending.begin(), B->pending.begin() + nt);
         lk.unlock();
@@ -548,6 +558,7 @@ static void dispatch_loop(omr_batcher* B) {
         for (auto& r : results) B->done[r.first] = std::move(r.second);
         B->outstanding -= (int64_t)results.size();
         B->n_batches += 1;
+        B->t_round_end = std::chrono::steady_clock::now();
         B->n_rendered += rendered;
         B->n_dedup += dedup;
         B->cv_out.notify_all();
@@ -764,9 +775,32 @@ static int pool_pick(omr_pool* P) {
     return best;
 }
 
+// Route by the request's cache identity (ImageRegionCtx.java:165-177: image, plane, region; the
+// settings travel with it): identical requests in flight together land on the same batcher, so the
+// pool deduplicates them as one batcher does, instead of each batcher rendering its own copy.  A
+// home batcher more than `slack` jobs behind the least-queued one is bypassed (load balance wins
+// over dedup for a hot key).
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 0x100000001B3ull;
+    return h;
+}
+static int pool_pick_keyed(omr_pool* P, uint64_t h, int64_t slack) {
+    const int n = (int)P->b.size();
+    const int home = (int)((h >> 17) % (uint64_t)n);
+    const int least = pool_pick(P);
+    const int64_t qh = P->b[home]->outstanding.load(std::memory_order_relaxed);
+    const int64_t ql = P->b[least]->outstanding.load(std::memory_order_relaxed);
+    return qh <= ql + slack ? home : least;
+}
+
 omr_status omr_pool_submit(omr_pool* P, const omr_tile_job* job, uint64_t* ticket) {
-    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
-    const int best = pool_pick(P);
+    if (!P || !ticket || !job) return OMR_INVALID_ARGUMENT;
+    uint64_t h = 0xCBF29CE484222325ull;
+    h = fnv1a(h, &job->pb, sizeof(job->pb));
+    const int32_t id[7] = {job->z, job->t, job->x, job->y, job->width, job->height, job->has_projection};
+    h = fnv1a(h, id, sizeof(id));
+    const int best = pool_pick_keyed(P, h, P->b[0]->max_batch / 2);
     uint64_t t = 0;
     const omr_status st = omr_batcher_submit(P->b[best], job, &t);
     if (st) return st;
@@ -775,8 +809,13 @@ omr_status omr_pool_submit(omr_pool* P, const omr_tile_job* job, uint64_t* ticke
 }
 
 omr_status omr_pool_submit_mask(omr_pool* P, const omr_mask_job* job, uint64_t* ticket) {
-    if (!P || !ticket) return OMR_INVALID_ARGUMENT;
-    const int best = pool_pick(P);
+    if (!P || !ticket || !job) return OMR_INVALID_ARGUMENT;
+    uint64_t h = 0xCBF29CE484222325ull;
+    const int32_t id[4] = {job->width, job->height, job->flip_h, job->flip_v};
+    h = fnv1a(h, id, sizeof(id));
+    h = fnv1a(h, job->rgba, 4);
+    if (job->bits) h = fnv1a(h, job->bits, std::min<size_t>(job->n_bytes, 256));
+    const int best = pool_pick_keyed(P, h, P->b[0]->max_batch / 2);
     uint64_t t = 0;
     const omr_status st = omr_batcher_submit_mask(P->b[best], job, &t);
     if (st) return st;

@@ -124,17 +124,25 @@ static hipEvent_t pooled_event(Ctx* c) {
     return e;
 }
 
-KernelTimer::KernelTimer(Ctx* ctx, int k) : c(ctx), kind(k) {
+thread_local KernelTimer* tl_ext_timer = nullptr;
+
+KernelTimer::KernelTimer(Ctx* ctx, int k, bool ext_launch) : c(ctx), kind(k) {
     if (!c->timing) return;
-    hipEvent_t start = pooled_event(c);
+    start = pooled_event(c);
     stop = pooled_event(c);
     if (!start || !stop) { stop = nullptr; return; }
-    (void)hipEventRecord(start, c->stream);
+    (void)hipEventRecord(start, c->stream);     // re-stamped by an ext launch
     c->timed.push_back({start, stop, kind});
+    if (ext_launch) {
+        ext = true;
+        prev = tl_ext_timer;
+        tl_ext_timer = this;
+    }
 }
 
 KernelTimer::~KernelTimer() {
-    if (stop) (void)hipEventRecord(stop, c->stream);
+    if (ext) tl_ext_timer = prev;
+    if (stop && !used) (void)hipEventRecord(stop, c->stream);
 }
 
 }  // namespace omr

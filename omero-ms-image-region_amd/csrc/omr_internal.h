@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -146,10 +147,28 @@ struct Ctx {
 struct KernelTimer {
     Ctx* c;
     int kind;
-    hipEvent_t stop = nullptr;
-    KernelTimer(Ctx* ctx, int k);
+    hipEvent_t start = nullptr, stop = nullptr;
+    bool ext = false, used = false;             // ext: the next omr_launch stamps the events itself
+    KernelTimer* prev = nullptr;
+    // ext = true for a scope holding one kernel launched through omr_launch: the events are then
+    // the dispatch's own start / end timestamps (hipExtLaunchKernel), the duration a rocprofv3
+    // kernel trace reports, instead of two queue packets around it (which read ~1 us high on a
+    // 16 us kernel)
+    KernelTimer(Ctx* ctx, int k, bool ext_launch = false);
     ~KernelTimer();
 };
+extern thread_local KernelTimer* tl_ext_timer;
+
+template <typename F, typename... Args>
+inline void omr_launch(F kernel, const dim3& g, const dim3& b, uint32_t lds, hipStream_t s, Args... args) {
+    KernelTimer* t = tl_ext_timer;
+    if (t && !t->used && t->stop) {
+        t->used = true;
+        hipExtLaunchKernelGGL(kernel, g, b, lds, s, t->start, t->stop, 0u, args...);
+    } else {
+        hipLaunchKernelGGL(kernel, g, b, lds, s, args...);
+    }
+}
 
 omr_status fail(Ctx* c, omr_status s, const std::string& msg);
 omr_status hip_fail(Ctx* c, hipError_t e, const char* what);

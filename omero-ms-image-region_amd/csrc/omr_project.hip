@@ -542,17 +542,17 @@ static hipError_t launch_project_v(const K3Args& a, int alg, uint32_t n_iter, bo
     const dim3 gs((chunks16 + 63) / 64, n), g1((chunks16 + kBlock - 1) / kBlock, n);
     switch (alg) {
     case OMR_PROJECTION_MAX:
-        hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MAX, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_MAX, true>), gs, dim3(kBlock), 0, s, a, n_iter);
         break;
     case OMR_PROJECTION_MEAN:
-        if (split && narrow_ok<T>(n_iter)) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
-        else if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true>), gs, dim3(kBlock), 0, s, a, n_iter);
-        else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, false>), g1, dim3(kBlock), 0, s, a, n_iter);
+        if (split && narrow_ok<T>(n_iter)) omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else if (split) omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_MEAN, false>), g1, dim3(kBlock), 0, s, a, n_iter);
         break;
     default:
-        if (split && narrow_ok<T>(n_iter)) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
-        else if (split) hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true>), gs, dim3(kBlock), 0, s, a, n_iter);
-        else hipLaunchKernelGGL((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, false>), g1, dim3(kBlock), 0, s, a, n_iter);
+        if (split && narrow_ok<T>(n_iter)) omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else if (split) omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, true>), gs, dim3(kBlock), 0, s, a, n_iter);
+        else omr_launch((k_project_v<T, BEI, BEO, OMR_PROJECTION_SUM, false>), g1, dim3(kBlock), 0, s, a, n_iter);
         break;
     }
     return hipGetLastError();
@@ -626,7 +626,7 @@ omr_status enqueue_projection(Ctx* ctx, const void* const* d_stacks, void* const
     const dim3 grid((unsigned)bx, (unsigned)n);
     const bool bi = be_in != 0, bo = be_out != 0;
     hipError_t e;
-    KernelTimer timer(ctx, 3);
+    KernelTimer timer(ctx, 3, true);       // the vector path's one launch stamps its own events
     // Vector path: every stack and output 16-B aligned, planes a whole number of 16-B chunks.
     bool vec = (a.plane * bpp) % 16 == 0;
     for (int i = 0; i < n && vec; ++i)

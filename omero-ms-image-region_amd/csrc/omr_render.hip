@@ -232,21 +232,31 @@ constexpr int kBucketsLog2 = OMR_K2_BUCKETS_LOG2, kBuckets = 1 << kBucketsLog2;
 constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 2u * kBuckets));
 
 // Bucket map of a channel with thresholds T[1] = t1 .. T[cmax] = k1: the smallest shift with
-// (k1 - t1) >> shift <= kBuckets - 2, origin = t1 - 2^shift (0 when t1 < 2^shift), hi = the last
-// key of bucket kBuckets - 1 (saturated at 2^32 - 1).
+// (k1 - t1) >> shift <= kBuckets - 3, origin = t1 - 2^shift rounded down to a multiple of 2^shift
+// (0 when t1 < 2^shift) -- so a key's bucket is (key >> shift) - (origin >> shift) and K2 folds
+// the second term into its table address -- and hi = the last key of bucket kBuckets - 1
+// (saturated at 2^32 - 1).  T[1] lands in bucket 1 (bucket 0 holds no threshold), T[cmax] at most
+// in bucket (span >> shift) + 2.
 struct BucketMap { uint32_t org, hi, sh, pad; };
 __device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1) {
     const uint32_t span = k1 - t1;
     const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
     uint32_t sh = bits > (uint32_t)kBucketsLog2 ? bits - kBucketsLog2 : 0u;
-    if ((span >> sh) > (uint32_t)kBuckets - 2u) ++sh;
+    while ((span >> sh) > (uint32_t)kBuckets - 3u) ++sh;
     BucketMap m;
     m.sh = sh;
-    m.org = t1 >= (1u << sh) ? t1 - (1u << sh) : 0u;
+    const uint64_t step = 1ull << sh;
+    m.org = t1 >= step ? (uint32_t)((t1 - step) & ~(step - 1)) : 0u;
     const uint64_t end = (uint64_t)m.org + ((uint64_t)kBuckets << sh) - 1u;
     m.hi = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end;
     m.pad = 0;
     return m;
+}
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t x, uint32_t lo, uint32_t hi) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
 }
 
 // #{c in 1..255 : T[c] <= key} over the sorted thresholds.
@@ -346,21 +356,30 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
                 const uint32_t cnan = (T[0] >> 8) & 0xFFu;
                 const BucketMap& M = reinterpret_cast<const BucketMap*>(s_bkt + na * kBuckets)[a];
                 const uint32_t org = M.org, hi = M.hi, sh = M.sh;
+                const uint16_t* const Bk0 = Bk - (org >> sh);           // org is a multiple of 2^sh
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {
                     uint32_t raw = c.dw[j];
                     if constexpr (BE) raw = bswap32(raw);
-                    const uint32_t key = raw_key<PT>(raw);
-                    const uint32_t e = Bk[(min(max(key, org), hi) - org) >> sh];
+                    uint32_t key;
+                    if constexpr (PT == OMR_PIXELS_FLOAT) key = raw ^ ((uint32_t)((int32_t)raw >> 31) | 0x80000000u);
+                    else key = raw_key<PT>(raw);
+                    const uint32_t e = Bk0[med3_u32(key, org, hi) >> sh];
                     uint32_t base = e & 0xFFu;
                     uint32_t len = e >> 8;
-                    while (len > 0) {
-                        const uint32_t half = len >> 1;
-                        const bool le = T[base + half + 1] <= key;
+                    if (len > 0) {                  // the first step unrolled: usually the only one
+                        uint32_t half = len >> 1;
+                        bool le = T[base + half + 1] <= key;
                         base = le ? base + half + 1 : base;
                         len = le ? len - half - 1 : half;
+                        while (len > 0) {
+                            half = len >> 1;
+                            le = T[base + half + 1] <= key;
+                            base = le ? base + half + 1 : base;
+                            len = le ? len - half - 1 : half;
+                        }
                     }
-                    if constexpr (PT == OMR_PIXELS_FLOAT) base = ((raw & 0x7FFFFFFFu) > 0x7F800000u) ? cnan : base;
+                    if constexpr (PT == OMR_PIXELS_FLOAT) base = __builtin_isnan(__uint_as_float(raw)) ? cnan : base;
                     acc[j] += tab[base];
                     if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
                 }
