@@ -188,7 +188,7 @@ omr_status omr_ctx_create(int32_t device_ordinal, omr_ctx** out) {
     if (const char* v = std::getenv("OMR_JPEG_EST_CENTIBPP")) c->jpeg_est_centibpp = std::max(5, std::atoi(v));
     if (const char* v = std::getenv("OMR_K2_EVAL_CPT")) {   // 2 / 4 plain grid stride, -1 / -2 pipelined
         const int k = std::atoi(v);
-        c->k2_eval_cpt = (k == 4 || k == 2 || k == -1) ? k : -2;
+        c->k2_eval_cpt = (k == 4 || k == 2 || k == -1 || k == -3) ? k : -2;
     }
     *out = c;
     return OMR_OK;

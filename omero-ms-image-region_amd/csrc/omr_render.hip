@@ -82,7 +82,8 @@ struct K2Args {
     const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
     const uint32_t* thresh;     // [n_active][256] kModeThresh code thresholds (K1)
-    const uint16_t* buckets;    // [n_active][kBuckets] kModeThresh key buckets (K1)
+    const uint32_t* buckets;    // [n_active][1 << bk_log2] kModeThresh key buckets (K1)
+    int32_t bk_log2;            // buckets per channel (log2): k2_buckets_log2(n_active)
     int32_t use_thresh;         // some channel is kModeThresh: stage thresh + buckets in LDS too
     uint32_t n_work;            // work blocks of 256*CPT chunks (grid-stride in eval mode)
     uint32_t* out;              // [n_tiles][H][W]
@@ -227,9 +228,22 @@ template <int PT> __device__ __forceinline__ uint32_t raw_key(uint32_t raw) {
 #define OMR_K2_BUCKETS_LOG2 11
 #endif
 constexpr int kBucketsLog2 = OMR_K2_BUCKETS_LOG2, kBuckets = 1 << kBucketsLog2;
-// channels whose threshold + bucket tables fit K2's 48 KiB LDS budget (8 at 2048 buckets; the
-// 16-byte bucket maps ride on top)
-constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 2u * kBuckets));
+// Buckets per channel: kBuckets u32 entries (8 KiB) for up to 4 threshold channels, half as many
+// above, so 8 channels' threshold + bucket tables still fit K2's 48 KiB (the 16-byte bucket maps
+// ride on top).
+__host__ __device__ constexpr int k2_buckets_log2(int na) { return na <= 4 ? kBucketsLog2 : kBucketsLog2 - 1; }
+__host__ __device__ constexpr int k2_buckets(int na) { return 1 << k2_buckets_log2(na); }
+// the launch's bucket count (log2): k2_buckets_log2, or OMR_K2_BUCKETS_LG (9..11) for measurement
+static inline int k2_launch_buckets_log2(int na) {
+    static const int env = [] {
+        const char* e = std::getenv("OMR_K2_BUCKETS_LG");
+        const int v = e ? std::atoi(e) : 0;
+        return v >= 9 && v <= kBucketsLog2 ? v : 0;
+    }();
+    if (env && (size_t)na * (2048 + (4u << env) + 16) <= 64 * 1024) return env;
+    return k2_buckets_log2(na);
+}
+constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 4u * (kBuckets / 2)));
 
 // Bucket map of a channel with thresholds T[1] = t1 .. T[cmax] = k1: the smallest shift with
 // (k1 - t1) >> shift <= kBuckets - 3, origin = t1 - 2^shift rounded down to a multiple of 2^shift
@@ -238,16 +252,17 @@ constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 2u * kBu
 // (saturated at 2^32 - 1).  T[1] lands in bucket 1 (bucket 0 holds no threshold), T[cmax] at most
 // in bucket (span >> shift) + 2.
 struct BucketMap { uint32_t org, hi, sh, pad; };
-__device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1) {
+__device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1, int lg) {
     const uint32_t span = k1 - t1;
     const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
-    uint32_t sh = bits > (uint32_t)kBucketsLog2 ? bits - kBucketsLog2 : 0u;
-    while ((span >> sh) > (uint32_t)kBuckets - 3u) ++sh;
+    const uint32_t nbk = 1u << lg;
+    uint32_t sh = bits > (uint32_t)lg ? bits - lg : 0u;
+    while ((span >> sh) > nbk - 3u) ++sh;                 // sh <= 23 (span < 2^32, lg >= 10)
     BucketMap m;
     m.sh = sh;
     const uint64_t step = 1ull << sh;
     m.org = t1 >= step ? (uint32_t)((t1 - step) & ~(step - 1)) : 0u;
-    const uint64_t end = (uint64_t)m.org + ((uint64_t)kBuckets << sh) - 1u;
+    const uint64_t end = (uint64_t)m.org + ((uint64_t)nbk << sh) - 1u;
     m.hi = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end;
     m.pad = 0;
     return m;
@@ -267,27 +282,35 @@ __device__ __forceinline__ uint32_t thresh_count(const uint32_t* __restrict__ T,
     return pos;
 }
 
-// grid: (kBuckets/256, n_active) x 256 threads; the maps follow the n_active bucket tables.
+// grid: (buckets / 256, n_active) x 256 threads; the maps follow the n_active bucket tables.
+// Entry of bucket [ks, ke]: lo = #T <= ks in bits 0-7, and in bits 8-31 the offset t - ks of its
+// one threshold t when it holds exactly one (1 .. 2^23 - 1: T[c] > ks, sh <= 23), 0xFFFFFF when
+// it holds none, 0x800000 | n when it holds n >= 2 (both above every in-bucket offset).  K2 then
+// quantizes a key of the bucket as lo + ((key - ks) >= offset) -- one table read, no threshold
+// read -- and only keys in a bucket of two or more thresholds search its n thresholds.
 __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restrict__ plan,
                                                        const uint32_t* __restrict__ thr,
-                                                       uint16_t* __restrict__ bkt) {
+                                                       uint32_t* __restrict__ bkt, int lg) {
     const int a = blockIdx.y;
     if (plan->ch[a].mode != kModeThresh) return;
+    const int nbk = 1 << lg;
     const uint32_t* T = thr + a * 256;
     const uint32_t cmax = T[0] & 0xFFu;
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     const uint32_t k1 = cmax ? T[cmax] : 0u;
-    const BucketMap m = bucket_map(cmax ? T[1] : 0u, k1);
-    if (b == 0) reinterpret_cast<BucketMap*>(bkt + gridDim.y * kBuckets)[a] = m;
-    uint16_t e = 0;
+    const BucketMap m = bucket_map(cmax ? T[1] : 0u, k1, lg);
+    if (b == 0) reinterpret_cast<BucketMap*>(bkt + gridDim.y * nbk)[a] = m;
+    uint32_t e = 0xFFFFFF00u;
     if (cmax) {
         const uint64_t ks = (uint64_t)m.org + ((uint64_t)b << m.sh);
         const uint64_t ke = ks + (1ull << m.sh) - 1;
         const uint32_t lo = thresh_count(T, (uint32_t)std::min<uint64_t>(ks, k1));
         const uint32_t hi = thresh_count(T, (uint32_t)std::min<uint64_t>(ke, k1));
-        e = (uint16_t)(lo | ((hi - lo) << 8));
+        const uint32_t n = hi - lo;
+        const uint32_t off = n == 0 ? 0xFFFFFFu : n == 1 ? T[lo + 1] - (uint32_t)ks : 0x800000u | n;
+        e = lo | (off << 8);
     }
-    bkt[a * kBuckets + b] = e;
+    bkt[a * nbk + b] = e;
 }
 
 #ifndef OMR_K2_CPT
@@ -296,24 +319,24 @@ __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restr
 constexpr int kCPT = OMR_K2_CPT;   // chunks per thread of the fixed-channel-count kernels
 
 // LDS of one K2 block: contrib [na][256] u32, then (kModeThresh) thresholds [na][256] u32 and
-// buckets [na][kBuckets] u16.
-__host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh) {
-    return (size_t)na * (1024 + (thresh ? 1024 + 2 * kBuckets + sizeof(BucketMap) : 0));
+// buckets [na][k2_buckets(na)] u32 + their maps.
+__host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh, int lg) {
+    return (size_t)na * (1024 + (thresh ? 1024 + 4 * (1 << lg) + sizeof(BucketMap) : 0));
 }
 
 template <int MODE, int BPP>
 __device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_contrib, int na) {
     // one 16-byte load per lane for up to 4 channels of contrib; the threshold tables follow
-    for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
+    for (int i = threadIdx.x * 4; i < na * 256; i += blockDim.x * 4)
         *reinterpret_cast<uint4*>(s_contrib + i) = *reinterpret_cast<const uint4*>(A.contrib + i);
     if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
         if (A.use_thresh) {
             uint32_t* s_thr = s_contrib + na * 256;
-            for (int i = threadIdx.x * 4; i < na * 256; i += kBlock * 4)
+            for (int i = threadIdx.x * 4; i < na * 256; i += blockDim.x * 4)
                 *reinterpret_cast<uint4*>(s_thr + i) = *reinterpret_cast<const uint4*>(A.thresh + i);
             uint32_t* s_b = s_thr + na * 256;
             const uint32_t* g_b = reinterpret_cast<const uint32_t*>(A.buckets);
-            for (int i = threadIdx.x * 4; i < na * (kBuckets / 2 + 4); i += kBlock * 4)   // + the maps
+            for (int i = threadIdx.x * 4; i < na * ((1 << A.bk_log2) + 4); i += blockDim.x * 4)   // + the maps
                 *reinterpret_cast<uint4*>(s_b + i) = *reinterpret_cast<const uint4*>(g_b + i);
         }
     }
@@ -333,7 +356,8 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
         return static_cast<const uint8_t*>(A.planes[(int64_t)t * A.size_c + A.ch[a].index]);
     };
     const uint32_t* const s_thr = s_contrib + na * 256;
-    const uint16_t* const s_bkt = reinterpret_cast<const uint16_t*>(s_thr + na * 256);
+    const uint32_t* const s_bkt = s_thr + na * 256;
+    const int nbk = 1 << A.bk_log2;
     const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
     uint32_t acc[VEC];
 #pragma unroll
@@ -352,11 +376,11 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
         if constexpr ((MODE == kK2Eval || MODE == kK2Thresh) && BPP == 4) {
             if (MODE == kK2Thresh || p.mode == kModeThresh) {          // uniform: bucket, then the few thresholds in it
                 const uint32_t* T = s_thr + a * 256;
-                const uint16_t* Bk = s_bkt + a * kBuckets;
+                const uint32_t* Bk = s_bkt + a * nbk;
                 const uint32_t cnan = (T[0] >> 8) & 0xFFu;
-                const BucketMap& M = reinterpret_cast<const BucketMap*>(s_bkt + na * kBuckets)[a];
-                const uint32_t org = M.org, hi = M.hi, sh = M.sh;
-                const uint16_t* const Bk0 = Bk - (org >> sh);           // org is a multiple of 2^sh
+                const BucketMap& M = reinterpret_cast<const BucketMap*>(s_bkt + na * nbk)[a];
+                const uint32_t org = M.org, hi = M.hi, sh = M.sh, inb = (1u << sh) - 1u;
+                const uint32_t* const Bk0 = Bk - (org >> sh);           // org is a multiple of 2^sh
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {
                     uint32_t raw = c.dw[j];
@@ -364,17 +388,15 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
                     uint32_t key;
                     if constexpr (PT == OMR_PIXELS_FLOAT) key = raw ^ ((uint32_t)((int32_t)raw >> 31) | 0x80000000u);
                     else key = raw_key<PT>(raw);
-                    const uint32_t e = Bk0[med3_u32(key, org, hi) >> sh];
-                    uint32_t base = e & 0xFFu;
-                    uint32_t len = e >> 8;
-                    if (len > 0) {                  // the first step unrolled: usually the only one
-                        uint32_t half = len >> 1;
-                        bool le = T[base + half + 1] <= key;
-                        base = le ? base + half + 1 : base;
-                        len = le ? len - half - 1 : half;
+                    const uint32_t kc = med3_u32(key, org, hi);
+                    const uint32_t e = Bk0[kc >> sh];
+                    const uint32_t off = e >> 8;
+                    uint32_t base = (e & 0xFFu) + ((kc & inb) >= off ? 1u : 0u);
+                    if (off - 0x800000u < 0x7FFFFFu) {              // two or more thresholds here
+                        uint32_t len = off & 0xFFu;
                         while (len > 0) {
-                            half = len >> 1;
-                            le = T[base + half + 1] <= key;
+                            const uint32_t half = len >> 1;
+                            const bool le = T[base + half + 1] <= key;
                             base = le ? base + half + 1 : base;
                             len = le ? len - half - 1 : half;
                         }
@@ -463,7 +485,8 @@ struct K2Batch {
 // Positions of work block wb's chunks for this thread, then (NA > 0) every plane pointer (scalar
 // when the block sits in one tile) and every pixel load back to back: no wait between them.
 template <int BPP, int VEC, int NA, int CPT>
-__device__ __forceinline__ void k2_issue(const K2Args& A, uint32_t wb, K2Batch<BPP, VEC, NA, CPT>& B) {
+__device__ __forceinline__ void k2_issue(const K2Args& A, uint32_t wb, K2Batch<BPP, VEC, NA, CPT>& B,
+                                         uint32_t tid = threadIdx.x) {
     constexpr int NL = NA > 0 ? NA : 1;
     const uint32_t cpr = A.cpr.d, cptd = A.cpt.d;
     const uint32_t g0 = wb * (kBlock * CPT);
@@ -475,7 +498,7 @@ __device__ __forceinline__ void k2_issue(const K2Args& A, uint32_t wb, K2Batch<B
     };
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-        B.gk[k] = g0 + k * kBlock + threadIdx.x;
+        B.gk[k] = g0 + k * kBlock + tid;
         const uint32_t g = min(B.gk[k], A.total - 1);   // tail lanes load a valid chunk, store nothing
         const uint32_t t = A.tile_uniform ? btile : fdiv(g, A.cpt);
         const uint32_t rem = g - t * cptd;
@@ -542,21 +565,26 @@ __device__ __forceinline__ void k2_work(const K2Args& A, uint32_t wb, uint32_t* 
 // workgroup's next work block are issued before the current block is quantized, so every lane
 // keeps NA * CPT 16-byte loads in flight through the compute (the plain grid stride above waits
 // out the HBM latency once per block, then computes with nothing in flight).
-template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, int CPT>
-__global__ void __launch_bounds__(kBlock) k_render_pipe(const K2Args A) {
+// SUB: work blocks per workgroup (256 threads each) sharing one copy of the LDS tables, so a
+// register-light form (one chunk per lane) can hold more waves per CU than the tables' LDS
+// would allow 256-thread workgroups.
+template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int NA, int MODE, int CPT, int SUB = 1>
+__global__ void __launch_bounds__(kBlock * SUB) k_render_pipe(const K2Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_contrib[];
     K2Batch<BPP, VEC, NA, CPT> b0, b1;
-    uint32_t wb = blockIdx.x;
-    if (wb < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, wb, b0);
+    const uint32_t tid = SUB == 1 ? threadIdx.x : threadIdx.x % kBlock;
+    const uint32_t stride = gridDim.x * SUB;
+    uint32_t wb = blockIdx.x * SUB + (SUB == 1 ? 0u : threadIdx.x / kBlock);   // wave-uniform
+    if (wb < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, wb, b0, tid);
     k2_stage_tables<MODE, BPP>(A, s_contrib, NA);                 // behind the first loads
     __syncthreads();
-    while (wb < A.n_work) {                                       // uniform; two blocks per trip
-        const uint32_t w1 = wb + gridDim.x;
-        if (w1 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w1, b1);
+    while (wb < A.n_work) {                                       // wave-uniform; two blocks per trip
+        const uint32_t w1 = wb + stride;
+        if (w1 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w1, b1, tid);
         k2_finish<BPP, VEC, BE, SIGNED, PT, NA, MODE, CPT>(A, b0, s_contrib);
         if (w1 >= A.n_work) break;
-        const uint32_t w2 = w1 + gridDim.x;
-        if (w2 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w2, b0);
+        const uint32_t w2 = w1 + stride;
+        if (w2 < A.n_work) k2_issue<BPP, VEC, NA, CPT>(A, w2, b0, tid);
         k2_finish<BPP, VEC, BE, SIGNED, PT, NA, MODE, CPT>(A, b1, s_contrib);
         wb = w2;
     }
@@ -964,7 +992,7 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
     L.contrib_off = align_up(sizeof(RenderPlan), 256);
     L.thresh_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
     L.bucket_off = L.thresh_off + align_up((size_t)kMaxActive * 256 * 4, 256);
-    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * (kBuckets * 2 + sizeof(BucketMap)), 256);
+    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * (kBuckets * 4 + sizeof(BucketMap)), 256);
     L.extra_off = L.lut_off + align_up(pp.lut_bytes, 256);
     L.total = L.extra_off + extra;
     return L;
@@ -975,7 +1003,7 @@ static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
 // per instantiation: a grid sized for 8 resident blocks per CU left 3 of every 8 waiting for a
 // second round.
 static thread_local int tl_cu_count = 0;
-template <auto KERN>
+template <auto KERN, int SUB = 1>
 static int pipe_grid(const K2Args& a, int grid, size_t lds) {
     // occupancy per (device, LDS bytes) of this instantiation: the LDS footprint differs between
     // launches (threshold tables or not), and a pool's batchers launch it on several devices
@@ -992,17 +1020,17 @@ static int pipe_grid(const K2Args& a, int grid, size_t lds) {
             if (cache[i].dev == dev && cache[i].lds == lds) { occ = cache[i].occ; break; }
         if (occ < 0) {
             int o = 0;
-            occ = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, KERN, kBlock, lds) == hipSuccess ? o : 0;
+            occ = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, KERN, kBlock * SUB, lds) == hipSuccess ? o : 0;
             if (n_cache < 16) cache[n_cache++] = {dev, lds, occ};
         }
     }
     if (occ <= 0) return grid;
-    return (int)std::min<uint64_t>(a.n_work, (uint64_t)tl_cu_count * (uint64_t)occ);
+    return (int)std::min<uint64_t>((a.n_work + SUB - 1) / SUB, (uint64_t)tl_cu_count * (uint64_t)occ);
 }
 
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s, int cpt = kCPT) {
-    const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0);
+    const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_log2);
     if constexpr (BPP == 4 && VEC > 1 && (MODE == kK2Thresh || MODE == kK2Eval)) {
         // software-pipelined grid stride (k_render_pipe; cpt -1: one chunk per lane and block,
         // -2: two), the default for 1..4 channels
@@ -1010,9 +1038,14 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small
 #define OMR_PIPE(NAV, CPTV)                                                                       \
     {                                                                                             \
         constexpr auto kern = &k_render_pipe<BPP, VEC, BE, SIGNED, PT, NAV, MODE, CPTV>;         \
-        hipLaunchKernelGGL(kern, dim3(pipe_grid<kern>(a, grid, lds)), dim3(kBlock), lds, s, a);   \
+        omr_launch(kern, dim3(pipe_grid<kern>(a, grid, lds)), dim3(kBlock), lds, s, a);   \
         return hipGetLastError();                                                                 \
     }
+            if (cpt == -3 && na == 3) {   // measurement: one chunk per lane, two work blocks per workgroup
+                constexpr auto kern = &k_render_pipe<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1, 2>;
+                omr_launch(kern, dim3(pipe_grid<kern, 2>(a, grid, lds)), dim3(kBlock * 2), lds, s, a);
+                return hipGetLastError();
+            }
             switch (na * 2 + (cpt == -2 ? 1 : 0)) {
             case 2: OMR_PIPE(1, 1)
             case 3: OMR_PIPE(1, 2)
@@ -1030,10 +1063,10 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small
         // flight at 3 channels; measured slower than kCPT on C5)
         if (cpt == 4) {
             switch (na) {
-            case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 1: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 2: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 3: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 4: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 4>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
             default: break;
             }
         }
@@ -1041,20 +1074,20 @@ static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small
     if constexpr (BPP <= 2 && kCPT > 1) {   // grid-stride eval modes size their own grid
         if (small) {
             switch (na) {
-            case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
-            case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 1: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 2: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 3: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
+            case 4: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE, 1>), dim3(grid), dim3(kBlock), lds, s, a); return hipGetLastError();
             default: break;
             }
         }
     }
     switch (na) {
-    case 1: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 2: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 3: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    case 4: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
-    default: hipLaunchKernelGGL((k_render<BPP, VEC, BE, SIGNED, PT, 0, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 1: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 1, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 2: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 2, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 3: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 3, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    case 4: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 4, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
+    default: omr_launch((k_render<BPP, VEC, BE, SIGNED, PT, 0, MODE>), dim3(grid), dim3(kBlock), lds, s, a); break;
     }
     return hipGetLastError();
 }
@@ -1191,7 +1224,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     bool use_thresh = false;
     for (int i = 0; i < na; ++i) use_thresh |= pp.plan.ch[i].mode == kModeThresh;
     uint32_t* d_thresh = reinterpret_cast<uint32_t*>(ws + L.thresh_off);
-    uint16_t* d_buckets = reinterpret_cast<uint16_t*>(ws + L.bucket_off);
+    uint32_t* d_buckets = reinterpret_cast<uint32_t*>(ws + L.bucket_off);
     std::vector<uint32_t> thr;
     if (use_thresh) {                               // the code thresholds, on the host (exact)
         thr.assign((size_t)na * 256, 0u);
@@ -1227,8 +1260,8 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     }
     if (use_thresh) {
-        hipLaunchKernelGGL(k_build_buckets, dim3(kBuckets / 256, na), dim3(256), 0, ctx->stream, d_plan, d_thresh,
-                           d_buckets);
+        hipLaunchKernelGGL(k_build_buckets, dim3((1 << k2_launch_buckets_log2(na)) / 256, na), dim3(256), 0,
+                           ctx->stream, d_plan, d_thresh, d_buckets, k2_launch_buckets_log2(na));
         OMR_HIP(ctx, hipGetLastError());
     }
     (void)d_luts;
@@ -1248,6 +1281,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.contrib = d_contrib;
     a.thresh = d_thresh;
     a.buckets = d_buckets;
+    a.bk_log2 = k2_launch_buckets_log2(na);
     a.use_thresh = use_thresh ? 1 : 0;
     a.out = d_out;
     a.status = d_status;
@@ -1268,7 +1302,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     // small launches and the runtime-channel-count kernels
     // (negative: the software-pipelined float kernel, k_render_pipe, at |cpt| chunks)
     const int cpt_sel = (na >= 1 && na <= 4 && !small) ? (bpp == 4 && aligned ? ctx->k2_eval_cpt : kCPT) : 1;
-    const int cpt_thread = cpt_sel < 0 ? -cpt_sel : cpt_sel;
+    const int cpt_thread = cpt_sel == -3 ? 1 : cpt_sel < 0 ? -cpt_sel : cpt_sel;   // -3: one chunk, two blocks per WG
     a.tile_uniform = (cpt % ((uint64_t)kBlock * cpt_thread)) == 0 ? 1 : 0;
     a.nt_store = ctx->k2_nt_store ? 1 : 0;
     a.total = (uint32_t)total;
@@ -1303,11 +1337,11 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.n_work = (uint32_t)((total + per_block - 1) / per_block);
     const bool eval_mode = bpp >= 4;     // kK2Eval: grid-stride over the work blocks
     // resident blocks per CU: 8 (2 per SIMD), fewer when the LDS tables (160 KiB per CU) allow fewer
-    const uint64_t k2_res = std::min<uint64_t>(8, (160u * 1024u) / k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0));
+    const uint64_t k2_res = std::min<uint64_t>(8, (160u * 1024u) / k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_log2));
     const int grid = eval_mode ? (int)std::min<uint64_t>(a.n_work, (uint64_t)ctx->cu_count * k2_res) : (int)a.n_work;
     hipError_t e;
     const bool be = big_endian != 0;
-    KernelTimer timer(ctx, 2);
+    KernelTimer timer(ctx, 2, true);      // K2's one launch stamps its own events (hipExtLaunchKernel)
     tl_cu_count = ctx->cu_count;
     if (aligned) {
         switch (bpp) {

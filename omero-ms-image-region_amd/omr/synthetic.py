@@ -47,6 +47,7 @@ def torch_tiles_u16(n_tiles, channels, h, w, device, seed=SEED):
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed)
+    torch.manual_seed(seed)                 # the Gamma background samples from the global RNG
     out = torch.empty((n_tiles, channels, h, w), dtype=torch.int16, device=device)
     yy = torch.arange(h, device=device, dtype=torch.float32).view(h, 1)
     xx = torch.arange(w, device=device, dtype=torch.float32).view(1, w)
