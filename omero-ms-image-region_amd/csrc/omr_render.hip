@@ -235,11 +235,9 @@ __host__ __device__ constexpr int k2_buckets_log2(int na) { return na <= 4 ? kBu
 __host__ __device__ constexpr int k2_buckets(int na) { return 1 << k2_buckets_log2(na); }
 // the launch's bucket count (log2): k2_buckets_log2, or OMR_K2_BUCKETS_LG (9..11) for measurement
 static inline int k2_launch_buckets_log2(int na) {
-    static const int env = [] {
-        const char* e = std::getenv("OMR_K2_BUCKETS_LG");
-        const int v = e ? std::atoi(e) : 0;
-        return v >= 9 && v <= kBucketsLog2 ? v : 0;
-    }();
+    const char* ev = std::getenv("OMR_K2_BUCKETS_LG");      // read per call: tests A/B it
+    const int v = ev ? std::atoi(ev) : 0;
+    const int env = v >= 9 && v <= kBucketsLog2 ? v : 0;
     if (env && (size_t)na * (2048 + (4u << env) + 16) <= 64 * 1024) return env;
     return k2_buckets_log2(na);
 }

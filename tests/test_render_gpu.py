@@ -504,3 +504,37 @@ def test_inverted_and_empty_windows(ctx, pt, dtype, lo, hi):
         st, exp = O.render(chans, planes, pt, w, h)
         assert st == 0
         np.testing.assert_array_equal(got, exp, err_msg=f"window {ws}:{we}")
+
+
+@pytest.mark.parametrize("lg,cpt", [("9", "-2"), ("10", "-2"), ("11", "-1"), ("11", "-3"), ("10", "-3")])
+def test_c5_bucket_and_pipe_variants_exact(lg, cpt, monkeypatch):
+    """The measurement variants of the float threshold path (OMR_K2_BUCKETS_LG: buckets per
+    channel, read per call; OMR_K2_EVAL_CPT: chunks per lane of the pipelined kernel, -3 two work
+    blocks per workgroup, read at context creation) render the C5 composite bit-exact: coarser
+    buckets only move keys between the one-read entries and the in-bucket searches."""
+    import torch
+    import omr
+    h = w = 512
+    rng = np.random.default_rng(20261015 + 7)
+    planes = c5_planes(h, w, rng)
+    chans = c5_channels(planes)
+    src = [p.astype(">f4") for p in planes]
+    blob = np.concatenate([s.view(np.uint8).reshape(-1) for s in src])
+    n = 5                                                    # ragged against any work-block size
+    d = torch.from_numpy(np.concatenate([blob] * n)).to("cuda")
+    plane = h * w * 4
+    st, exp = O.render(chans, src, _lib.PIXELS_FLOAT, w, h, big_endian=True, model="rgb")
+    assert st == 0
+    monkeypatch.setenv("OMR_K2_BUCKETS_LG", lg)
+    monkeypatch.setenv("OMR_K2_EVAL_CPT", cpt)
+    c = omr.Context(0)
+    try:
+        out = torch.empty((n, h, w), dtype=torch.int32, device="cuda")
+        c.render_batch_strided_device(O.make_qdef("rgb"), chans, d, 3 * plane, plane, n, _lib.PIXELS_FLOAT, w, h,
+                                      out, big_endian=True)
+        c.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+    finally:
+        c.close()
+    for t in range(n):
+        np.testing.assert_array_equal(got[t], exp, err_msg=f"tile {t}")
