@@ -82,8 +82,8 @@ struct K2Args {
     const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
     const uint32_t* thresh;     // [n_active][256] kModeThresh code thresholds (K1)
-    const uint32_t* buckets;    // [n_active][1 << bk_log2] kModeThresh key buckets (K1)
-    int32_t bk_log2;            // buckets per channel (log2): k2_buckets_log2(n_active)
+    const uint32_t* buckets;    // [n_active][bk_n] kModeThresh key buckets (K1)
+    int32_t bk_n;               // buckets per channel: k2_launch_buckets(n_active)
     int32_t use_thresh;         // some channel is kModeThresh: stage thresh + buckets in LDS too
     uint32_t n_work;            // work blocks of 256*CPT chunks (grid-stride in eval mode)
     uint32_t* out;              // [n_tiles][H][W]
@@ -233,13 +233,19 @@ constexpr int kBucketsLog2 = OMR_K2_BUCKETS_LOG2, kBuckets = 1 << kBucketsLog2;
 // ride on top).
 __host__ __device__ constexpr int k2_buckets_log2(int na) { return na <= 4 ? kBucketsLog2 : kBucketsLog2 - 1; }
 __host__ __device__ constexpr int k2_buckets(int na) { return 1 << k2_buckets_log2(na); }
-// the launch's bucket count (log2): k2_buckets_log2, or OMR_K2_BUCKETS_LG (9..11) for measurement
-static inline int k2_launch_buckets_log2(int na) {
-    const char* ev = std::getenv("OMR_K2_BUCKETS_LG");      // read per call: tests A/B it
-    const int v = ev ? std::atoi(ev) : 0;
-    const int env = v >= 9 && v <= kBucketsLog2 ? v : 0;
-    if (env && (size_t)na * (2048 + (4u << env) + 16) <= 64 * 1024) return env;
-    return k2_buckets_log2(na);
+// the launch's bucket count: k2_buckets, or for measurement OMR_K2_BUCKETS_LG (10..11: 2^lg) /
+// OMR_K2_BUCKETS (a multiple of 256 from 1024 to 2048), read per call (tests A/B them)
+static inline int k2_launch_buckets(int na) {
+    int env = 0;
+    if (const char* ev = std::getenv("OMR_K2_BUCKETS")) {
+        const int v = std::atoi(ev);
+        if (v >= 1024 && v <= kBuckets && v % 256 == 0) env = v;
+    } else if (const char* el = std::getenv("OMR_K2_BUCKETS_LG")) {
+        const int v = std::atoi(el);
+        if (v >= 10 && v <= kBucketsLog2) env = 1 << v;
+    }
+    if (env && (size_t)na * (2048 + 4u * env + 16) <= 64 * 1024) return env;
+    return k2_buckets(na);
 }
 constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 4u * (kBuckets / 2)));
 
@@ -250,12 +256,12 @@ constexpr int kMaxThreshActive = (int)((48u * 1024u) / (1024u + 1024u + 4u * (kB
 // (saturated at 2^32 - 1).  T[1] lands in bucket 1 (bucket 0 holds no threshold), T[cmax] at most
 // in bucket (span >> shift) + 2.
 struct BucketMap { uint32_t org, hi, sh, pad; };
-__device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1, int lg) {
+__device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1, uint32_t nbk) {
     const uint32_t span = k1 - t1;
     const uint32_t bits = span ? 32u - (uint32_t)__clz(span) : 0u;
-    const uint32_t nbk = 1u << lg;
-    uint32_t sh = bits > (uint32_t)lg ? bits - lg : 0u;
-    while ((span >> sh) > nbk - 3u) ++sh;                 // sh <= 23 (span < 2^32, lg >= 10)
+    const uint32_t lg = 31u - (uint32_t)__clz(nbk);
+    uint32_t sh = bits > lg ? bits - lg : 0u;
+    while ((span >> sh) > nbk - 3u) ++sh;                 // sh <= 23 (span < 2^32, nbk >= 1024)
     BucketMap m;
     m.sh = sh;
     const uint64_t step = 1ull << sh;
@@ -288,15 +294,14 @@ __device__ __forceinline__ uint32_t thresh_count(const uint32_t* __restrict__ T,
 // read -- and only keys in a bucket of two or more thresholds search its n thresholds.
 __global__ void __launch_bounds__(256) k_build_buckets(const RenderPlan* __restrict__ plan,
                                                        const uint32_t* __restrict__ thr,
-                                                       uint32_t* __restrict__ bkt, int lg) {
+                                                       uint32_t* __restrict__ bkt, int nbk) {
     const int a = blockIdx.y;
     if (plan->ch[a].mode != kModeThresh) return;
-    const int nbk = 1 << lg;
     const uint32_t* T = thr + a * 256;
     const uint32_t cmax = T[0] & 0xFFu;
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     const uint32_t k1 = cmax ? T[cmax] : 0u;
-    const BucketMap m = bucket_map(cmax ? T[1] : 0u, k1, lg);
+    const BucketMap m = bucket_map(cmax ? T[1] : 0u, k1, (uint32_t)nbk);
     if (b == 0) reinterpret_cast<BucketMap*>(bkt + gridDim.y * nbk)[a] = m;
     uint32_t e = 0xFFFFFF00u;
     if (cmax) {
@@ -318,8 +323,8 @@ constexpr int kCPT = OMR_K2_CPT;   // chunks per thread of the fixed-channel-cou
 
 // LDS of one K2 block: contrib [na][256] u32, then (kModeThresh) thresholds [na][256] u32 and
 // buckets [na][k2_buckets(na)] u32 + their maps.
-__host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh, int lg) {
-    return (size_t)na * (1024 + (thresh ? 1024 + 4 * (1 << lg) + sizeof(BucketMap) : 0));
+__host__ __device__ constexpr size_t k2_lds_bytes(int na, bool thresh, int nbk) {
+    return (size_t)na * (1024 + (thresh ? 1024 + 4 * nbk + sizeof(BucketMap) : 0));
 }
 
 template <int MODE, int BPP>
@@ -334,7 +339,7 @@ __device__ __forceinline__ void k2_stage_tables(const K2Args& A, uint32_t* s_con
                 *reinterpret_cast<uint4*>(s_thr + i) = *reinterpret_cast<const uint4*>(A.thresh + i);
             uint32_t* s_b = s_thr + na * 256;
             const uint32_t* g_b = reinterpret_cast<const uint32_t*>(A.buckets);
-            for (int i = threadIdx.x * 4; i < na * ((1 << A.bk_log2) + 4); i += blockDim.x * 4)   // + the maps
+            for (int i = threadIdx.x * 4; i < na * (A.bk_n + 4); i += blockDim.x * 4)   // + the maps
                 *reinterpret_cast<uint4*>(s_b + i) = *reinterpret_cast<const uint4*>(g_b + i);
         }
     }
@@ -355,7 +360,7 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
     };
     const uint32_t* const s_thr = s_contrib + na * 256;
     const uint32_t* const s_bkt = s_thr + na * 256;
-    const int nbk = 1 << A.bk_log2;
+    const int nbk = A.bk_n;
     const int64_t in_off = ((int64_t)row * A.row_stride + (int64_t)cc * VEC) * BPP;
     uint32_t acc[VEC];
 #pragma unroll
@@ -1028,7 +1033,7 @@ static int pipe_grid(const K2Args& a, int grid, size_t lds) {
 
 template <int BPP, int VEC, bool BE, bool SIGNED, int PT, int MODE>
 static hipError_t launch_render_na(const K2Args& a, int na, int grid, bool small, hipStream_t s, int cpt = kCPT) {
-    const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_log2);
+    const size_t lds = k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_n);
     if constexpr (BPP == 4 && VEC > 1 && (MODE == kK2Thresh || MODE == kK2Eval)) {
         // software-pipelined grid stride (k_render_pipe; cpt -1: one chunk per lane and block,
         // -2: two), the default for 1..4 channels
@@ -1258,8 +1263,8 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     }
     if (use_thresh) {
-        hipLaunchKernelGGL(k_build_buckets, dim3((1 << k2_launch_buckets_log2(na)) / 256, na), dim3(256), 0,
-                           ctx->stream, d_plan, d_thresh, d_buckets, k2_launch_buckets_log2(na));
+        hipLaunchKernelGGL(k_build_buckets, dim3(k2_launch_buckets(na) / 256, na), dim3(256), 0,
+                           ctx->stream, d_plan, d_thresh, d_buckets, k2_launch_buckets(na));
         OMR_HIP(ctx, hipGetLastError());
     }
     (void)d_luts;
@@ -1279,7 +1284,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.contrib = d_contrib;
     a.thresh = d_thresh;
     a.buckets = d_buckets;
-    a.bk_log2 = k2_launch_buckets_log2(na);
+    a.bk_n = k2_launch_buckets(na);
     a.use_thresh = use_thresh ? 1 : 0;
     a.out = d_out;
     a.status = d_status;
@@ -1335,7 +1340,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     a.n_work = (uint32_t)((total + per_block - 1) / per_block);
     const bool eval_mode = bpp >= 4;     // kK2Eval: grid-stride over the work blocks
     // resident blocks per CU: 8 (2 per SIMD), fewer when the LDS tables (160 KiB per CU) allow fewer
-    const uint64_t k2_res = std::min<uint64_t>(8, (160u * 1024u) / k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_log2));
+    const uint64_t k2_res = std::min<uint64_t>(8, (160u * 1024u) / k2_lds_bytes(na > 0 ? na : 1, a.use_thresh != 0, a.bk_n));
     const int grid = eval_mode ? (int)std::min<uint64_t>(a.n_work, (uint64_t)ctx->cu_count * k2_res) : (int)a.n_work;
     hipError_t e;
     const bool be = big_endian != 0;

@@ -506,7 +506,8 @@ def test_inverted_and_empty_windows(ctx, pt, dtype, lo, hi):
         np.testing.assert_array_equal(got, exp, err_msg=f"window {ws}:{we}")
 
 
-@pytest.mark.parametrize("lg,cpt", [("9", "-2"), ("10", "-2"), ("11", "-1"), ("11", "-3"), ("10", "-3")])
+@pytest.mark.parametrize("lg,cpt", [("10", "-2"), ("11", "-1"), ("11", "-3"), ("10", "-3"), ("n1280", "-2"),
+                                    ("n1792", "-2")])
 def test_c5_bucket_and_pipe_variants_exact(lg, cpt, monkeypatch):
     """The measurement variants of the float threshold path (OMR_K2_BUCKETS_LG: buckets per
     channel, read per call; OMR_K2_EVAL_CPT: chunks per lane of the pipelined kernel, -3 two work
@@ -525,7 +526,10 @@ def test_c5_bucket_and_pipe_variants_exact(lg, cpt, monkeypatch):
     plane = h * w * 4
     st, exp = O.render(chans, src, _lib.PIXELS_FLOAT, w, h, big_endian=True, model="rgb")
     assert st == 0
-    monkeypatch.setenv("OMR_K2_BUCKETS_LG", lg)
+    if lg.startswith("n"):
+        monkeypatch.setenv("OMR_K2_BUCKETS", lg[1:])        # a bucket count, not a power of two
+    else:
+        monkeypatch.setenv("OMR_K2_BUCKETS_LG", lg)
     monkeypatch.setenv("OMR_K2_EVAL_CPT", cpt)
     c = omr.Context(0)
     try:
