@@ -322,7 +322,7 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
 
 PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "png_sq.json")
 # batched PNG stages (omr_png.hip launch_png_batch timer kinds) -> the kernels they launch
-PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse",),
+PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse", "k_pngb_hist"),
                      22: ("k_pngb_tables", "k_pngb_block_offsets"), 23: ("k_pngb_encode",),
                      24: ("k_pngb_fixup", "k_pngb_meta", "k_pngb_offsets"), 25: ("k_pngb_emit",),
                      26: ("k_pngb_crc", "k_pngb_finish")}
@@ -355,6 +355,36 @@ def png_valu_roofline(stage_ms):
                           "lds_bank_conflict_share": round(conf / lds, 3) if lds else None,
                           "avg_ms": round(ms, 5)}
     return out
+
+
+PNG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "f2_pmc_traffic_png.json")
+
+
+def png_measured_traffic(alg_bytes):
+    """HBM bytes per batched-PNG call of 256 C2 tiles, per stage, from the committed PMC passes
+    (tools/gpu.sh pmc=png: FETCH_SIZE x 2 read, WRITE_SIZE written, one counter per pass; each
+    kernel's largest grid = the 256-tile launch), against this run's algorithmic bytes (ARGB in +
+    files out)."""
+    try:
+        with open(PNG_PMC) as fh:
+            ks = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    big = {}
+    for k in ks:
+        name = k["kernel"].split("(")[0].split("::")[-1]
+        if "hbm_read_bytes" in k and (name not in big or k["grid_size"] > big[name]["grid_size"]):
+            big[name] = k
+    per = {}
+    for kind, names in PNG_STAGE_KERNELS.items():
+        rows = [big[n] for n in names if n in big]
+        if rows:
+            per[str(kind)] = {"kernels": list(names), "read_mb": round(sum(r["hbm_read_bytes"] for r in rows) / 1e6, 1),
+                              "write_mb": round(sum(r["hbm_write_bytes"] for r in rows) / 1e6, 1)}
+    tot = sum(v["read_mb"] + v["write_mb"] for v in per.values()) * 1e6
+    return {"source": os.path.relpath(PNG_PMC, os.path.dirname(os.path.abspath(__file__))), "per_stage": per,
+            "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(alg_bytes / 1e6, 1),
+            "ratio": round(tot / alg_bytes, 3) if alg_bytes else None}
 
 
 JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04u2.json")
@@ -819,6 +849,9 @@ def png_section(torch, ctx, data):
             vr = png_valu_roofline(avg)
             if vr:
                 leg["valu_roofline"] = vr
+            mt = png_measured_traffic(alg_all)
+            if mt:
+                leg["roofline"]["measured_traffic"] = mt
         batched[f"tiles_per_call_{n}"] = leg
     res["batched"] = batched
     if "tiles_per_call_256" in batched:
