@@ -414,7 +414,7 @@ def jpeg_measured_traffic(algo_bytes):
 
 def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
     """B1 / F1 / B3 are VALU-issue-bound: achieved = VALU issue cycles per launch
-    (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/profile_jpeg_r04.sh, at 2 cycles,
+    (SQ_INSTS_VALU per MCU from the committed PMC passes, tools/gpu.sh sq=jpeg, at 2 cycles,
     plus 2 more for every f64 and transcendental instruction) x MCUs / the kernel's measured average
     duration; peak = every SIMD issuing every cycle at 2.4 GHz."""
     case = "c1" if name.startswith("c1") else "c2"

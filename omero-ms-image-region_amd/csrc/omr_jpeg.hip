@@ -821,8 +821,8 @@ __constant__ uint8_t c_zigzag[64] = {
     35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
     58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
-// Measurement-only ablations of B1 / F1 (tools/ablate_jpeg.sh builds libomr variants with
-// -DOMR_ABL=<mask>; their outputs are wrong).  0 in every real build.
+// Measurement-only ablations of B1 / F1 (`tools/ab_build.sh abl<m> -DOMR_ABL=<m>` builds a libomr
+// variant; its outputs are wrong).  0 in every real build.
 #ifndef OMR_ABL
 #define OMR_ABL 0
 #endif

@@ -1563,10 +1563,10 @@ struct PngBatch {
     uint16_t* bh;                               // [parse blocks][316] symbol counts of each parse block
     uint32_t* poff;                             // [parse blocks] bit offset of each parse block's codes
     uint32_t* img_bits;                         // [n] stream bits: header + codes + EOB
-    uint32_t* blk_b0;                           // [parse blocks] first bit of the block in its stream
-    uint32_t* blk_b1;                           // [parse blocks] one past its last bit
-    uint32_t* blk_cf;                           // [parse blocks] its first (partial) word
-    uint32_t* blk_cl;                           // [parse blocks] its last (partial) word
+    uint32_t* blk_b0;                           // [groups] first bit of the P4 group (kPngbGroup segments) in its stream
+    uint32_t* blk_b1;                           // [groups] one past its last bit
+    uint32_t* blk_cf;                           // [groups] its first (partial) word
+    uint32_t* blk_cl;                           // [groups] its last (partial) word
     int32_t total_pblk, pad3;
     int64_t total_segs;
     uint32_t* trace;                            // [3][segments] parse traces (S, M, D)

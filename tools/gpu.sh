@@ -17,6 +17,9 @@
 #   pmc=<probe>                FETCH_SIZE / WRITE_SIZE passes over a probe -> pmc_traffic_<probe>.json
 #   sq=<probe>                 SQ instruction / wait / LDS-conflict passes -> sq_<probe>.txt
 #   py=<script> [args]         python3 tools/<script> [args] -> <script>.out
+#   ab=<probe>:<v1>[,<v2>...]  same-box A/B/n: kernel traces of the probe with the in-tree libomr.so
+#                              ("new") and ab/libomr_<v>.so (OMR_LIB; built by tools/ab_build.sh),
+#                              alternated twice -> per-kernel medians in ab_<probe>.txt
 set -o pipefail
 TAG=${1:?tag}; shift
 O=gpurun_out/$TAG; mkdir -p $O
@@ -113,6 +116,22 @@ for step in "$@"; do
         python3 tools/sq_json.py $O/sq_$arg.txt $O/sq_$arg.json $TAG > /dev/null || exit 1
         find $O/sq_$arg -name '*counter_collection.csv' -delete
         grep -E "==|VALU/wave|WAIT|BANK|IDX" $O/sq_$arg.txt | head -40 ;;
+    ab)
+        probe=${arg%%:*}; vars=${arg#*:}
+        cmd=$(probe_cmd $probe) || exit 2
+        for i in 1 2; do
+            for v in new ${vars//,/ }; do
+                if [ $v = new ]; then unset OMR_LIB; else export OMR_LIB=$R/ab/libomr_$v.so; fi
+                ( cd /tmp && JPEG_PROBE_ITERS=${JPEG_PROBE_ITERS:-10} timeout -k 10 240 rocprofv3 --kernel-trace \
+                    --output-format csv -d $R/$O/ab_$v$i -o t -- $cmd ) > $O/ab_$v$i.log 2>&1 \
+                    || { echo "ab $v $i failed"; tail -20 $O/ab_$v$i.log; exit 1; }
+                f=$(find $O/ab_$v$i -name '*kernel_trace.csv' | head -1)
+                { echo "== $v $i"; python3 tools/trace_summary.py $f; } >> $O/ab_$probe.txt
+                rm -rf $O/ab_$v$i
+            done
+        done
+        unset OMR_LIB
+        cat $O/ab_$probe.txt | cut -c1-120 ;;
     py)
         script=${arg%% *}; rest=${arg#"$script"}
         run 600 $(basename $script .py).out python3 -u tools/$script $rest

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """C2 -> JPEG (or, with JPEG_PROBE_CASE=c1, C1: 1-channel uint8 greyscale) on 64 tiles (JPEG_PROBE_TILES), unfused
 (K1+K2 then B1..B6) and fused (F1..B6), a few calls each: the program the JPEG PMC passes
-(tools/profile_jpeg_r02.sh) profile."""
+(tools/gpu.sh sq=jpeg / pmc=jpeg / ab=jpeg:...) profile."""
 import os
 import sys
 
