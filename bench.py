@@ -310,6 +310,32 @@ def jpeg_section(torch, ctx, data, B, steps, warmup, cpu_seconds, threads, with_
     return res
 
 
+def kernel_build_id():
+    """Fingerprint of the kernel sources (csrc/*.hip and the device headers): a committed SQ / PMC
+    profile carries the id of the build it was collected on (tools/sq_json.py, tools/pmc_traffic.py),
+    and the bench marks a profile of another build as such instead of mixing it silently into this
+    run's rooflines."""
+    import hashlib
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "omero-ms-image-region_amd", "csrc")
+    h = hashlib.sha1()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:12]
+
+
+def profile_provenance(doc, path):
+    """source / build fields for a roofline read from a committed profile file."""
+    bid = doc.get("build_id") if isinstance(doc, dict) else None
+    cur = kernel_build_id()
+    out = {"source": os.path.relpath(path, os.path.dirname(os.path.abspath(__file__))),
+           "profile_build_id": bid, "this_build_id": cur, "same_build": bid == cur}
+    if bid != cur:
+        out["note"] = "committed profile of another build: counters not measured this run"
+    return out
+
+
 VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "jpeg_valu_pmc.json")
 VALU_PEAK_ISSUE_CYCLES_PER_S = 256 * 4 * 2.4e9   # 1,024 SIMD-32s at 2.4 GHz
 # issue cycles of one wave64 VALU instruction: 2 on a SIMD-32; f64 add / mul / fma issue at half
@@ -339,8 +365,8 @@ def png_valu_roofline(stage_ms):
     except (OSError, ValueError):
         return None
     ks = doc.get("kernels", {})
-    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S,
-           "source": os.path.relpath(PNG_SQ, os.path.dirname(os.path.abspath(__file__)))}
+    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S}
+    out.update(profile_provenance(doc, PNG_SQ))
     for kind, names in PNG_STAGE_KERNELS.items():
         ms = stage_ms.get(kind)
         rows = [v for k, v in ks.items() if any(k.endswith("::" + nm) for nm in names)]
@@ -367,7 +393,8 @@ def png_measured_traffic(alg_bytes):
     files out)."""
     try:
         with open(PNG_PMC) as fh:
-            ks = json.load(fh)["kernels"]
+            doc = json.load(fh)
+        ks = doc["kernels"]
     except (OSError, ValueError, KeyError):
         return None
     big = {}
@@ -382,9 +409,10 @@ def png_measured_traffic(alg_bytes):
             per[str(kind)] = {"kernels": list(names), "read_mb": round(sum(r["hbm_read_bytes"] for r in rows) / 1e6, 1),
                               "write_mb": round(sum(r["hbm_write_bytes"] for r in rows) / 1e6, 1)}
     tot = sum(v["read_mb"] + v["write_mb"] for v in per.values()) * 1e6
-    return {"source": os.path.relpath(PNG_PMC, os.path.dirname(os.path.abspath(__file__))), "per_stage": per,
-            "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(alg_bytes / 1e6, 1),
-            "ratio": round(tot / alg_bytes, 3) if alg_bytes else None}
+    out = profile_provenance(doc, PNG_PMC)
+    out.update({"per_stage": per, "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(alg_bytes / 1e6, 1),
+                "ratio": round(tot / alg_bytes, 3) if alg_bytes else None})
+    return out
 
 
 JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04u2.json")
@@ -398,7 +426,8 @@ def jpeg_measured_traffic(algo_bytes):
     pass), against this run's algorithmic bytes (planes in + JPEG files out)."""
     try:
         with open(JPEG_PMC) as fh:
-            ks = json.load(fh)["kernels"]
+            doc = json.load(fh)
+        ks = doc["kernels"]
     except (OSError, ValueError, KeyError):
         return None
     per = {}
@@ -407,9 +436,10 @@ def jpeg_measured_traffic(algo_bytes):
         if k is not None:
             per[key] = {"read_mb": round(k["hbm_read_bytes"] / 1e6, 1), "write_mb": round(k["hbm_write_bytes"] / 1e6, 1)}
     tot = sum(v["read_mb"] + v["write_mb"] for v in per.values()) * 1e6
-    return {"source": os.path.relpath(JPEG_PMC, os.path.dirname(os.path.abspath(__file__))), "per_kernel": per,
-            "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(algo_bytes / 1e6, 1),
-            "ratio": round(tot / algo_bytes, 3)}
+    out = profile_provenance(doc, JPEG_PMC)
+    out.update({"per_kernel": per, "total_mb": round(tot / 1e6, 1), "algorithmic_mb": round(algo_bytes / 1e6, 1),
+                "ratio": round(tot / algo_bytes, 3)})
+    return out
 
 
 def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
@@ -420,11 +450,13 @@ def jpeg_valu_roofline(name, mcus, j1_ms, f1_ms, j3_ms):
     case = "c1" if name.startswith("c1") else "c2"
     try:
         with open(VALU_PMC) as fh:
-            pmc = json.load(fh).get(case, {})
+            doc = json.load(fh)
+        pmc = doc.get(case, {})
     except (OSError, ValueError):
         return None
-    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S,
-           "source": os.path.relpath(VALU_PMC, os.path.dirname(os.path.abspath(__file__))) + f" [{case}]"}
+    out = {"bound": "valu", "unit": "issue-cycles/s", "peak": VALU_PEAK_ISSUE_CYCLES_PER_S}
+    out.update(profile_provenance(doc, VALU_PMC))
+    out["source"] += f" [{case}]"
     for label, key, ms in (("B1_fdct", "k_jpeg_fdct_batch", j1_ms), ("F1_render_fdct", "k_jpeg_render_fdct", f1_ms),
                            ("B3_huffman", "k_jpeg_huff_thread", j3_ms)):
         k = next((k for k in pmc if key in k), None)
@@ -516,6 +548,7 @@ def _timed(torch, ctx, step, steps, warmup):
 
 
 C3_WINDOWS, C3_WINDOW_S = 7, 0.05
+C3_SETS = 4            # distinct C3 request stack sets (96 MiB each) taken in turn
 
 
 def _gated_burst_ms(torch, ctx, launch, n, gate_ms=30.0):
@@ -594,10 +627,22 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
     S, Z, C = 512, 64, 3
     g = torch.Generator(device=dev)
     g.manual_seed(20261015 + 3)
-    # uniform uint16 values (every LUT entry, worst case for the window compares), stored big-endian
-    stacks = [torch.randint(0, 65536, (Z, S, S), dtype=torch.int32, device=dev, generator=g) for _ in range(C)]
-    stacks = [(s & 0xFF) << 8 | (s >> 8) for s in stacks]                                # -> BE bytes
-    stacks = [(s - 65536 * (s >= 32768).to(torch.int32)).to(torch.int16).contiguous() for s in stacks]
+    # uniform uint16 values (every LUT entry, worst case for the window compares), stored big-endian.
+    # C3_SETS distinct request stacks (3 x 32 MiB each) taken in turn: their 384 MiB exceed the
+    # 256 MiB Infinity Cache, so every request reads its planes from HBM as a stream of distinct
+    # requests does (round 5 re-read one 96 MiB set, partly a cache hit: its per-launch events read
+    # 3 % faster than a rocprofv3 trace of the same kernel)
+    def make_set():
+        st = [torch.randint(0, 65536, (Z, S, S), dtype=torch.int32, device=dev, generator=g) for _ in range(C)]
+        st = [(s & 0xFF) << 8 | (s >> 8) for s in st]                                   # -> BE bytes
+        return [(s - 65536 * (s >= 32768).to(torch.int32)).to(torch.int16).contiguous() for s in st]
+    sets = [make_set() for _ in range(C3_SETS)]
+    stacks = sets[0]
+    turn = [0]
+
+    def next_set():
+        turn[0] += 1
+        return sets[turn[0] % C3_SETS]
     chans = c2_channels(C)
     qd = make_qdef("rgb")
     out = torch.empty((S, S), dtype=torch.int32, device=dev)
@@ -607,7 +652,7 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
     res = {}
     for name, alg, end in (("max", _lib.PROJECTION_MAX, Z - 1), ("mean", _lib.PROJECTION_MEAN, Z - 1)):
         def step():
-            ctx.render_projected_device(qd, chans, stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, out,
+            ctx.render_projected_device(qd, chans, next_set(), _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, out,
                                         big_endian=True, bindings=binds)
         el, avg = _timed(torch, ctx, step, steps, warmup)
         one = _windows(ctx.synchronize, step, C3_WINDOWS, C3_WINDOW_S)
@@ -617,16 +662,17 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
         ctxs = [ctx, ctx2]
         k = [0]
 
-        def step2():
+        def step2():            # requests 2j and 2j + 1 (one per context) read stack set j
             i = k[0] & 1
+            st = sets[(k[0] >> 1) % C3_SETS]
             k[0] += 1
-            ctxs[i].render_projected_device(qd, chans, stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end,
-                                            outs[i], big_endian=True, bindings=binds)
+            ctxs[i].render_projected_device(qd, chans, st, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, outs[i],
+                                            big_endian=True, bindings=binds)
 
         def sync2():
             ctx.synchronize()
             ctx2.synchronize()
-        for _ in range(warmup):
+        for _ in range(2 * warmup):    # even: the last two requests read the same set
             step2()
         sync2()
         two = _windows(sync2, step2, C3_WINDOWS, C3_WINDOW_S)
@@ -638,7 +684,7 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
             outs3 = [torch.empty((S, S), dtype=torch.int16, device=dev) for _ in range(C)]
 
             def k3_launch():
-                ctx.project_stacks_device(stacks, _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, outs3,
+                ctx.project_stacks_device(next_set(), _lib.PIXELS_UINT16, S, S, Z, alg, 0, end, outs3,
                                           big_endian_in=True)
             # back-to-back launches overlap one's tail with the next one's head: a throughput
             # figure, reported beside the roofline (which follows the kernel trace's duration)
@@ -666,7 +712,9 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
                           "unit": "GB/s", "frac": round(alg_bytes / (k3 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                           "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(k3, 5),
                           "timing": "per-launch HIP events around each launch on its stream (system fence "
-                                    "off): the kernel duration a rocprofv3 trace reports"}}
+                                    "off): the kernel duration a rocprofv3 trace reports",
+                          "working_set": f"{C3_SETS} request stack sets x {C * Z * S * S * 2 >> 20} MiB in turn "
+                                         "(beyond the 256 MiB Infinity Cache)"}}
         if burst:
             r["roofline"]["burst_throughput_frac"] = round(alg_bytes / (burst * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             r["roofline"]["burst_timing"] = ("200 launches queued behind a spin kernel, two events around the "
@@ -1226,6 +1274,69 @@ def pcie_probe(torch, device, mib=512):
     return res
 
 
+def _get(d, *keys):
+    for k in keys:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return d
+
+
+def sections_summary(line):
+    """The headline figure of every section, as the LAST key of the JSON line: a driver record that
+    keeps only the line's tail still shows them (the detail, with its sources, is earlier in the
+    line).  Fracs are HBM (or VALU-issue) fractions of peak; ms are per-launch averages."""
+    s = {"c2_render": {"tiles_per_s": line.get("value"), "hbm_frac": _get(line, "roofline", "frac"),
+                       "k2_avg_ms": _get(line, "roofline", "avg_launch_ms"),
+                       "traffic_ratio": (round(line["roofline"]["traffic"] / line["roofline"]["algorithmic_bytes_per_launch"], 4)
+                                         if _get(line, "roofline", "traffic") else None)}}
+    for case in ("c2_u16_4ch_rgb_to_jpeg", "c1_u8_grey_to_jpeg"):
+        j = _get(line, "jpeg", case)
+        if j:
+            s["jpeg_" + case.split("_")[0]] = {
+                "fused_tiles_per_s": _get(j, "fused", "tiles_per_s"), "unfused_tiles_per_s": j.get("tiles_per_s"),
+                "f1_ms": _get(j, "fused", "kernel_ms", "F1_render_fdct"),
+                "fused_total_ms": _get(j, "fused", "kernel_ms", "jpeg_total"),
+                "f1_valu_frac": _get(j, "valu_roofline", "F1_render_fdct", "frac"),
+                "traffic_ratio": _get(j, "valu_roofline", "measured_traffic", "ratio"),
+                "byte_identical_to_unfused": _get(j, "fused", "byte_identical_to_unfused")}
+    p = _get(line, "png", "batched", "tiles_per_call_256")
+    if p:
+        s["png_batched_256"] = {"tiles_per_s": p.get("tiles_per_s"), "ms_per_call": p.get("ms_per_call"),
+                                "hbm_frac": _get(p, "roofline", "frac"),
+                                "traffic_ratio": _get(p, "roofline", "measured_traffic", "ratio")}
+    for alg in ("max", "mean"):
+        c = _get(line, "c3_projection", alg)
+        if c:
+            s["c3_" + alg] = {"hbm_frac": _get(c, "roofline", "frac"), "k3_avg_ms": _get(c, "roofline", "avg_launch_ms"),
+                              "k3_trace_frac": _get(c, "roofline", "trace_consistent_frac"),
+                              "requests_per_s": c.get("requests_per_s")}
+    c5 = line.get("c5_float")
+    if c5:
+        s["c5_float"] = {"hbm_frac": _get(c5, "roofline", "frac"), "k2_avg_ms": _get(c5, "roofline", "avg_launch_ms"),
+                         "tiles_per_s": c5.get("tiles_per_s")}
+    h = line.get("host_fed")
+    if h:
+        s["host_fed"] = {"tiles_per_s": _get(h, "device_out", "tiles_per_s"),
+                         "vs_pcie_probe": h.get("device_out_vs_pcie_probe")}
+        it = _get(h, "serving", "interactive")
+        if it:
+            bk = next((k for k in it if k.startswith("batcher")), None)
+            s["serving_one_in_flight"] = {
+                "batcher_tiles_per_s": _get(it, bk, "tiles_per_s"), "batcher_p50_ms": _get(it, bk, "p50_ms"),
+                "independent_tiles_per_s": _get(it, "independent_contexts", "tiles_per_s"),
+                "independent_p50_ms": _get(it, "independent_contexts", "p50_ms")}
+    lat = line.get("p50_tile_latency_ms")
+    if lat:
+        s["p50_ms"] = {"render_c_abi": _get(lat, "native_c_abi", "render_device_resident", "p50_ms"),
+                       "render_jpeg_c_abi": _get(lat, "native_c_abi", "render_jpeg_one_call", "p50_ms")}
+    if line.get("cpu_baseline"):
+        s["cpu_baseline_tiles_per_s"] = line["cpu_baseline"].get("value")
+        if line.get("value") and line["cpu_baseline"].get("value"):
+            s["gpu_vs_cpu"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
+    return s
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` without a launcher: start N rank processes (RANK/LOCAL_RANK/
     WORLD_SIZE/MASTER_* as torch.distributed.run sets them) and wait for them.  Called before
@@ -1508,6 +1619,7 @@ def main():
         line.update(extra)
         if "cpu_baseline" not in line:
             line["cpu_baseline"] = None
+        line["sections"] = sections_summary(line)      # last: the part of the line a tail keeps
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist:

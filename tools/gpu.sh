@@ -114,6 +114,10 @@ for step in "$@"; do
         done
         python3 tools/pmc_kernels.py $(find $O/sq_$arg -name '*counter_collection.csv') > $O/sq_$arg.txt || exit 1
         python3 tools/sq_json.py $O/sq_$arg.txt $O/sq_$arg.json $TAG > /dev/null || exit 1
+        if [ $arg = jpeg ]; then      # per-MCU form for bench.py's JPEG VALU roofline (1024^2 tiles: 4096 MCUs)
+            python3 tools/pmc_kernels.py --json $O/jpeg_valu_pmc.json --case ${JPEG_PROBE_CASE:-c2} \
+                --mcus $((JPEG_PROBE_TILES * 4096)) $(find $O/sq_$arg -name '*counter_collection.csv') > /dev/null || exit 1
+        fi
         find $O/sq_$arg -name '*counter_collection.csv' -delete
         grep -E "==|VALU/wave|WAIT|BANK|IDX" $O/sq_$arg.txt | head -40 ;;
     ab)

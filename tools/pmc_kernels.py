@@ -61,6 +61,8 @@ def main():
             with open(opt["json"]) as fh:
                 doc = json.load(fh)
         doc[opt.get("case", "default")] = out
+        from build_id import build_id
+        doc["build_id"] = build_id()
         with open(opt["json"], "w") as fh:
             json.dump(doc, fh, indent=1, sort_keys=True)
 

@@ -37,8 +37,9 @@ def main():
         if "WRITE_SIZE" in rec:
             rec["hbm_write_bytes"] = rec["WRITE_SIZE"] * 1024
         res.append(rec)
+    from build_id import build_id
     with open(out, "w") as fh:
-        json.dump({"note": "per dispatch; read = FETCH_SIZE x 2 x 1024 (gfx950), write = WRITE_SIZE x 1024; "
+        json.dump({"build_id": build_id(), "note": "per dispatch; read = FETCH_SIZE x 2 x 1024 (gfx950), write = WRITE_SIZE x 1024; "
                            "one counter per pass", "kernels": res}, fh, indent=1)
     for r in res:
         print(f'{r["kernel"][:90]:90s} grid {r["grid_size"]:>9d} rd {r.get("hbm_read_bytes", 0) / 1e6:10.3f} MB '

@@ -11,7 +11,8 @@ import sys
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
-    doc = {"source": sys.argv[3] if len(sys.argv) > 3 else src,
+    from build_id import build_id
+    doc = {"source": sys.argv[3] if len(sys.argv) > 3 else src, "build_id": build_id(),
            "note": "per-launch means over the probe's dispatches of each kernel's largest grid", "kernels": {}}
     cur = None
     for line in open(src):
