@@ -234,6 +234,7 @@ void omr_ctx_destroy(omr_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->aux) (void)hipFree(c->aux);
     if (c->d_crc_pow) (void)hipFree(c->d_crc_pow);
+    for (auto& l : c->dev_luts) (void)hipFree(l.d);
     if (c->d_flag) (void)hipFree(c->d_flag);
     if (c->h_flag) (void)hipHostFree(c->h_flag);
     if (c->h_out) (void)hipHostFree(c->h_out);

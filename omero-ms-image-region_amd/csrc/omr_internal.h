@@ -73,7 +73,8 @@ struct ChanParam {
     float alpha;        // alpha/255f (OMR_SEM_ALPHA_SEPARATE)
     float cratio[3];    // c/255f     (OMR_SEM_ALPHA_SEPARATE)
     float pad1;
-    uint64_t lut_off;   // byte offset of this channel's quantization LUT in the workspace
+    uint64_t lut_addr;  // device address of this channel's quantization byte LUT (kModeLut16;
+                        // the context's device LUT cache, Ctx::dev_luts)
     uint8_t qtab[256];  // kModeTable8: q of raw byte t, built on the host (host libm, exact)
     uint8_t lut_rgb[768];  // LutReader colours (valid when has_lut)
 };
@@ -132,6 +133,16 @@ struct Ctx {
     // chunks per lane of K2's float / 32-bit grid-stride modes (env OMR_K2_EVAL_CPT=2|4; 4
     // measured 6% slower on C5, DESIGN.md §K2, so 2 by default)
     int k2_eval_cpt = -2;            // float / 32-bit K2: -1 / -2 pipelined chunks per lane, 2 / 4 plain
+    // Device cache of the kModeLut16 byte LUTs (non-linear 16-bit families, noise reduction): a
+    // setting's LUT is built on the host once (host_quant_lut) and uploaded once, and every later
+    // request with that setting reads it in place (omr_render.hip device_quant_lut).  LRU, at most
+    // kDevLutEntries LUTs and kDevLutBytes in all.
+    struct DevLut { std::vector<uint8_t> key; uint8_t* d = nullptr; size_t bytes = 0; uint64_t used = 0; };
+    static constexpr int kDevLutEntries = 64;
+    static constexpr size_t kDevLutBytes = (size_t)256 << 20;
+    std::vector<DevLut> dev_luts;
+    size_t dev_lut_bytes = 0;
+    uint64_t dev_lut_clock = 0;
     // kernel timing (omr_ctx_enable_kernel_timing)
     bool timing = false;
     struct Timed { hipEvent_t start, stop; int kind; };

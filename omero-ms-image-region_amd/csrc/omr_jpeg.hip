@@ -999,7 +999,7 @@ struct PlaneSource {
                 v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
             } else {
                 const int xi = min(max(x, p.gmin), p.gmax);
-                v = F.R.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
+                v = reinterpret_cast<const uint8_t*>(p.lut_addr)[(uint32_t)(xi - p.gmin)];
             }
             return tab[v];
         }
@@ -2186,17 +2186,21 @@ static omr_status render_jpeg_one(Ctx* ctx, const omr_quantum_def* qdef, const o
                                   uint8_t* out, size_t cap, size_t* out_len) {
     if (!ctx) return OMR_INVALID_ARGUMENT;
     if (!d_planes || size_c <= 0) return fail(ctx, OMR_INVALID_ARGUMENT, "bad plane list");
-    if (W <= 0 || H <= 0 || W > kJpegBatchMaxDim || H > kJpegBatchMaxDim)
-        return fail(ctx, OMR_INVALID_ARGUMENT, "JPEG request: tile dimensions must be 1..4096");
+    omr_status st = check_jpeg_dims(ctx, W, H);
+    if (st) return st;
     OMR_HIP(ctx, hipSetDevice(ctx->device));
-    omr_status st = ensure_aux(ctx, (size_t)W * H * 4);
+    st = ensure_aux(ctx, (size_t)W * H * 4);
     if (st) return st;
     uint32_t* argb = static_cast<uint32_t*>(ctx->aux);
     omr_ctx* cx = static_cast<omr_ctx*>(ctx);
     st = omr_render_packed_int_device(cx, qdef, channels, size_c, d_planes, row_stride, pt, be, W, H, fh, fv, argb);
     if (st) return st;
     OMR_HIP(ctx, launch_flag_out(ctx->stream, ctx->d_flag, ctx->h_flag));   // read after the JPEG's sync
-    const omr_status jst = encode_jpeg_single_batched(ctx, argb, W, H, quality, out, cap, out_len, 0);
+    // regions past 4096 a side (region mode is unbounded, ImageRegionRequestHandler.java:817-827):
+    // the whole-image J1-J6 encoder, as omr_encode_jpeg_device does
+    const omr_status jst = W <= kJpegBatchMaxDim && H <= kJpegBatchMaxDim
+                               ? encode_jpeg_single_batched(ctx, argb, W, H, quality, out, cap, out_len, 0)
+                               : omr_encode_jpeg_device(cx, argb, W, H, quality, out, cap, out_len);
     OMR_HIP(ctx, hipStreamSynchronize(ctx->stream));     // (already idle unless the encode failed early)
     if (*static_cast<volatile int32_t*>(ctx->h_flag))
         return fail(ctx, OMR_QUANTIZATION, "pixel value outside the quantization LUT domain");

@@ -18,7 +18,7 @@ struct K2Chan {
     int32_t second;     // the a1*v + cdStart rounding stage is not the identity
     int32_t wsi;        // integral window start (FusedRender::f32: x - wsi in int32)
     double ws, a0, a1;
-    uint64_t lut_off;   // workspace offset of the byte LUT (kModeLut16)
+    uint64_t lut_addr;  // device address of the byte LUT (kModeLut16; the context's LUT cache)
 };
 
 
@@ -119,7 +119,6 @@ struct FusedRender {
     K2Chan ch[kFusedMaxActive];
     const uint32_t* contrib;     // [n_active][256] (workspace; built by K1 unless the kernel builds it)
     const RenderPlan* plan;      // the staged plan (kernels that build the tables themselves)
-    const uint8_t* ws_base;      // workspace base (kModeLut16 byte LUTs)
     int32_t* flag;               // sticky quantization-error word
     int32_t n_active, mode, cd_start, cds8, cde8, is_signed;
     int32_t any_check;           // some channel's LUT domain is narrower than its pixel type

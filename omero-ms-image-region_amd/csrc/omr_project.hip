@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(kBlock) k_project_render(K3RArgs A) {
                     v = linear16(x, k, A.R.cd_start, A.R.cds8, A.R.cde8);
                 } else {
                     const int xi = min(max(x, k.gmin), k.gmax);
-                    v = A.R.ws_base[k.lut_off + (uint32_t)(xi - k.gmin)];
+                    v = reinterpret_cast<const uint8_t*>(k.lut_addr)[(uint32_t)(xi - k.gmin)];
                 }
                 e = tab[v];
             }

@@ -79,7 +79,6 @@ struct K2Args {
     const uint8_t* sbase;       // strided batches: plane(t, c) = sbase + t*tile_stride + c*chan_stride
     int64_t tile_stride, chan_stride;
     int32_t strided;
-    const uint8_t* ws_base;     // workspace base (quantization LUTs)
     const uint32_t* contrib;    // [n_active][256]
     const uint32_t* thresh;     // [n_active][256] kModeThresh code thresholds (K1)
     const uint32_t* buckets;    // [n_active][bk_n] kModeThresh key buckets (K1)
@@ -428,7 +427,7 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
                     v = linear16(x, p, cds, cds8, cde8);
                 } else {
                     const int xi = min(max(x, p.gmin), p.gmax);
-                    v = A.ws_base[p.lut_off + (uint32_t)(xi - p.gmin)];
+                    v = reinterpret_cast<const uint8_t*>(p.lut_addr)[(uint32_t)(xi - p.gmin)];
                 }
                 e = tab[v];
             } else if constexpr (MODE == kK2Eval) {
@@ -620,9 +619,7 @@ static inline bool k2_small_launch(uint64_t total_chunks, int cu_count) {
 struct PreparedPlan {
     RenderPlan plan;
     size_t plan_bytes = 0;
-    int n_lut = 0;
-    size_t lut_bytes = 0;
-    std::vector<uint8_t> lut_host;   // the kModeLut16 byte LUTs (lut_bytes), built on the host
+    int n_lut = 0;                   // kModeLut16 channels (their LUTs: the context's device cache)
 };
 
 static double host_family_map(const ChanParam& p, double x) { return family_map_code(p.family, x, p.k, p.ws, p.we); }
@@ -806,17 +803,24 @@ static void host_quant_lut_compute(const ChanParam& p, int cds, int cde, bool mo
     }
 }
 
-static void host_quant_lut(const ChanParam& p, int cds, int cde, bool mono, uint8_t* out) {
-    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
-    struct Key {
-        int32_t cds, cde, family, nr, gmin, gmax, lo, hi, second, mono;
-        double ws, we, k, ys, a0, a1, dec;
-    };
-    Key key;
+// Everything a kModeLut16 byte LUT depends on (host and device LUT caches).
+struct QuantLutKey {
+    int32_t cds, cde, family, nr, gmin, gmax, lo, hi, second, mono;
+    double ws, we, k, ys, a0, a1, dec;
+};
+static QuantLutKey quant_lut_key(const ChanParam& p, int cds, int cde, bool mono) {
+    QuantLutKey key;
     std::memset(&key, 0, sizeof(key));
     key.cds = cds; key.cde = cde; key.family = p.family; key.nr = p.nr; key.gmin = p.gmin; key.gmax = p.gmax;
     key.lo = p.lo; key.hi = p.hi; key.second = p.second; key.mono = mono;
     key.ws = p.ws; key.we = p.we; key.k = p.k; key.ys = p.ys; key.a0 = p.a0; key.a1 = p.a1; key.dec = p.dec;
+    return key;
+}
+
+static void host_quant_lut(const ChanParam& p, int cds, int cde, bool mono, uint8_t* out) {
+    const int64_t n = (int64_t)p.gmax - p.gmin + 1;
+    using Key = QuantLutKey;
+    const Key key = quant_lut_key(p, cds, cde, mono);
     struct Entry { Key k; std::vector<uint8_t> lut; };
     static std::mutex mu;
     static std::vector<Entry> cache;                 // most recent last
@@ -870,6 +874,52 @@ static void host_thresholds(const ChanParam& p, int32_t pt, int cds, int cde, ui
     cache.push_back(e);
 }
 
+// The device copy of a channel's kModeLut16 byte LUT, from the context's LRU cache (Ctx::dev_luts).
+// A miss builds the LUT on the host (host_quant_lut) and uploads it once; a hit costs a key compare:
+// no host evaluation, no PCIe traffic and no pinned-slot growth per request.
+static omr_status device_quant_lut(Ctx* ctx, const ChanParam& p, int cds, int cde, bool mono, uint64_t* addr) {
+    const QuantLutKey key = quant_lut_key(p, cds, cde, mono);
+    const uint8_t* kb = reinterpret_cast<const uint8_t*>(&key);
+    const size_t n = (size_t)((int64_t)p.gmax - p.gmin + 1);
+    for (auto& e : ctx->dev_luts)
+        if (e.bytes == n && std::memcmp(e.key.data(), kb, sizeof(key)) == 0) {
+            e.used = ++ctx->dev_lut_clock;
+            *addr = reinterpret_cast<uint64_t>(e.d);
+            return OMR_OK;
+        }
+    // evict least recently used entries past the count / byte budget; queued kernels of this
+    // context's stream may still read them, so the stream drains first (misses only)
+    bool drained = false;
+    while (!ctx->dev_luts.empty() && ((int)ctx->dev_luts.size() >= Ctx::kDevLutEntries ||
+                                      ctx->dev_lut_bytes + n > Ctx::kDevLutBytes)) {
+        if (!drained) { OMR_HIP(ctx, hipStreamSynchronize(ctx->stream)); drained = true; }
+        auto lru = std::min_element(ctx->dev_luts.begin(), ctx->dev_luts.end(),
+                                    [](const Ctx::DevLut& a, const Ctx::DevLut& b) { return a.used < b.used; });
+        OMR_HIP(ctx, hipFree(lru->d));
+        ctx->dev_lut_bytes -= lru->bytes;
+        ctx->dev_luts.erase(lru);
+    }
+    std::vector<uint8_t> host(n);
+    host_quant_lut(p, cds, cde, mono, host.data());
+    Ctx::DevLut e;
+    e.key.assign(kb, kb + sizeof(key));
+    e.bytes = n;
+    void* d = nullptr;
+    if (hipMalloc(&d, n) != hipSuccess) return fail(ctx, OMR_OOM, "device LUT allocation failed");
+    e.d = static_cast<uint8_t*>(d);
+    hipError_t er = hipMemcpyAsync(e.d, host.data(), n, hipMemcpyHostToDevice, ctx->stream);
+    if (er == hipSuccess) er = hipStreamSynchronize(ctx->stream);     // `host` is freed on return
+    if (er != hipSuccess) {
+        (void)hipFree(e.d);
+        return hip_fail(ctx, er, "device LUT upload");
+    }
+    e.used = ++ctx->dev_lut_clock;
+    ctx->dev_lut_bytes += n;
+    ctx->dev_luts.push_back(std::move(e));
+    *addr = reinterpret_cast<uint64_t>(ctx->dev_luts.back().d);
+    return OMR_OK;
+}
+
 static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_channel_binding* ch,
                                int32_t size_c, int32_t pixel_type, PreparedPlan& pp) {
     if (!q) return fail(ctx, OMR_INVALID_ARGUMENT, "null quantum def");
@@ -888,7 +938,7 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
     P.greyscale = q->model == OMR_MODEL_GREYSCALE;
     P.sem = ctx->sem;
     int na = 0;
-    size_t lut_off = 0;
+    pp.n_lut = 0;
     for (int c = 0; c < size_c; ++c) {
         if (!ch[c].active) continue;
         if (P.greyscale && na == 1) break;   // GreyScaleStrategy renders the first active channel (S8)
@@ -954,8 +1004,6 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
                 if (p.mode == kModeLut16) {
                     const int64_t n = (int64_t)p.gmax - p.gmin + 1;
                     if (n > (1 << 24)) return fail(ctx, OMR_INVALID_ARGUMENT, "LUT domain too large");
-                    p.lut_off = lut_off;
-                    lut_off += align_up((size_t)n, 256);
                     pp.n_lut++;
                 }
             }
@@ -971,32 +1019,32 @@ static omr_status prepare_plan(Ctx* ctx, const omr_quantum_def* q, const omr_cha
         for (int i = 0; i < na; ++i)
             if (P.ch[i].mode == kModeThresh) P.ch[i].mode = kModeEval;
     pp.plan_bytes = offsetof(RenderPlan, ch) + sizeof(ChanParam) * (size_t)(na > 0 ? na : 1);
-    pp.lut_bytes = lut_off;
-    pp.lut_host.clear();
     if (pp.n_lut > 0) {
-        pp.lut_host.assign(lut_off, 0);
         const bool int_bounds = (P.sem & OMR_SEM_WINDOW_INT_BOUNDS) != 0;   // x in [(int)ws, ws): may wrap
+        OMR_HIP(ctx, hipSetDevice(ctx->device));
         for (int i = 0; i < na; ++i)
-            if (P.ch[i].mode == kModeLut16)
-                host_quant_lut(P.ch[i], q->cd_start, q->cd_end, !int_bounds && monotone_q(P.ch[i], *q),
-                               pp.lut_host.data() + P.ch[i].lut_off);
+            if (P.ch[i].mode == kModeLut16) {
+                const omr_status st = device_quant_lut(ctx, P.ch[i], q->cd_start, q->cd_end,
+                                                       !int_bounds && monotone_q(P.ch[i], *q), &P.ch[i].lut_addr);
+                if (st) return st;
+            }
     }
     return OMR_OK;
 }
 
-// Workspace layout for one render launch: [plan][contrib][luts][extra...]
+// Workspace layout for one render launch: [plan][contrib][thresholds][buckets][extra...] (the
+// byte LUTs live in the context's device LUT cache)
 struct RenderLayout {
-    size_t plan_off = 0, contrib_off = 0, thresh_off = 0, bucket_off = 0, lut_off = 0, extra_off = 0, total = 0;
+    size_t plan_off = 0, contrib_off = 0, thresh_off = 0, bucket_off = 0, extra_off = 0, total = 0;
 };
 
-static RenderLayout layout_for(const PreparedPlan& pp, size_t extra) {
+static RenderLayout layout_for(const PreparedPlan&, size_t extra) {
     RenderLayout L;
     L.plan_off = 0;
     L.contrib_off = align_up(sizeof(RenderPlan), 256);
     L.thresh_off = L.contrib_off + align_up((size_t)kMaxActive * 256 * 4, 256);
     L.bucket_off = L.thresh_off + align_up((size_t)kMaxActive * 256 * 4, 256);
-    L.lut_off = L.bucket_off + align_up((size_t)kMaxActive * (kBuckets * 4 + sizeof(BucketMap)), 256);
-    L.extra_off = L.lut_off + align_up(pp.lut_bytes, 256);
+    L.extra_off = L.bucket_off + align_up((size_t)kMaxActive * (kBuckets * 4 + sizeof(BucketMap)), 256);
     L.total = L.extra_off + extra;
     return L;
 }
@@ -1222,7 +1270,6 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
     uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
-    uint8_t* d_luts = ws + L.lut_off;
     const int na = pp.plan.n_active;
     bool use_thresh = false;
     for (int i = 0; i < na; ++i) use_thresh |= pp.plan.ch[i].mode == kModeThresh;
@@ -1236,13 +1283,10 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
                 host_thresholds(pp.plan.ch[i], pixel_type, pp.plan.cd_start, pp.plan.cd_end, thr.data() + 256 * i);
     }
     const bool thr_with_plan = use_thresh && !(ptr_src && ptr_bytes);   // one staging launch for both
-    // LUT offsets are relative to the LUT region; make them workspace-relative for K2.
-    for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off += L.lut_off;
     omr_status st = thr_with_plan
                         ? stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, d_thresh, thr.data(), thr.size() * 4)
                         : stage_h2d2(ctx, d_plan, &pp.plan, pp.plan_bytes, const_cast<const void**>(d_plane_ptrs),
                                      ptr_src, ptr_src ? ptr_bytes : 0);
-    for (int a = 0; a < pp.plan.n_active; ++a) pp.plan.ch[a].lut_off -= L.lut_off;
     if (st != OMR_OK) return st;
     if (use_thresh && !thr_with_plan && (st = stage_h2d(ctx, d_thresh, thr.data(), thr.size() * 4))) return st;
     const int bpp = bytes_per_pixel(pixel_type);
@@ -1260,14 +1304,12 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
                                pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
             OMR_HIP(ctx, hipGetLastError());
         }
-        if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     }
     if (use_thresh) {
         hipLaunchKernelGGL(k_build_buckets, dim3(k2_launch_buckets(na) / 256, na), dim3(256), 0,
                            ctx->stream, d_plan, d_thresh, d_buckets, k2_launch_buckets(na));
         OMR_HIP(ctx, hipGetLastError());
     }
-    (void)d_luts;
     if (total == 0) return OMR_OK;
     if (total >= (1ull << 31)) return fail(ctx, OMR_INVALID_ARGUMENT, "batch too large for one launch");
     K2Args a;
@@ -1280,7 +1322,6 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         a.tile_stride = strided->tile_stride;
         a.chan_stride = strided->chan_stride;
     }
-    a.ws_base = ws;
     a.contrib = d_contrib;
     a.thresh = d_thresh;
     a.buckets = d_buckets;
@@ -1328,7 +1369,7 @@ static omr_status enqueue_render(Ctx* ctx, PreparedPlan& pp, int32_t pixel_type,
         k.ws = c.ws;
         k.a0 = c.a0;
         k.a1 = c.a1;
-        k.lut_off = c.lut_off + L.lut_off;
+        k.lut_addr = c.lut_addr;
         if (c.mode != kModeLinear16) all_linear = false;
         if (!(c.mode == kModeLinear16 && fast_linear_ok(c, pp.plan))) all_fast = false;
     }
@@ -1414,7 +1455,6 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
     RenderPlan* d_plan = reinterpret_cast<RenderPlan*>(ws + L.plan_off);
     uint32_t* d_contrib = reinterpret_cast<uint32_t*>(ws + L.contrib_off);
     const int na = pp.plan.n_active;
-    for (int a = 0; a < na; ++a) pp.plan.ch[a].lut_off += ws_off + L.lut_off;   // relative to ctx->ws
     omr_status st = stage_h2d(ctx, d_plan, &pp.plan, pp.plan_bytes);
     if (st) return st;
     if (build_contrib) {
@@ -1422,7 +1462,6 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
                            fp->pixel_type == OMR_PIXELS_INT8 ? 1 : 0);
         OMR_HIP(ctx, hipGetLastError());
     }
-    if (pp.n_lut > 0 && (st = stage_h2d(ctx, ws + L.lut_off, pp.lut_host.data(), pp.lut_bytes))) return st;
     std::memset(&F, 0, sizeof(F));
     double tlo, thi;
     type_bounds(fp->pixel_type, tlo, thi);
@@ -1459,7 +1498,7 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
         k.wsi = wint ? (int32_t)k.ws : 0;
         k.a0 = c.a0;
         k.a1 = c.a1;
-        k.lut_off = c.lut_off;
+        k.lut_addr = c.lut_addr;
     }
     // The fused JPEG kernel (bias_int16), Fast16 with integral window starts: the f32 form where
     // it is proven exact for every pixel value (16-bit pixels: x in [0, 65535] after the bias)
@@ -1471,7 +1510,6 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
     }
     F.contrib = d_contrib;
     F.plan = d_plan;
-    F.ws_base = static_cast<const uint8_t*>(ctx->ws);
     F.flag = ctx->d_flag;
     F.n_active = na;
     F.mode = fp->mode;
