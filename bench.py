@@ -548,6 +548,7 @@ def _timed(torch, ctx, step, steps, warmup):
 
 
 C3_WINDOWS, C3_WINDOW_S = 7, 0.05
+SERVING_PASSES = 3     # timed passes of each serving leg (median): one pass is ~20-60 ms of requests
 C3_SETS = 4            # distinct C3 request stack sets (96 MiB each) taken in turn
 
 
@@ -934,13 +935,15 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
     reqs = [(0, 0, (i % grid) * TILE, ((i // grid) % grid) * TILE) for i in range(n_req)]
     dev = torch.empty((TILE, TILE), dtype=torch.int32, device="cuda")
     lat = []
-    t0 = time.perf_counter()
-    for r in reqs[:64]:
-        a = time.perf_counter()
-        ctx.render_pixel_buffer_tiles(qd, chans, pb, [r], TILE, TILE, out=dev, bindings=binds)
-        ctx.encode_jpeg_device(dev, TILE, TILE, 0.9)
-        lat.append(time.perf_counter() - a)
-    el = time.perf_counter() - t0
+    for warm in (True, False):       # a warm-up pass first (staging buffers, page cache, clocks)
+        lat.clear()
+        t0 = time.perf_counter()
+        for r in reqs[:64]:
+            a = time.perf_counter()
+            ctx.render_pixel_buffer_tiles(qd, chans, pb, [r], TILE, TILE, out=dev, bindings=binds)
+            ctx.encode_jpeg_device(dev, TILE, TILE, 0.9)
+            lat.append(time.perf_counter() - a)
+        el = time.perf_counter() - t0
     res = {"requests": n_req, "clients": clients,
            "one_at_a_time": {"tiles_per_s": round(64 / el, 1), "p50_ms": round(1e3 * float(np.median(lat)), 3)}}
     res["interactive"] = serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, res["one_at_a_time"])
@@ -962,15 +965,19 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
                     for t in ts:
                         b.wait(t)
                         lats.append(time.perf_counter() - a)
-            for warm in (True, False):
-                lats.clear()
+            els = []
+            for p in range(1 + SERVING_PASSES):    # a warm-up pass, then timed passes (median)
+                if p == 1:
+                    lats.clear()
                 ths = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
                 t0 = time.perf_counter()
                 for t in ths:
                     t.start()
                 for t in ths:
                     t.join()
-                el = time.perf_counter() - t0
+                if p:
+                    els.append(time.perf_counter() - t0)
+            el = float(np.median(els))
             st = b.stats()
         if isinstance(st, list):
             leg = {"devices": list(pool_devices), "jobs_per_device": [s["jobs"] for s in st],
@@ -980,14 +987,14 @@ def serving_section(torch, ctx, pb, qd, chans, binds, grid, n_req=256, clients=8
             leg = {"rendered": st["rendered"], "dedup": st["dedup"], "rounds": st["batches"]}
         # stats cover the warm-up pass too: rendered / dedup per served request, and the rate of
         # distinct renders (what the GPU did) apart from requests answered by a sibling's render
-        passes = 2
+        passes = 1 + SERVING_PASSES
         leg["rendered_per_s"] = round(leg["rendered"] / passes / el, 1)
         leg["dedup_share"] = round(leg["dedup"] / max(1, leg["rendered"] + leg["dedup"]), 3)
         res[name] = {"tiles_per_s": round(n_req / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3), **leg}
     return res
 
 
-def serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, single, per_client=8):
+def serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, single, per_client=32, passes=3):
     """The same tiles with ONE request in flight per client (a viewer asking for the next tile only
     when the last has arrived): `clients` threads each on its own context rendering its requests
     directly (the reference's shape: every worker renders its own request) against the batcher
@@ -1012,17 +1019,21 @@ def serving_interactive(torch, ctx, pb, qd, chans, binds, reqs, clients, single,
                 a = time.perf_counter()
                 job(k, r)
                 lats.append(time.perf_counter() - a)
-        for warm in (True, False):
-            lats.clear()
+        rates = []
+        for p in range(passes + 1):        # a warm-up pass, then `passes` timed ones (median rate)
+            if p == 1:
+                lats.clear()
             ths = [threading.Thread(target=client, args=(k,)) for k in range(clients)]
             t0 = time.perf_counter()
             for t in ths:
                 t.start()
             for t in ths:
                 t.join()
-            el = time.perf_counter() - t0
-        return {"tiles_per_s": round(clients * per_client / el, 1), "p50_ms": round(1e3 * float(np.median(lats)), 3),
-                "p90_ms": round(1e3 * float(np.percentile(lats, 90)), 3)}
+            if p:
+                rates.append(clients * per_client / (time.perf_counter() - t0))
+        return {"tiles_per_s": round(float(np.median(rates)), 1), "p50_ms": round(1e3 * float(np.median(lats)), 3),
+                "p90_ms": round(1e3 * float(np.percentile(lats, 90)), 3), "passes": passes,
+                "requests_per_pass": clients * per_client}
 
     def direct(k, r):
         ctxs[k].render_pixel_buffer_tiles(qd, chans, pb, [r], TILE, TILE, out=devs[k], bindings=binds)

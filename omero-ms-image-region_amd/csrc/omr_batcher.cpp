@@ -10,6 +10,15 @@
 // pixel-buffer call (omr_render_pixel_buffer_tiles, device output) and one batched JPEG encode,
 // and hands every job its own file.  Identical requests in flight together (the same cache key)
 // are rendered once.
+//
+// Dispatch lanes (round 6): a batcher runs `lanes` dispatcher threads (default 2, env
+// OMR_BATCH_LANES), each with its own context (stream, pixel-buffer staging, device buffers).  A
+// round is synchronous on its lane -- tile upload, render, encode, readback -- so with one lane the
+// PCIe link idled while a round rendered, encoded and read back, and clients with one request in
+// flight split into two alternating halves that waited for each other.  With two lanes the next
+// round's upload runs beside the current round's render and encode.  Only lane 0 takes projection
+// jobs (it owns the HBM stack cache).  When no lane is busy the device is idle and a gather closes
+// after a short grace (kIdleGapUs) instead of the full arrival pause.
 #include "omr_internal.h"
 
 #include <atomic>
@@ -52,33 +61,57 @@ struct Result {
 
 }  // namespace omr
 
-struct omr_batcher {
-    int device = 0;
-    int max_batch = 64;
-    int max_wait_us = 500;
-    int gap_us = 200;                        // arrival pause that closes a gather (<= max_wait_us)
-    int last_round = 0;                      // jobs the previous round took
-    std::chrono::steady_clock::time_point t_round_end{};
-    std::chrono::steady_clock::time_point t_last_submit{};
+namespace omr {
+// One dispatcher thread with its own context and device buffers.
+struct Lane {
+    int index = 0;
     omr_ctx* ctx = nullptr;
     std::thread th;
-    std::mutex m;
-    std::condition_variable cv_in, cv_out;
-    std::vector<std::unique_ptr<omr::Job>> pending;
-    std::unordered_map<uint64_t, omr::Result> done;
-    uint64_t next_ticket = 1;
-    bool stop = false;
-    uint64_t n_jobs = 0, n_batches = 0, n_rendered = 0, n_dedup = 0;
-    uint32_t sem = 0;                        // OMR_SEM_* copied into every job at submit (under m)
-    std::atomic<int64_t> outstanding{0};     // jobs submitted and not yet completed (pool dispatch)
-    // device buffers of the dispatcher (grown on demand)
+    int last_round = 0;                      // jobs this lane's previous round took
+    std::chrono::steady_clock::time_point t_round_end{};
+    bool busy = false;                       // a round is in progress (under omr_batcher::m)
+    // device buffers of the lane (grown on demand)
     uint32_t* d_argb = nullptr;
     size_t argb_cap = 0;
     uint8_t* d_jpeg = nullptr;                   // encoded files of a group (JPEG / PNG batch output)
     size_t jpeg_cap = 0;
     uint8_t* d_stack = nullptr;                  // projection jobs: scratch for stacks the cache cannot hold
     size_t stack_cap = 0;
-    // HBM stack cache (projection jobs): (pixel buffer, c, t) Z-stacks kept resident, LRU, up to
+    uint64_t* d_offs = nullptr;
+    uint32_t* d_lens = nullptr;
+    int32_t* d_stat = nullptr;
+    int32_t* d_rstat = nullptr;    // per-tile render status (QuantizationException per tile)
+    int meta_cap = 0;
+};
+constexpr int kIdleGapUs = 30;   // gather grace when no lane is busy (simultaneous submits still meet)
+}  // namespace omr
+
+struct omr_batcher {
+    int device = 0;
+    int max_batch = 64;
+    int max_wait_us = 500;
+    int gap_us = 200;                        // arrival pause that closes a gather (<= max_wait_us)
+    // the same for lanes > 0 (env OMR_BATCH_LANE_GAP_US): an overlap lane gathers what arrived while
+    // the lane below was busy, so a short pause closes it (30 us: the interactive serving leg's
+    // best of 30 / 200 us, tools/serving_ab.py)
+    int lane_gap_us = 30;
+    std::chrono::steady_clock::time_point t_last_submit{};
+    omr_ctx* ctx = nullptr;                  // lane 0's context (set_semantics and errors of the batcher)
+    std::vector<std::unique_ptr<omr::Lane>> lanes;
+    int busy_lanes = 0;                      // under m
+    std::mutex m;
+    std::condition_variable cv_in, cv_out;
+    std::vector<std::unique_ptr<omr::Job>> pending;
+    std::unordered_map<uint64_t, omr::Result> done;
+    // cross-lane dedup: the cache key of every job a lane is rendering -> the tickets of identical
+    // jobs another lane took meanwhile (answered with the same bytes when the render completes)
+    std::unordered_map<std::string, std::vector<uint64_t>> inflight;
+    uint64_t next_ticket = 1;
+    bool stop = false;
+    uint64_t n_jobs = 0, n_batches = 0, n_rendered = 0, n_dedup = 0;
+    uint32_t sem = 0;                        // OMR_SEM_* copied into every job at submit (under m)
+    std::atomic<int64_t> outstanding{0};     // jobs submitted and not yet completed (pool dispatch)
+    // HBM stack cache (lane 0 only) (projection jobs): (pixel buffer, c, t) Z-stacks kept resident, LRU, up to
     // stack_cache_max bytes, so repeated p= requests on one image (other settings, ranges, flips)
     // skip the PCIe upload the reference repeats per request (ImageRegionRequestHandler.java:516-533)
     struct StackEntry { uint64_t serial; int32_t c, t; size_t bytes; uint8_t* d; uint64_t used; };
@@ -86,11 +119,6 @@ struct omr_batcher {
     std::atomic<int64_t> stack_cache_max{(int64_t)4 << 30};
     std::atomic<uint64_t> stack_hits{0}, stack_misses{0}, stack_resident{0};
     uint64_t stack_tick = 0;
-    uint64_t* d_offs = nullptr;
-    uint32_t* d_lens = nullptr;
-    int32_t* d_stat = nullptr;
-    int32_t* d_rstat = nullptr;    // per-tile render status (QuantizationException per tile)
-    int meta_cap = 0;
 };
 
 namespace omr {
@@ -150,7 +178,7 @@ static omr_status regrow(omr_ctx* c, T*& p, size_t bytes) {
     return OMR_OK;
 }
 
-static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
+static omr_status grow_dev(Lane* B, size_t argb, size_t jpeg, int n) {
     omr_ctx* c = B->ctx;
     omr_status st;
     if (argb > B->argb_cap) {
@@ -177,11 +205,21 @@ static omr_status grow_dev(omr_batcher* B, size_t argb, size_t jpeg, int n) {
 // entries that already carry an error): JPEG and PNG in one batched launch each (sides up to
 // 4096; larger planes, e.g. a projected full plane, one at a time), TIFF by the host writer, ARGB
 // as the packed int[] itself.
-static omr_status encode_group(omr_batcher* B, int n, int W, int H, int format, float quality,
-                               std::vector<Result>& out) {
+// d_rstat (optional): the render's per-tile status on the device, read back with the encoder's
+// lengths (one stream sync per round) and applied to out first.
+static omr_status encode_group(Lane* B, int n, int W, int H, int format, float quality,
+                               std::vector<Result>& out, const int32_t* d_rstat = nullptr) {
     omr_ctx* c = B->ctx;
     const size_t px = (size_t)W * H;
     const bool batched = W <= 4096 && H <= 4096;
+    std::vector<int32_t> rstat(d_rstat ? n : 0);
+    auto apply_rstat = [&]() {
+        for (int i = 0; i < (int)rstat.size(); ++i)
+            if (rstat[i] && !out[i].st) {
+                out[i].st = rstat[i];
+                out[i].err = "pixel value outside the quantization LUT domain";
+            }
+    };
     if ((format == OMR_FORMAT_JPEG || format == OMR_FORMAT_PNG) && batched) {
         const size_t cap = format == OMR_FORMAT_JPEG ? (size_t)n * (px * 4 + 65536)
                                                      : omr_png_batch_max_bytes(W, H, 3, n);
@@ -197,17 +235,25 @@ static omr_status encode_group(omr_batcher* B, int n, int W, int H, int format, 
         std::vector<uint32_t> lens(n);
         OMR_HIP(c, hipMemcpyAsync(offs.data(), B->d_offs, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
         OMR_HIP(c, hipMemcpyAsync(lens.data(), B->d_lens, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        if (d_rstat) OMR_HIP(c, hipMemcpyAsync(rstat.data(), d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
         OMR_HIP(c, hipStreamSynchronize(c->stream));
+        apply_rstat();
         uint64_t used = 0;
         for (int i = 0; i < n; ++i) {
             if (!lens[i]) return fail(c, OMR_INTERNAL, "encode batch buffer too small");
             used = std::max<uint64_t>(used, offs[i] + lens[i]);
         }
         std::vector<uint8_t> all(used);
-        OMR_HIP(c, hipMemcpy(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost));
+        OMR_HIP(c, hipMemcpyAsync(all.data(), B->d_jpeg, used, hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
         for (int i = 0; i < n; ++i)
             if (!out[i].st) out[i].bytes.assign(all.begin() + offs[i], all.begin() + offs[i] + lens[i]);
     } else if (format == OMR_FORMAT_JPEG || format == OMR_FORMAT_PNG || format == OMR_FORMAT_TIFF) {
+        if (d_rstat) {
+            OMR_HIP(c, hipMemcpyAsync(rstat.data(), d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+            OMR_HIP(c, hipStreamSynchronize(c->stream));
+            apply_rstat();
+        }
         const size_t cap = format == OMR_FORMAT_JPEG ? omr_jpeg_max_bytes(W, H)
                          : format == OMR_FORMAT_PNG  ? omr_png_max_bytes(W, H, 3)
                                                      : omr_tiff_max_bytes(W, H);   // TIFFImageWriter (:583-596)
@@ -223,8 +269,11 @@ static omr_status encode_group(omr_batcher* B, int n, int W, int H, int format, 
             out[i].bytes.assign(buf.begin(), buf.begin() + len);
         }
     } else {                                               // OMR_FORMAT_ARGB: the packed int[] itself
+        if (d_rstat) OMR_HIP(c, hipMemcpyAsync(rstat.data(), d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
         std::vector<uint8_t> all(px * 4 * n);
-        OMR_HIP(c, hipMemcpy(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost));
+        OMR_HIP(c, hipMemcpyAsync(all.data(), B->d_argb, all.size(), hipMemcpyDeviceToHost, c->stream));
+        OMR_HIP(c, hipStreamSynchronize(c->stream));
+        apply_rstat();
         for (int i = 0; i < n; ++i)
             if (!out[i].st) out[i].bytes.assign(all.begin() + px * 4 * i, all.begin() + px * 4 * (i + 1));
     }
@@ -235,7 +284,7 @@ static omr_status encode_group(omr_batcher* B, int n, int W, int H, int format, 
 // distinct tiles; out[u] receives each one's bytes, or OMR_QUANTIZATION for a tile with a pixel
 // outside the LUT domain — only that tile fails, as only that request's Renderer would throw
 // in the reference (one Renderer per request, ImageRegionRequestHandler.java:436-440, :479-480).
-static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
+static omr_status run_group(Lane* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
     omr_ctx* c = B->ctx;
     const Job& j0 = *jobs[0];
     c->sem = j0.sem;      // the group's semantics (every job of a group has the same), dispatcher thread only
@@ -267,15 +316,7 @@ static omr_status run_group(omr_batcher* B, const std::vector<Job*>& jobs, std::
                                    j0.spec.flip_h, j0.spec.flip_v, B->d_argb, 1, B->d_rstat);
     if (st) return st;
     std::vector<Result> sub(n);
-    std::vector<int32_t> rstat(n);
-    OMR_HIP(c, hipMemcpyAsync(rstat.data(), B->d_rstat, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
-    OMR_HIP(c, hipStreamSynchronize(c->stream));
-    for (int i = 0; i < n; ++i)
-        if (rstat[i]) {
-            sub[i].st = rstat[i];
-            sub[i].err = "pixel value outside the quantization LUT domain";
-        }
-    st = encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, sub);
+    st = encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, sub, B->d_rstat);
     if (st) return st;
     for (int i = 0; i < n; ++i) out[live[i]] = std::move(sub[i]);
     return OMR_OK;
@@ -348,8 +389,9 @@ static void stack_drop(omr_batcher* B, const uint8_t* d) {
 // ImageRegionRequestHandler.java:506-559), and the group's planes are encoded in one batch.
 // A request whose render fails (OMR_QUANTIZATION, the quirk-3 OMR_INTERNAL, a bad z range) fails
 // alone.
-static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
-    omr_ctx* c = B->ctx;
+static omr_status run_projection_group(omr_batcher* B, Lane* L, const std::vector<Job*>& jobs,
+                                       std::vector<Result>& out) {
+    omr_ctx* c = L->ctx;
     const Job& j0 = *jobs[0];
     c->sem = j0.sem;
     int32_t dims[6];
@@ -363,17 +405,17 @@ static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& 
         if (j0.ch[ch].active) act.push_back(ch);
     const size_t stack_bytes = align_up(px * (size_t)bytes_per_pixel(PT) * Z, 256);
     const uint64_t serial = pixel_buffer_serial(j0.pb);
-    omr_status st = grow_dev(B, px * 4 * n, 0, n);
+    omr_status st = grow_dev(L, px * 4 * n, 0, n);
     if (st) return st;
     const size_t scratch_bytes = stack_bytes * std::max<size_t>(1, act.size());
     auto scratch = [&](size_t a, uint8_t** d) -> omr_status {   // the uncached fallback, grown on first use
-        if (scratch_bytes > B->stack_cap) {
-            B->stack_cap = 0;
-            const omr_status s2 = regrow(c, B->d_stack, scratch_bytes);
+        if (scratch_bytes > L->stack_cap) {
+            L->stack_cap = 0;
+            const omr_status s2 = regrow(c, L->d_stack, scratch_bytes);
             if (s2) return s2;
-            B->stack_cap = scratch_bytes;
+            L->stack_cap = scratch_bytes;
         }
-        *d = B->d_stack + stack_bytes * a;
+        *d = L->d_stack + stack_bytes * a;
         return OMR_OK;
     };
     out.assign(n, Result{});
@@ -403,7 +445,7 @@ static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& 
         if (!st)
             st = omr_render_projected_device(c, &j0.qdef, j0.ch.data(), SC, stacks.data(), PT, 1, W, H, Z,
                                              j0.spec.projection, start, end, 1, j0.spec.flip_h, j0.spec.flip_v,
-                                             B->d_argb + px * i);
+                                             L->d_argb + px * i);
         if (!st) st = omr_ctx_synchronize(c);              // this request's QuantizationException, if any
         if (st) {
             if (st == OMR_DEVICE || st == OMR_OOM) return st;
@@ -412,11 +454,11 @@ static omr_status run_projection_group(omr_batcher* B, const std::vector<Job*>& 
             st = OMR_OK;
         }
     }
-    return encode_group(B, n, W, H, j0.spec.format, j0.spec.quality, out);
+    return encode_group(L, n, W, H, j0.spec.format, j0.spec.quality, out);
 }
 
 // Every mask job of a dispatch round with the same semantics: one omr_render_shape_mask_png_batch.
-static omr_status run_mask_group(omr_batcher* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
+static omr_status run_mask_group(Lane* B, const std::vector<Job*>& jobs, std::vector<Result>& out) {
     omr_ctx* c = B->ctx;
     c->sem = jobs[0]->sem;
     const int n = (int)jobs.size();
@@ -447,42 +489,121 @@ static omr_status run_mask_group(omr_batcher* B, const std::vector<Job*>& jobs, 
     return OMR_OK;
 }
 
-static void dispatch_loop(omr_batcher* B) {
+// The region / shape-mask cache key of a job within its group (ImageRegionCtx.java:165-177).
+static std::string tile_key(const Job& jb) {
+    const omr_tile_job& s = jb.spec;
+    std::string key;
+    if (jb.kind == kJobTile) {
+        const int32_t k4[4] = {s.z, s.t, s.x, s.y};
+        append(key, k4, sizeof(k4));
+    } else if (jb.kind == kJobProjection) {
+        append(key, &s.t, sizeof(s.t));
+    } else {
+        // the caller's byte count and null-ness too: an empty mask (padded to one zero byte) must
+        // not share the result of a real 1-byte zero mask
+        const int64_t nb = jb.mask.bits ? (int64_t)jb.mask.n_bytes : -1;
+        const int32_t m4[4] = {jb.mask.width, jb.mask.height, jb.mask.flip_h, jb.mask.flip_v};
+        append(key, m4, sizeof(m4));
+        append(key, &nb, sizeof(nb));
+        append(key, jb.mask.rgba, 4);
+        append(key, jb.mask_bits.data(), jb.mask_bits.size());
+    }
+    return key;
+}
+
+static void dispatch_loop(omr_batcher* B, Lane* L) {
     (void)hipSetDevice(B->device);
+    // lane 0 takes every kind; a higher lane takes tiles and masks, and gathers only while a lower
+    // lane is busy: a second lane exists to overlap a round's upload with another round's render
+    // and encode, not to split one burst into two smaller (and less deduplicated) rounds
+    auto eligible = [&](const Job& j) { return L->index == 0 || j.kind != kJobProjection; };
+    auto lower_busy = [&]() {
+        for (int i = 0; i < L->index; ++i)
+            if (B->lanes[i]->busy) return true;
+        return false;
+    };
+    auto n_eligible = [&]() {
+        int k = 0;
+        for (auto& j : B->pending) k += eligible(*j);
+        return k;
+    };
     std::unique_lock<std::mutex> lk(B->m);
     for (;;) {
-        B->cv_in.wait(lk, [&] { return B->stop || !B->pending.empty(); });
-        if (B->pending.empty() && B->stop) return;
+        B->cv_in.wait(lk, [&] { return B->stop || (n_eligible() > 0 && (L->index == 0 || lower_busy())); });
+        if (B->stop && n_eligible() == 0) return;
+        if (!B->stop && L->index > 0 && !lower_busy()) continue;
         // gather: up to max_batch jobs, what arrives within max_wait_us of the oldest one, or --
-        // whichever comes first -- until the arrivals pause for gap_us.  The device is idle while
-        // the dispatcher gathers, so a burst (a viewer's screenful, the clients answered by the last
-        // round) is taken as soon as it has landed instead of after the whole max_wait_us.  Right
-        // after a round, as many jobs as it took also close the gather: clients that wait for their
-        // answer before asking again come back together, and their round goes as soon as they are
-        // all in.  After an idle spell (longer than max_wait_us) only the arrival pause counts, so
-        // a fresh burst is still gathered whole (and its duplicates rendered once).
-        const bool follow = B->last_round > 0 &&
-                            B->pending.front()->t_submit - B->t_round_end < std::chrono::microseconds(B->max_wait_us);
+        // whichever comes first -- until the arrivals pause for gap_us.  A burst (a viewer's
+        // screenful, the clients answered by the last round) is taken as soon as it has landed
+        // instead of after the whole max_wait_us.  Right after a round, as many jobs as it took also
+        // close the gather: clients that wait for their answer before asking again come back
+        // together, and their round goes as soon as they are all in.  After an idle spell (longer
+        // than max_wait_us) only the pause counts, so a fresh burst is still gathered whole (and its
+        // duplicates rendered once).  With no lane busy the device is idle: the pause shrinks to
+        // kIdleGapUs, enough for submits made together to meet.
+        const Job* first = nullptr;
+        for (auto& j : B->pending)
+            if (eligible(*j)) { first = j.get(); break; }
+        const bool follow = L->last_round > 0 &&
+                            first->t_submit - L->t_round_end < std::chrono::microseconds(B->max_wait_us);
         for (;;) {
-            if (B->stop || (int)B->pending.size() >= B->max_batch) break;
-            if (follow && (int)B->pending.size() >= B->last_round) break;
+            const int ne = n_eligible();
+            if (B->stop || ne >= B->max_batch || ne == 0) break;
+            if (follow && ne >= L->last_round) break;
             const auto now = std::chrono::steady_clock::now();
-            const auto deadline =
-                std::min(B->pending.front()->t_submit + std::chrono::microseconds(B->max_wait_us),
-                         B->t_last_submit + std::chrono::microseconds(B->gap_us));
+            const int gap = B->busy_lanes == 0 ? std::min(B->gap_us, kIdleGapUs)
+                          : L->index > 0          ? B->lane_gap_us
+                                                  : B->gap_us;
+            const auto deadline = std::min(first->t_submit + std::chrono::microseconds(B->max_wait_us),
+                                           B->t_last_submit + std::chrono::microseconds(gap));
             if (now >= deadline) break;
             B->cv_in.wait_until(lk, deadline);
+            first = nullptr;                             // another lane may have taken the oldest job
+            for (auto& j : B->pending)
+                if (eligible(*j)) { first = j.get(); break; }
+            if (!first) break;
         }
         std::vector<std::unique_ptr<Job>> take;
-        const size_t nt = std::min(B->pending.size(), (size_t)B->max_batch);
-        B->last_round = (int)nt;
-        for (size_t i = 0; i < nt; ++i) take.push_back(std::move(B->pending[i]));
-        B->pending.erase(B->pending.begin(), B->pending.begin() + nt);
+        for (size_t i = 0; i < B->pending.size() && (int)take.size() < B->max_batch;) {
+            if (eligible(*B->pending[i])) {
+                take.push_back(std::move(B->pending[i]));
+                B->pending.erase(B->pending.begin() + (long)i);
+            } else {
+                ++i;
+            }
+        }
+        if (take.empty()) continue;
+        // cross-lane dedup: a job identical to one another lane is rendering waits for that render
+        std::vector<std::string> my_keys;
+        uint64_t followed = 0;
+        for (size_t i = 0; i < take.size();) {
+            std::string key = take[i]->group_key + '\x01' + tile_key(*take[i]);
+            auto it = B->inflight.find(key);
+            if (it != B->inflight.end() &&
+                std::find(my_keys.begin(), my_keys.end(), key) == my_keys.end()) {
+                it->second.push_back(take[i]->ticket);
+                take.erase(take.begin() + (long)i);
+                ++followed;
+                continue;
+            }
+            if (it == B->inflight.end()) {
+                B->inflight.emplace(key, std::vector<uint64_t>());
+                my_keys.push_back(std::move(key));
+            }
+            ++i;
+        }
+        B->n_dedup += followed;
+        if (take.empty()) continue;
+        L->last_round = (int)take.size();
+        L->busy = true;
+        B->busy_lanes++;
         lk.unlock();
+        if (L->index + 1 < (int)B->lanes.size()) B->cv_in.notify_all();   // the next lane may gather now
         // group by settings; dedupe identical tiles (the region cache key) inside each group
         std::map<std::string, std::vector<Job*>> groups;
         for (auto& j : take) groups[j->group_key].push_back(j.get());
         std::vector<std::pair<uint64_t, Result>> results;
+        std::vector<std::pair<std::string, size_t>> keyed;   // cache key of each rendered job -> its result
         uint64_t rendered = 0, dedup = 0;
         for (auto& g : groups) {
             std::vector<Job*> uniq;
@@ -490,24 +611,7 @@ static void dispatch_loop(omr_batcher* B) {
             std::map<std::string, int> seen;
             const int kind = g.second[0]->kind;
             for (size_t i = 0; i < g.second.size(); ++i) {
-                const Job& jb = *g.second[i];
-                const omr_tile_job& s = jb.spec;
-                std::string key;                       // the region / shape-mask cache key within the group
-                if (kind == kJobTile) {
-                    const int32_t k4[4] = {s.z, s.t, s.x, s.y};
-                    append(key, k4, sizeof(k4));
-                } else if (kind == kJobProjection) {
-                    append(key, &s.t, sizeof(s.t));
-                } else {
-                    // the caller's byte count and null-ness too: an empty mask (padded to one zero
-                    // byte) must not share the result of a real 1-byte zero mask
-                    const int64_t nb = jb.mask.bits ? (int64_t)jb.mask.n_bytes : -1;
-                    const int32_t m4[4] = {jb.mask.width, jb.mask.height, jb.mask.flip_h, jb.mask.flip_v};
-                    append(key, m4, sizeof(m4));
-                    append(key, &nb, sizeof(nb));
-                    append(key, jb.mask.rgba, 4);
-                    append(key, jb.mask_bits.data(), jb.mask_bits.size());
-                }
+                const std::string key = tile_key(*g.second[i]);
                 auto it = seen.find(key);
                 if (it == seen.end()) {
                     seen[key] = (int)uniq.size();
@@ -530,35 +634,70 @@ static void dispatch_loop(omr_batcher* B) {
                 const size_t per = (size_t)dims[0] * dims[1] * 8 + 65536;
                 chunk = std::max<size_t>(1, std::min(chunk, kProjectionBatchBytes / per));
             }
-            for (size_t b0 = 0; b0 < uniq.size() && st == OMR_OK; b0 += chunk) {
-                std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + std::min(uniq.size(), b0 + chunk));
+            // each sub-batch answers its own jobs: a failure in a later sub-batch (OOM, a device
+            // error) fails that sub-batch's jobs only, and the planes earlier ones rendered stand
+            std::vector<omr_status> part_st(uniq.size(), OMR_OK);
+            std::vector<std::string> part_err(uniq.size());
+            for (size_t b0 = 0; b0 < uniq.size(); b0 += chunk) {
+                const size_t b1 = std::min(uniq.size(), b0 + chunk);
+                std::vector<Job*> part(uniq.begin() + b0, uniq.begin() + b1);
                 std::vector<Result> po;
                 try {
-                    st = kind == kJobTile ? run_group(B, part, po)
-                       : kind == kJobProjection ? run_projection_group(B, part, po)
-                                                : run_mask_group(B, part, po);
-                } catch (const std::bad_alloc&) {     // host memory: this group fails, the server lives
-                    st = fail(B->ctx, OMR_OOM, "host allocation failed in the batcher");
+                    st = kind == kJobTile ? run_group(L, part, po)
+                       : kind == kJobProjection ? run_projection_group(B, L, part, po)
+                                                : run_mask_group(L, part, po);
+                } catch (const std::bad_alloc&) {     // host memory: this sub-batch fails, the server lives
+                    st = fail(L->ctx, OMR_OOM, "host allocation failed in the batcher");
                 } catch (const std::exception& e) {
-                    st = fail(B->ctx, OMR_INTERNAL, std::string("batcher: ") + e.what());
+                    st = fail(L->ctx, OMR_INTERNAL, std::string("batcher: ") + e.what());
                 }
-                for (auto& r : po) out.push_back(std::move(r));
+                po.resize(part.size());
+                for (size_t k = 0; k < part.size(); ++k) {
+                    if (st) {
+                        part_st[b0 + k] = st;
+                        part_err[b0 + k] = L->ctx->last_error;
+                    }
+                    out.push_back(std::move(po[k]));
+                }
+                if (st == OMR_DEVICE) {               // a device error poisons the context: stop here
+                    for (size_t k = b1; k < uniq.size(); ++k) {
+                        part_st[k] = st;
+                        part_err[k] = L->ctx->last_error;
+                        out.emplace_back();
+                    }
+                    break;
+                }
             }
             rendered += uniq.size();
-            const std::string err = st ? B->ctx->last_error : std::string();
             for (size_t i = 0; i < g.second.size(); ++i) {
                 Result r;
-                if (st) { r.st = st; r.err = err; }
-                else if (out[slot[i]].st) { r.st = out[slot[i]].st; r.err = out[slot[i]].err; }
-                else r.bytes = out[slot[i]].bytes;
+                const int u = slot[i];
+                if (part_st[u]) { r.st = part_st[u]; r.err = part_err[u]; }
+                else if (out[u].st) { r.st = out[u].st; r.err = out[u].err; }
+                else r.bytes = out[u].bytes;
                 results.emplace_back(g.second[i]->ticket, std::move(r));
+                if (std::find(uniq.begin(), uniq.end(), g.second[i]) != uniq.end())
+                    keyed.emplace_back(g.second[i]->group_key + '\x01' + tile_key(*g.second[i]), results.size() - 1);
             }
         }
         lk.lock();
+        size_t answered = results.size();
+        for (auto& kr : keyed) {                  // the other lanes' identical jobs, same answer
+            auto it = B->inflight.find(kr.first);
+            if (it == B->inflight.end()) continue;
+            for (uint64_t t : it->second) {
+                B->done[t] = results[kr.second].second;
+                ++answered;
+            }
+            B->inflight.erase(it);
+        }
+        for (const auto& k : my_keys) B->inflight.erase(k);   // (keys of jobs that failed before grouping)
         for (auto& r : results) B->done[r.first] = std::move(r.second);
-        B->outstanding -= (int64_t)results.size();
+        B->outstanding -= (int64_t)answered;
         B->n_batches += 1;
-        B->t_round_end = std::chrono::steady_clock::now();
+        L->t_round_end = std::chrono::steady_clock::now();
+        L->busy = false;
+        B->busy_lanes--;
         B->n_rendered += rendered;
         B->n_dedup += dedup;
         B->cv_out.notify_all();
@@ -578,15 +717,26 @@ omr_status omr_batcher_create(int32_t device, int32_t max_batch, int32_t max_wai
     B->device = device;
     B->max_batch = max_batch;
     B->max_wait_us = max_wait_us;
-    const omr_status st = omr_ctx_create(device, &B->ctx);
-    if (st) {
-        delete B;
-        return st;
+    int lanes = 2;
+    if (const char* v = std::getenv("OMR_BATCH_LANES")) lanes = std::max(1, std::min(8, std::atoi(v)));
+    for (int i = 0; i < lanes; ++i) {
+        auto L = std::make_unique<Lane>();
+        L->index = i;
+        const omr_status st = omr_ctx_create(device, &L->ctx);
+        if (st) {
+            for (auto& x : B->lanes) omr_ctx_destroy(x->ctx);
+            delete B;
+            return st;
+        }
+        B->lanes.push_back(std::move(L));
     }
+    B->ctx = B->lanes[0]->ctx;
     if (const char* v = std::getenv("OMR_STACK_CACHE_MB")) B->stack_cache_max = (int64_t)std::atoll(v) << 20;
     B->gap_us = std::min(max_wait_us, 200);
     if (const char* v = std::getenv("OMR_BATCH_GAP_US")) B->gap_us = std::max(0, std::min(max_wait_us, std::atoi(v)));
-    B->th = std::thread(dispatch_loop, B);
+    B->lane_gap_us = std::min(B->gap_us, 30);
+    if (const char* v = std::getenv("OMR_BATCH_LANE_GAP_US")) B->lane_gap_us = std::max(0, std::min(max_wait_us, std::atoi(v)));
+    for (auto& L : B->lanes) L->th = std::thread(dispatch_loop, B, L.get());
     *out = B;
     return OMR_OK;
 }
@@ -598,13 +748,16 @@ void omr_batcher_destroy(omr_batcher* B) {
         B->stop = true;
     }
     B->cv_in.notify_all();
-    if (B->th.joinable()) B->th.join();
+    for (auto& L : B->lanes)
+        if (L->th.joinable()) L->th.join();
     (void)hipSetDevice(B->device);
     for (auto& e : B->stacks) (void)hipFree(e.d);
-    for (void* p : {(void*)B->d_argb, (void*)B->d_jpeg, (void*)B->d_offs, (void*)B->d_lens, (void*)B->d_stat,
-                    (void*)B->d_rstat, (void*)B->d_stack})
-        if (p) (void)hipFree(p);
-    omr_ctx_destroy(B->ctx);
+    for (auto& L : B->lanes) {
+        for (void* p : {(void*)L->d_argb, (void*)L->d_jpeg, (void*)L->d_offs, (void*)L->d_lens, (void*)L->d_stat,
+                        (void*)L->d_rstat, (void*)L->d_stack})
+            if (p) (void)hipFree(p);
+        omr_ctx_destroy(L->ctx);
+    }
     delete B;
 }
 
@@ -621,7 +774,7 @@ static void enqueue(omr_batcher* B, std::unique_ptr<Job> j, uint64_t* ticket) {
         B->n_jobs++;
         B->outstanding++;
     }
-    B->cv_in.notify_one();
+    B->cv_in.notify_all();     // every idle lane (lane 0 alone takes projection jobs)
 }
 
 omr_status omr_batcher_submit(omr_batcher* B, const omr_tile_job* job, uint64_t* ticket) {

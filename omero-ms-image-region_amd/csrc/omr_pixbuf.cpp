@@ -474,7 +474,9 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
     };
     for (int g = 0; g < ngroups; ++g) {
         const int s = g & 1, t0 = gstart[g], cnt = gstart[g + 1] - t0;
-        if (g >= 2) OMR_HIP(ctx, hipEventSynchronize(P->h2d[s]));   // pinned slot s is free again
+        // pinned slot s is free again (also across calls: a call with per-tile statuses returns
+        // without a final sync; an event never recorded completes at once)
+        OMR_HIP(ctx, hipEventSynchronize(P->h2d[s]));
         uint8_t* hin = static_cast<uint8_t*>(P->pin_in[s]);
         uint8_t* din = static_cast<uint8_t*>(P->d_in[s]);
         const void** tab = reinterpret_cast<const void**>(hin);
@@ -516,8 +518,8 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
             });
             if (io_error) return fail(ctx, OMR_INTERNAL, "pixel buffer read failed");
         }
-        if (g >= 2) OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free
-        if (g >= 2 && P->copy_b) OMR_HIP(ctx, hipStreamWaitEvent(P->copy_b, P->rend[s], 0));
+        OMR_HIP(ctx, hipStreamWaitEvent(P->copy, P->rend[s], 0));   // device slot s is free (this or a past call)
+        if (P->copy_b) OMR_HIP(ctx, hipStreamWaitEvent(P->copy_b, P->rend[s], 0));
         if (bands && !direct) {
             OMR_HIP(ctx, hipMemcpyAsync(din, hin, tab_bytes + band_bytes * gbands[g].size(), hipMemcpyHostToDevice,
                                         P->copy));
@@ -595,6 +597,12 @@ omr_status render_pixel_buffer_tiles(omr_ctx* ctx, const omr_pixel_buffer* pb, c
     if (host_out && !out_pinned) {
         st = finish_host(ngroups - 1);
         if (st) return st;
+    }
+    if (d_status && !host_out) {
+        // per-tile statuses carry the QuantizationException; the caller (the batcher) encodes on
+        // the same stream and syncs once after that.  The sticky flag is cleared behind the render.
+        OMR_HIP(ctx, launch_flag_out(ctx->stream, ctx->d_flag, ctx->h_flag));
+        return OMR_OK;
     }
     st = omr_ctx_synchronize(ctx);
     // with per-tile statuses the QuantizationException belongs to the flagged tiles only

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Batcher serving from a ROMIO file, for same-box A/B of the dispatcher count
-(OMR_BATCHER_WORKERS in this process's environment): 8 client threads, 8 JPEG tiles (1024^2, C2
+(OMR_BATCH_LANES in this process's environment): 8 client threads, 8 JPEG tiles (1024^2, C2
 settings, q 0.9) in flight each, 256 requests per pass; (a) the bench's pattern (16 distinct tiles
 of t 0, most requests deduplicated), (b) 64 distinct tiles over 4 timepoints.  Second of two passes
 timed.  One JSON line: answered and rendered tiles/s, p50 latency."""
@@ -26,7 +26,7 @@ def main():
     img = rng.integers(0, 65536, (NT, C, 1, grid * T, grid * T), dtype=np.uint16)
     fd, path = tempfile.mkstemp(prefix="omr_serve_", dir="/dev/shm")
     os.close(fd)
-    res = {"workers": os.environ.get("OMR_BATCHER_WORKERS", "default")}
+    res = {"workers": os.environ.get("OMR_BATCH_LANES", "default")}
     try:
         write_romio(path, img, _lib.PIXELS_UINT16)
         del img
