@@ -903,6 +903,7 @@ struct ArgbSource {
         px[2] = px2_of(nclamp[S] ? nb[S].y : nb[S].x); px[3] = px2_of(nb[S].y);
     }
     __device__ __forceinline__ uint32_t at(int x, int y) const { return *px_at<uint32_t>((uint32_t)(y * W + x)); }
+    __device__ __forceinline__ bool grey_possible() const { return true; }
     template <typename T>
     __device__ __forceinline__ const T* px_at(uint32_t i) const {
         return reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(img) + i * 4u);
@@ -993,7 +994,7 @@ struct PlaneSource {
                 v = fast16(x, p);
             } else if constexpr (MODE == kFusedFast16I) {
                 v = fast16i(x, p);
-            } else if constexpr (MODE == kFusedFast16F) {
+            } else if constexpr (MODE == kFusedFast16F || MODE == kFusedFast16FS) {
                 v = fast16f(x, p.wsi, F.R.fa[a], F.R.fb[a]);
             } else if (MODE == kFusedLinear16 || p.mode == kModeLinear16) {   // uniform
                 v = linear16(x, p, F.R.cd_start, F.R.cds8, F.R.cde8);
@@ -1031,13 +1032,16 @@ struct PlaneSource {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
             uint32_t w0 = raw[S][a][0], w1 = raw[S][a][1];
-            if constexpr (BPP == 2 && MODE == kFusedFast16F && OMR_F1_PK && (OMR_ABL & kAblRender) == 0) {
+            if constexpr (BPP == 2 && (MODE == kFusedFast16F || MODE == kFusedFast16FS) && OMR_F1_PK &&
+                          (OMR_ABL & kAblRender) == 0) {
                 // packed form: the byte swap of big-endian pixels is folded into the v_perm that
                 // builds 2^23 + x, so the raw word stays in file order (the sign bias moves to
-                // each half's first byte)
-                const uint32_t sg = F.R.is_signed ? (BE ? 0x00800080u : 0x80008000u) : 0u;
-                w0 ^= sg;
-                w1 ^= sg;
+                // each half's first byte; int16 pixels only: a compile-time mode)
+                if constexpr (MODE == kFusedFast16FS) {
+                    constexpr uint32_t sg = BE ? 0x00800080u : 0x80008000u;
+                    w0 ^= sg;
+                    w1 ^= sg;
+                }
                 if (F.R.any_check && F.R.ch[a].check) {      // wave-uniform
                     const uint32_t n0 = BE ? bswap16x2(w0) : w0, n1 = BE ? bswap16x2(w1) : w1;
                     const uint32_t hi2 = F.R.dhi2[a], lo2 = F.R.dlo2[a];
@@ -1081,6 +1085,7 @@ struct PlaneSource {
         }
     }
     __device__ __forceinline__ uint32_t at(int, int) const { return 0; }   // never: H % 16 == 0
+    __device__ __forceinline__ bool grey_possible() const { return F.R.grey_ok != 0; }
     // after the last MCU: a channel whose domain holds no 16-bit value fails every pixel
     __device__ __forceinline__ void finish() {
         if constexpr (BPP == 2) err |= F.R.dnone != 0;
@@ -1142,7 +1147,10 @@ __device__ __forceinline__ void b1_body(const B1Args& A, Src& src, int* S) {
             const int chv = (H + 1) / 2;
             const int cyg = my * 8 + cy;
             const bool edge = Src::kEdgeRows && cyg >= chv;
-            grey = __ballot(!(is_grey(px[0]) && is_grey(px[1]) && is_grey(px[2]) && is_grey(px[3])) || edge) == 0;
+            // (wave-uniform: only where the source can be grey at all; the general path gives the
+            // same coefficients for a grey MCU, so the test is purely a shortcut)
+            grey = src.grey_possible() &&
+                   __ballot(!(is_grey(px[0]) && is_grey(px[1]) && is_grey(px[2]) && is_grey(px[3])) || edge) == 0;
             int y, cb0, cr0, cb1, cr1, cb2, cr2, cb3, cr3;
             const int blk = (cy >> 2) * 2 + (cx >> 2);
             const int o = blk * kBS + ((2 * cy) & 7) * kRS + ((2 * cx) & 7);
@@ -1930,7 +1938,8 @@ template <bool BE>
 static void launch_render_fdct_mode(dim3 g, hipStream_t st, const B1Args& a1, const FusedArgs& f) {
     switch (f.R.mode) {
     case kFusedFast16:
-        if (f.R.f32) launch_render_fdct_na<2, BE, kFusedFast16F>(g, st, a1, f);
+        if (f.R.f32 && f.R.is_signed) launch_render_fdct_na<2, BE, kFusedFast16FS>(g, st, a1, f);
+        else if (f.R.f32) launch_render_fdct_na<2, BE, kFusedFast16F>(g, st, a1, f);
         else if (f.R.ws_int) launch_render_fdct_na<2, BE, kFusedFast16I>(g, st, a1, f);
         else launch_render_fdct_na<2, BE, kFusedFast16>(g, st, a1, f);
         break;

@@ -114,7 +114,8 @@ __device__ __forceinline__ uint32_t contrib_entry(const RenderPlan* __restrict__
 constexpr int kFusedMaxActive = 4;
 enum FusedMode : int32_t { kFusedTable8 = 0, kFusedLinear16 = 1, kFusedMixed16 = 2, kFusedFast16 = 4,
                            kFusedFast16I = 5 /* launch-only: Fast16 with integral window starts */,
-                           kFusedFast16F = 6 /* launch-only: Fast16I in f32 (FusedRender::f32) */ };
+                           kFusedFast16F = 6 /* launch-only: Fast16I in f32 (FusedRender::f32) */,
+                           kFusedFast16FS = 7 /* launch-only: kFusedFast16F on int16 pixels (sign bias) */ };
 struct FusedRender {
     K2Chan ch[kFusedMaxActive];
     const uint32_t* contrib;     // [n_active][256] (workspace; built by K1 unless the kernel builds it)
@@ -131,6 +132,9 @@ struct FusedRender {
     // checked channel's domain holds no 16-bit value at all (every pixel fails)
     uint32_t dlo2[kFusedMaxActive], dhi2[kFusedMaxActive];
     int32_t dnone;
+    // an all-grey MCU (every pixel r == g == b) is possible: the greyscale model, or every channel's
+    // colour grey without a .lut; otherwise F1 skips its grey-MCU test (~15 VALU per MCU)
+    int32_t grey_ok;
 };
 
 // (fa, fb) for fast16f such that fast16f(x) == fast16i(x) for every x in [0, xmax] (the pixel

@@ -1517,6 +1517,16 @@ omr_status render_fused_stage(Ctx* ctx, FusedPlanBuf* fp, size_t ws_off, FusedRe
     F.cds8 = pp.plan.cd_start & 0xFF;
     F.cde8 = pp.plan.cd_end & 0xFF;
     F.is_signed = fp->pixel_type == OMR_PIXELS_INT8 || fp->pixel_type == OMR_PIXELS_INT16;
+    // grey MCUs: the greyscale model renders (v, v, v) unless a .lut colours it (OMR_SEM_GREYSCALE_LUT);
+    // the rgb model only when every channel's colour has r == g == b and no .lut
+    F.grey_ok = 1;
+    for (int i = 0; i < na; ++i) {
+        const ChanParam& c = pp.plan.ch[i];
+        const bool lut = c.has_lut && (!pp.plan.greyscale || (pp.plan.sem & OMR_SEM_GREYSCALE_LUT));
+        const bool grey_colour = pp.plan.greyscale || (c.ratio[0] == c.ratio[1] && c.ratio[1] == c.ratio[2] &&
+                                                       c.cratio[0] == c.cratio[1] && c.cratio[1] == c.cratio[2]);
+        if (lut || !grey_colour) F.grey_ok = 0;
+    }
     return OMR_OK;
 }
 
