@@ -1519,12 +1519,31 @@ static size_t png_scratch(int kind, int W, int H) { return png_layout(kind, W, H
 //   P8 k_pngb_emit     16 output bytes per lane: prefix chunks, IDAT header, zlib stream (deflate
 //                      words funnel-shifted, or stored blocks of the filtered stream), Adler,
 //                      IEND — aligned 16-byte stores
-//   P9 k_pngb_crc      braided CRC-32: one wave per 16 KiB strip, coalesced dword loads, the
-//                      strips combined by x^(8n) powers
+//   P8+P9 k_pngb_emit_crc  (round 6, the default) P8 with each wave's 4 KiB strip CRCed from the
+//                      registers it stores (16-byte braid over the lanes); P9b k_pngb_crc_combine
+//                      moves every strip's CRC to the range end by x^(8n) powers and XORs them
+//   P9 k_pngb_crc      (OMR_PNG_CRC_P9=1: after the plain P8) braided CRC-32 re-reading the file:
+//                      one wave per 16 KiB strip, coalesced dword loads, strips combined by powers
 //   P10 k_pngb_finish  one lane per image: the CRC bytes
 // =====================================================================================
 constexpr int kPngbGroup = 256;                 // segments per P4/P7 group
-constexpr int kPngbEmitBytes = 16 * 256;        // output bytes per P8 workgroup
+constexpr int kPngbEmitBytes = 16 * 256;        // output bytes per P8 workgroup (separate P9)
+// P8 with the IDAT CRC fused (round 6, the default): each wave emits one strip of the file and
+// CRCs the IDAT-range bytes of it from the registers it stored (k_pngb_emit_crc), P9b combines the
+// strips' CRCs (k_pngb_crc_combine), so the file is not read back from HBM by a separate CRC pass.
+// 4 KiB strips (round 6 A/B, profiles/r06/ab_png_crc_strip.txt): at 256 C2 tiles per call 4, 8 and
+// 16 KiB run alike (P8+P9b 0.343-0.348 ms); on the smaller batches of the probe's other cases 4 KiB
+// is 6 % faster (more waves, shorter CRC chains per lane).
+#ifndef OMR_PNG_CRC_STRIP_KIB
+#define OMR_PNG_CRC_STRIP_KIB 4
+#endif
+constexpr int kPngbEmitCrcStrip = OMR_PNG_CRC_STRIP_KIB * 1024;   // bytes a wave emits and CRCs (steps of 1 KiB)
+constexpr int kPngbEmitCrcBytes = 4 * kPngbEmitCrcStrip;   // file bytes per workgroup (4 waves)
+// env OMR_PNG_CRC_P9=1: the round-5 form (P8 4 KiB per workgroup, then the separate P9 pass)
+static bool png_crc_separate() {
+    static const bool v = [] { const char* e = std::getenv("OMR_PNG_CRC_P9"); return e && std::atoi(e) != 0; }();
+    return v;
+}
 constexpr int kPngbCrcBytes = 256 * 256;        // CRC range bytes per P9 workgroup
 constexpr int kPngbMaxSide = 4096;
 constexpr int kCrcPowLo = 4096, kCrcPowHi = 2048;
@@ -1580,7 +1599,8 @@ struct PngBatch {
     uint64_t* d_offsets;
     uint32_t* d_lengths;
     int32_t* d_status;
-    const uint32_t* crc_pow;                    // [kCrcPowLo + kCrcPowHi]
+    const uint32_t* crc_pow;                    // [kCrcPowAll] (k_png_crc_pow)
+    uint32_t* strip_crc;                        // [P8 workgroups][4] raw CRC of each P8+P9 strip at its end
 };
 
 // Image owning global item `x` of a stage whose per-image first items are `first` (sorted).
@@ -1609,12 +1629,39 @@ __device__ __forceinline__ PngArgs pngb_args(const PngImg& I) {
     return A;
 }
 
-// x^(8*256*j) mod P: [0, 4096) for j, [4096, 6144) for j * 4096 (one lane per entry).
+// x^-1 mod P (zlib's reflected form: bit 31 is x^0): with P = x Q + 1, x Q = P + 1 = 1 mod P, so
+// x^-1 = Q = x^31 + x^25 + x^22 + x^21 + x^15 + x^11 + x^10 + x^9 + x^7 + x^6 + x^4 + x^3 + x + 1
+constexpr uint32_t kCrcXInv = (1u << 0) | (1u << 6) | (1u << 9) | (1u << 10) | (1u << 16) | (1u << 20) |
+                              (1u << 21) | (1u << 22) | (1u << 24) | (1u << 25) | (1u << 27) | (1u << 28) |
+                              (1u << 30) | (1u << 31);
+static_assert(multmodp_c(1u << 30, kCrcXInv) == 1u << 31, "x * x^-1 == 1 mod P");
+constexpr int kCrcPowR = kCrcPowLo + kCrcPowHi;   // x^(8 r), r < 256
+constexpr int kCrcInvR = kCrcPowR + 256;          // x^(-8 r), r < 256
+constexpr int kCrcInvA = kCrcInvR + 256;          // x^(-8 256 a), a < 64
+constexpr int kCrcPowAll = kCrcInvA + 64;
+
+// x^(8*256*j) mod P: [0, 4096) for j, [4096, 6144) for j * 4096; then x^(8 r) and x^(-8 r) for
+// r < 256 and x^(-8*256*a) for a < 64 (one lane per entry).
 __global__ void __launch_bounds__(256) k_png_crc_pow(uint32_t* __restrict__ pw) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= kCrcPowLo + kCrcPowHi) return;
-    const uint64_t j = i < kCrcPowLo ? (uint64_t)i : (uint64_t)(i - kCrcPowLo) * kCrcPowLo;
-    pw[i] = x2nmodp(j * 256, 3);
+    if (i >= kCrcPowAll) return;
+    if (i < kCrcPowR) {
+        const uint64_t j = i < kCrcPowLo ? (uint64_t)i : (uint64_t)(i - kCrcPowLo) * kCrcPowLo;
+        pw[i] = x2nmodp(j * 256, 3);
+        return;
+    }
+    const bool inv = i >= kCrcInvR;
+    const uint64_t e = i < kCrcInvR ? (uint64_t)(i - kCrcPowR) : i < kCrcInvA ? (uint64_t)(i - kCrcInvR)
+                                                                             : (uint64_t)(i - kCrcInvA) * 256;
+    if (!inv) { pw[i] = x2nmodp(e, 3); return; }
+    uint32_t xi8 = kCrcXInv;                      // x^-8 = (x^-1)^8
+    for (int k = 0; k < 3; ++k) xi8 = multmodp(xi8, xi8);
+    uint32_t p = 1u << 31, b = xi8;
+    for (uint64_t n = e; n; n >>= 1) {            // (x^-8)^e by squaring
+        if (n & 1) p = multmodp(b, p);
+        b = multmodp(b, b);
+    }
+    pw[i] = p;
 }
 
 __global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
@@ -2432,7 +2479,40 @@ __device__ uint32_t pngb_file_byte(const PngBatch& B, const PngImg& I, const Png
     return k < 12 ? c_iend[k] : 0u;
 }
 
-// P8: 16 bytes of one file per lane, one aligned 16-byte store.
+// The 16 bytes of image I's file at k0 outside the dynamic stream's interior (chunk headers,
+// zlib header and Adler, stored blocks, CRC and IEND), byte by byte: a rare path, kept out of line
+// so it does not inflate the callers' registers.
+__device__ __noinline__ uint4 pngb_file_chunk_bytes(const PngBatch& B, const PngImg& I, const PngMeta& M, int64_t k0) {
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t v = 0;
+        for (int b = 0; b < 4; ++b) {
+            const int64_t k = k0 + 4 * j + b;
+            if (k < M.file_len) v |= pngb_file_byte(B, I, M, k) << (8 * b);
+        }
+        o[j] = v;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// The 16 bytes of image I's file at k0 (P8's body).
+__device__ __forceinline__ uint4 pngb_file_chunk(const PngBatch& B, const PngImg& I, const PngMeta& M, int64_t k0) {
+    const int64_t d0 = k0 - I.pre_len - 10;            // deflate byte of k0 (dynamic stream)
+    if (!M.stored && d0 >= 0 && k0 + 16 <= I.pre_len + 8 + M.zlen - 4) {
+        const uint32_t* w = B.words + I.words + (d0 >> 2);
+        const int sh = (int)(d0 & 3) * 8;
+        uint32_t x[5], o[4];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) x[j] = w[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = sh ? (x[j] >> sh) | (x[j + 1] << (32 - sh)) : x[j];
+        return make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    return pngb_file_chunk_bytes(B, I, M, k0);
+}
+
+// P8: 16 bytes of one file per lane, one aligned 16-byte store (the form with a separate P9).
 __global__ void __launch_bounds__(256) k_pngb_emit(PngBatch B) {
     const int i = pngb_image(B, B.eblk0, B.eblk_per, blockIdx.x);
     const PngImg& I = B.img[i];
@@ -2440,28 +2520,7 @@ __global__ void __launch_bounds__(256) k_pngb_emit(PngBatch B) {
     const int64_t lb = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.eblk_per : I.eblk0);
     const int64_t k0 = (lb * 256 + threadIdx.x) * 16;
     if (M.off < 0 || k0 >= M.file_len) return;
-    uint32_t o[4];
-    const int64_t d0 = k0 - I.pre_len - 10;            // deflate byte of k0 (dynamic stream)
-    if (!M.stored && d0 >= 0 && k0 + 16 <= I.pre_len + 8 + M.zlen - 4) {
-        const uint32_t* w = B.words + I.words + (d0 >> 2);
-        const int sh = (int)(d0 & 3) * 8;
-        uint32_t x[5];
-#pragma unroll
-        for (int j = 0; j < 5; ++j) x[j] = w[j];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = sh ? (x[j] >> sh) | (x[j + 1] << (32 - sh)) : x[j];
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t v = 0;
-            for (int b = 0; b < 4; ++b) {
-                const int64_t k = k0 + 4 * j + b;
-                if (k < M.file_len) v |= pngb_file_byte(B, I, M, k) << (8 * b);
-            }
-            o[j] = v;
-        }
-    }
-    *reinterpret_cast<uint4*>(B.out + M.off + k0) = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(B.out + M.off + k0) = pngb_file_chunk(B, I, M, k0);
 }
 
 // P9 tables (round 5): braid[b][v] = raw CRC of byte v at position b of a 4-byte word followed
@@ -2586,6 +2645,151 @@ __global__ void __launch_bounds__(256) k_pngb_crc(PngBatch B) {
     }
 }
 
+// P8+P9 tables: hop[b][v] = raw CRC of byte v at position b of a 4-byte word followed by 3 - b +
+// 1008 zero bytes (the state then sits at the same lane's next 16-byte chunk, 1 KiB on); lane16[k]
+// = x^(8 (1008 - 16 k)), the shift from the end of lane k's last chunk to the end of its strip.
+struct CrcHop {
+    uint32_t hop[4][256];
+    uint32_t lane16[64];
+};
+constexpr CrcHop make_crc_hop() {
+    CrcHop c{};
+    uint32_t t[256] = {}, t0[256] = {};
+    for (uint32_t n = 0; n < 256; ++n) {
+        uint32_t r = n;
+        for (int k = 0; k < 8; ++k) r = (r & 1) ? kCrcPoly ^ (r >> 1) : r >> 1;
+        t[n] = t0[n] = r;
+    }
+    for (int k = 0; k <= 1011; ++k) {          // t = CRC of byte n followed by k zero bytes
+        for (int b = 0; b < 4; ++b)
+            if (k == 1011 - b)
+                for (int n = 0; n < 256; ++n) c.hop[b][n] = t[n];
+        for (int n = 0; n < 256; ++n) t[n] = (t[n] >> 8) ^ t0[t[n] & 0xFF];
+    }
+    uint32_t x8 = 1u << 30;                    // x^1 -> x^8
+    for (int i = 0; i < 3; ++i) x8 = multmodp_c(x8, x8);
+    const uint32_t x32 = multmodp_c(multmodp_c(x8, x8), multmodp_c(x8, x8));
+    const uint32_t x128 = multmodp_c(multmodp_c(x32, x32), multmodp_c(x32, x32));          // x^(8*16)
+    uint32_t p = 1u << 31;                     // lane 63: x^0
+    for (int k = 63; k >= 0; --k) {
+        c.lane16[k] = p;
+        p = multmodp_c(x128, p);
+    }
+    return c;
+}
+__constant__ CrcHop c_hop = make_crc_hop();
+
+// P8 + P9 fused (round 6, the default): each wave emits a strip of the file (lane t, step
+// s: the 16 bytes at strip + 1 KiB s + 16 t -- one coalesced 1 KiB store per step) and CRCs it
+// from the same registers: lane t's 16 bytes are four words through slicing-by-4 tables, the
+// fourth with a table that also hops the state over the other lanes' 1008 bytes to its next chunk
+// (a 16-byte braid); no LDS staging, no barrier after the tables.  Bytes outside the IDAT range
+// ['IDAT', end of the zlib stream) read as 0.  The strip's raw CRC sits at the strip end E; it is
+// moved to the range end R1 (x^(8 (R1 - E)) from the power tables, or x^(-8 (E - R1)) for the
+// strip holding R1, whose trailing bytes read as 0) in P9b, which XORs it into the file's CRC; P10
+// stores it.  The file is not read back from HBM (P9 re-read it: 482 MB per 256 C2 tiles).
+__global__ void __launch_bounds__(256) k_pngb_emit_crc(PngBatch B) {
+    constexpr int kSteps = kPngbEmitCrcStrip / 1024;
+    __shared__ uint32_t sl[4][256], sh[4][256];
+    const int i = pngb_image(B, B.eblk0, B.eblk_per, blockIdx.x);
+    const PngImg& I = B.img[i];
+    const PngMeta& M = B.meta[i];
+    const int64_t lb = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.eblk_per : I.eblk0);
+    const int64_t F0 = lb * kPngbEmitCrcBytes;          // file offset of the workgroup's bytes
+    if (M.off < 0 || F0 >= M.file_len) return;          // workgroup-uniform
+    for (int k = threadIdx.x; k < 4 * 256; k += 256) {
+        sl[k >> 8][k & 255] = c_braid.last[k >> 8][k & 255];
+        sh[k >> 8][k & 255] = c_hop.hop[k >> 8][k & 255];
+    }
+    __syncthreads();                                    // the CRC tables
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t S0 = F0 + (int64_t)wv * kPngbEmitCrcStrip, E = S0 + kPngbEmitCrcStrip;
+    if (S0 >= M.file_len) return;                       // wave-uniform (P9b skips the strip too)
+    const int64_t R0 = I.pre_len + 4, R1 = I.pre_len + 8 + M.zlen;   // CRC range: 'IDAT' + zlib stream
+    const bool any = !(E <= R0 || S0 >= R1);            // wave-uniform: the strip holds range bytes
+    // range limits relative to this lane's first byte of the strip (clamped: a strip is 16 KiB)
+    const int64_t p0 = S0 + 16 * lane;
+    const int32_t lo = (int32_t)max<int64_t>(min<int64_t>(R0 - p0, 1 << 20), -(1 << 20));
+    const int32_t hi = (int32_t)max<int64_t>(min<int64_t>(R1 - p0, 1 << 20), -(1 << 20));
+    auto T = [&](const uint32_t (*t)[256], uint32_t x) {
+        return t[0][x & 255] ^ t[1][(x >> 8) & 255] ^ t[2][(x >> 16) & 255] ^ t[3][x >> 24];
+    };
+    uint32_t q = 0;
+#pragma unroll 4
+    for (int st = 0; st < kSteps; ++st) {
+        const int64_t k0 = p0 + 1024 * st;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k0 < M.file_len) {
+            v = pngb_file_chunk(B, I, M, k0);
+            *reinterpret_cast<uint4*>(B.out + M.off + k0) = v;
+        }
+        if (any) {
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t r = 1024 * st + 4 * j;    // word offset from p0
+                if (r < lo) w[j] = r + 4 <= lo ? 0u : w[j] & (0xFFFFFFFFu << (8 * (lo - r)));     // before the range
+                if (r + 4 > hi) w[j] = r >= hi ? 0u : w[j] & (0xFFFFFFFFu >> (8 * (r + 4 - hi))); // after it
+                q = (j < 3 || st == kSteps - 1) ? T(sl, q ^ w[j]) : T(sh, q ^ w[j]);
+            }
+        }
+    }
+    uint32_t c = 0;
+    if (any) {
+        c = q ? multmodp(c_hop.lane16[lane], q) : 0u;
+        for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o, 64);
+    }
+    // the strip's raw CRC at its end; P9b moves it to the range end (one thread per strip, so the
+    // GF(2) products run on every lane instead of on lane 0 of each wave)
+    if (lane == 0) B.strip_crc[(int64_t)blockIdx.x * 4 + wv] = c;
+}
+
+// P9b: every strip's CRC moved to its file's range end R1 -- x^(8 (R1 - E)), or x^(-8 (E - R1))
+// for the strip holding R1 -- plus the init / final inversions once per file, XORed into the CRC.
+__global__ void __launch_bounds__(256) k_pngb_crc_combine(PngBatch B, int64_t n_strips) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = g < n_strips;
+    const int64_t blk = live ? g >> 2 : (n_strips - 1) >> 2;
+    const int i = pngb_image(B, B.eblk0, B.eblk_per, blk);
+    const PngImg& I = B.img[i];
+    const PngMeta& M = B.meta[i];
+    const int64_t lb = blk - (B.uniform ? (int64_t)i * B.eblk_per : I.eblk0);
+    const int64_t S0 = lb * kPngbEmitCrcBytes + (g & 3) * (int64_t)kPngbEmitCrcStrip, E = S0 + kPngbEmitCrcStrip;
+    const int64_t R0 = I.pre_len + 4, R1 = I.pre_len + 8 + M.zlen;
+    // strips the emit skipped contribute 0 (no early return: the wave reduces below)
+    const bool used = live && !(M.off < 0 || S0 >= M.file_len || E <= R0 || S0 >= R1);
+    uint32_t c = used ? B.strip_crc[g] : 0u;
+    if (c) {
+        if (E <= R1) {                                  // x^(8 d), d = R1 - E = 256 jj + r
+            const uint64_t d = (uint64_t)(R1 - E), jj = d >> 8, r = d & 255;
+            if (r) c = multmodp(B.crc_pow[kCrcPowR + r], c);
+            if (jj & (kCrcPowLo - 1)) c = multmodp(B.crc_pow[jj & (kCrcPowLo - 1)], c);
+            if (jj >= kCrcPowLo) c = multmodp(B.crc_pow[kCrcPowLo + (jj / kCrcPowLo)], c);
+        } else {                                        // the strip holding R1: x^(-8 t), t < the strip
+            const uint64_t t = (uint64_t)(E - R1), a = t >> 8, r = t & 255;
+            if (r) c = multmodp(B.crc_pow[kCrcInvR + r], c);
+            if (a) c = multmodp(B.crc_pow[kCrcInvA + a], c);
+        }
+    }
+    if (used && E >= R1) {                              // the init / final inversions: x^(8 n) from the tables
+        const uint64_t n = (uint64_t)(R1 - R0), jj = n >> 8, r = n & 255;   // (x2nmodp's 21 dependent
+        uint32_t x = B.crc_pow[kCrcPowR + r];                                // constant loads cost 40 us)
+        if (jj & (kCrcPowLo - 1)) x = multmodp(B.crc_pow[jj & (kCrcPowLo - 1)], x);
+        if (jj >= kCrcPowLo) x = multmodp(B.crc_pow[kCrcPowLo + (jj / kCrcPowLo)], x);
+        c ^= ~multmodp(x, 0xFFFFFFFFu);
+    }
+    // one atomic per wave when its 64 strips are one file's (all but the waves at file seams):
+    // 256 files' CRC words otherwise take every strip's atomic in turn
+    const int i0 = __shfl(i, 0, 64);
+    if (__ballot(i != i0) == 0) {
+        for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0 && c) atomicXor(&B.meta[i].crc, c);
+    } else if (c) {
+        atomicXor(&B.meta[i].crc, c);
+    }
+}
+static_assert(kPngbEmitCrcStrip / 256 <= 64, "P8+P9: the inverse-power table covers a strip");
+
 // P10: the CRC bytes after the zlib stream.
 __global__ void __launch_bounds__(256) k_pngb_finish(PngBatch B) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2628,8 +2832,8 @@ static int png_prefix(int kind, int W, int H, const uint8_t* rgba, uint8_t* pre)
 
 static omr_status ensure_crc_pow(Ctx* ctx) {
     if (ctx->d_crc_pow) return OMR_OK;
-    OMR_HIP(ctx, hipMalloc(&ctx->d_crc_pow, sizeof(uint32_t) * (kCrcPowLo + kCrcPowHi)));
-    hipLaunchKernelGGL(k_png_crc_pow, dim3((kCrcPowLo + kCrcPowHi + 255) / 256), dim3(256), 0, ctx->stream,
+    OMR_HIP(ctx, hipMalloc(&ctx->d_crc_pow, sizeof(uint32_t) * kCrcPowAll));
+    hipLaunchKernelGGL(k_png_crc_pow, dim3((kCrcPowAll + 255) / 256), dim3(256), 0, ctx->stream,
                        ctx->d_crc_pow);
     OMR_HIP(ctx, hipGetLastError());
     return OMR_OK;
@@ -2643,7 +2847,7 @@ struct PngBatchPlan {
     int64_t rows = 0, rblk = 0, pblk = 0, grp = 0, eblk = 0, cblk = 0, segs = 0, toks = 0, flt = 0, words = 0;
     size_t rows_lds = 16, parse_lds = 16;
     bool uniform = true;
-    size_t o_img, o_first, o_flt, o_bh, o_poff, o_blk, o_trace, o_hist, o_tab, o_meta, o_rows, o_words;
+    size_t o_img, o_first, o_flt, o_bh, o_poff, o_blk, o_trace, o_hist, o_tab, o_meta, o_rows, o_words, o_scrc;
     size_t scratch = 0;
 };
 
@@ -2668,7 +2872,8 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         d.pre_len = png_prefix(h.kind, h.W, h.H, h.rgba, d.pre);
         const int64_t npb = (d.nseg + kParseLanes - 1) / kParseLanes, ng = (d.nseg + kPngbGroup - 1) / kPngbGroup;
         const int64_t max_file = d.pre_len + 8 + P.zlen + 4 + 12;
-        const int64_t ne = (max_file + kPngbEmitBytes - 1) / kPngbEmitBytes;
+        const int64_t eb = png_crc_separate() ? kPngbEmitBytes : kPngbEmitCrcBytes;
+        const int64_t ne = (max_file + eb - 1) / eb;
         const int64_t nc = (4 + P.zlen + kPngbCrcBytes - 1) / kPngbCrcBytes;
         if (L.rows + h.H > INT32_MAX || L.pblk + npb > INT32_MAX || L.grp + ng > INT32_MAX ||
             L.eblk + ne > INT32_MAX || L.cblk + nc > INT32_MAX)
@@ -2715,6 +2920,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
     L.o_meta = take(sizeof(PngMeta) * n);
     L.o_rows = take((size_t)L.rows * 16);
     L.o_words = take((size_t)L.words * 4 + 64);
+    L.o_scrc = take((size_t)L.eblk * 16);
     L.scratch = o;
     return OMR_OK;
 }
@@ -2739,7 +2945,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     auto at = [&](size_t rel) { return ws_off + rel; };
     const size_t o_img = at(L.o_img), o_first = at(L.o_first), o_flt = at(L.o_flt),
                  o_blk = at(L.o_blk), o_hist = at(L.o_hist), o_tab = at(L.o_tab), o_meta = at(L.o_meta),
-                 o_rows = at(L.o_rows), o_words = at(L.o_words);
+                 o_rows = at(L.o_rows), o_words = at(L.o_words), o_scrc = at(L.o_scrc);
     uint8_t* ws = static_cast<uint8_t*>(ctx->ws);
     PngBatch Bt{};
     Bt.img = reinterpret_cast<const PngImg*>(ws + o_img);
@@ -2779,6 +2985,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     Bt.d_lengths = d_lengths;
     Bt.d_status = d_status;
     Bt.crc_pow = ctx->d_crc_pow;
+    Bt.strip_crc = reinterpret_cast<uint32_t*>(ws + o_scrc);
     st = stage_h2d2(ctx, ws + o_img, I.data(), sizeof(PngImg) * n, ws + o_first, firsts.data(),
                     sizeof(int32_t) * 5 * n);
     if (st) return st;
@@ -2836,10 +3043,13 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     }
     {
         KernelTimer t(ctx, 25);
-        hipLaunchKernelGGL(k_pngb_emit, dim3((unsigned)eblk), dim3(256), 0, s, Bt);
+        if (png_crc_separate()) hipLaunchKernelGGL(k_pngb_emit, dim3((unsigned)eblk), dim3(256), 0, s, Bt);
+        else hipLaunchKernelGGL(k_pngb_emit_crc, dim3((unsigned)eblk), dim3(256), 0, s, Bt);   // P8 + P9
     }
     KernelTimer t_crc(ctx, 26);
-    hipLaunchKernelGGL(k_pngb_crc, dim3((unsigned)cblk), dim3(256), 0, s, Bt);
+    if (png_crc_separate()) hipLaunchKernelGGL(k_pngb_crc, dim3((unsigned)cblk), dim3(256), 0, s, Bt);
+    else hipLaunchKernelGGL(k_pngb_crc_combine, dim3((unsigned)((eblk * 4 + 255) / 256)), dim3(256), 0, s, Bt,
+                            (int64_t)(eblk * 4));
     hipLaunchKernelGGL(k_pngb_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Bt);
     OMR_HIP(ctx, hipGetLastError());
     return OMR_OK;

@@ -267,13 +267,20 @@ __device__ __forceinline__ BucketMap bucket_map(uint32_t t1, uint32_t k1, uint32
     m.org = t1 >= step ? (uint32_t)((t1 - step) & ~(step - 1)) : 0u;
     const uint64_t end = (uint64_t)m.org + ((uint64_t)nbk << sh) - 1u;
     m.hi = end > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)end;
-    m.pad = 0;
+    m.pad = m.org >= 0x80000000u ? 1u : 0u;               // float keys: K2 may clamp the raw bits
+    // (org >= key(+0.0) -- every threshold of a float channel sits above +0)
     return m;
 }
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t x, uint32_t lo, uint32_t hi) {
     uint32_t r;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+    return r;
+}
+
+__device__ __forceinline__ int32_t med3_i32(int32_t x, int32_t lo, int32_t hi) {
+    int32_t r;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
     return r;
 }
 
@@ -382,6 +389,39 @@ __device__ __forceinline__ void k2_chunk(const K2Args& A, Chunk<BPP, VEC> (&ckk)
                 const uint32_t cnan = (T[0] >> 8) & 0xFFu;
                 const BucketMap& M = reinterpret_cast<const BucketMap*>(s_bkt + na * nbk)[a];
                 const uint32_t org = M.org, hi = M.hi, sh = M.sh, inb = (1u << sh) - 1u;
+                if constexpr (PT == OMR_PIXELS_FLOAT || PT == OMR_PIXELS_INT32) {
+                    if (PT == OMR_PIXELS_INT32 || M.pad) {              // uniform: clamp the raw bits (k_build_buckets)
+                        // raw pixel bits as int32: key = raw ^ 2^31 is a monotone bijection for
+                        // int32, and for floats on the non-negative half (every negative float
+                        // and -0 clamps to org_r >= 0, where the count is 0 like theirs).  The
+                        // bucket of raw r is (r >> sh, arithmetic) + 2^(31 - sh) - (org >> sh).
+                        const int32_t org_r = (int32_t)(org ^ 0x80000000u), hi_r = (int32_t)(hi ^ 0x80000000u);
+                        const uint32_t* const Bkr = Bk - (org >> sh) + (0x80000000u >> sh);
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) {
+                            uint32_t raw = c.dw[j];
+                            if constexpr (BE) raw = bswap32(raw);
+                            const int32_t kc = med3_i32((int32_t)raw, org_r, hi_r);
+                            const uint32_t e = Bkr[kc >> sh];
+                            const uint32_t off = e >> 8;
+                            uint32_t base = (e & 0xFFu) + (((uint32_t)kc & inb) >= off ? 1u : 0u);
+                            if (off - 0x800000u < 0x7FFFFFu) {          // two or more thresholds here
+                                const uint32_t key = (uint32_t)kc ^ 0x80000000u;   // the clamped key: same count
+                                uint32_t len = off & 0xFFu;
+                                while (len > 0) {
+                                    const uint32_t half = len >> 1;
+                                    const bool le = T[base + half + 1] <= key;
+                                    base = le ? base + half + 1 : base;
+                                    len = le ? len - half - 1 : half;
+                                }
+                            }
+                            if constexpr (PT == OMR_PIXELS_FLOAT) base = __builtin_isnan(__uint_as_float(raw)) ? cnan : base;
+                            acc[j] += tab[base];
+                            if (NA == 0 || NA > 4) acc[j] = clamp_fields(acc[j]);
+                        }
+                        continue;
+                    }
+                }
                 const uint32_t* const Bk0 = Bk - (org >> sh);           // org is a multiple of 2^sh
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) {

@@ -365,6 +365,11 @@ def _edge_values(ch, pt, qd, n=65536):
     dict(pt=_lib.PIXELS_FLOAT, ws=-100.5, we=1000.25),
     dict(pt=_lib.PIXELS_FLOAT, ws=-100.5, we=1000.25, noise_reduction=True),
     dict(pt=_lib.PIXELS_FLOAT, ws=3.0, we=700.0, cd=(10, 200, 100)),
+    # windows at / just above +0: the bucket origin lands at or next to key(+0), where K2 switches
+    # between clamping the raw bits (origin >= key(+0)) and the key transform (round 6)
+    dict(pt=_lib.PIXELS_FLOAT, ws=0.0, we=1.0),
+    dict(pt=_lib.PIXELS_FLOAT, ws=1e-40, we=1e-38),
+    dict(pt=_lib.PIXELS_FLOAT, ws=1e-30, we=3e-30, reverse=True),
     dict(pt=_lib.PIXELS_FLOAT, ws=1.5, we=5000.0, family=_lib.FAMILY_LOGARITHMIC),
     dict(pt=_lib.PIXELS_FLOAT, ws=0.1, we=900.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=0.5),
     dict(pt=_lib.PIXELS_FLOAT, ws=2.0, we=300.0, family=_lib.FAMILY_POLYNOMIAL, coefficient=2.0),
