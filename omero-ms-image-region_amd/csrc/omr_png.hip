@@ -786,6 +786,45 @@ __global__ void __launch_bounds__(kParseLanes) k_png_lz_parse(DflArgs D, int32_t
 // The parallel steps (ranking, depths, length assignment, canonical codes) use every lane; the
 // two-queue merge, the Kraft repair and the run-length header are short serial loops on lane 0.
 
+// Exclusive scan over the workgroup (blockDim.x a multiple of 64, s_wave[blockDim.x / 64]).
+__device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t w = lane < nw ? s_wave[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;
+    }
+    __syncthreads();
+    const uint32_t off = wid ? s_wave[wid - 1] : 0;
+    total = s_wave[nw - 1];
+    __syncthreads();
+    return off + x - v;
+}
+
+// Measurement build only (tools/ab_build.sh <name> -DOMR_PNG_T3_PROBE): block 0's shader-clock
+// stamps at the phases of the table build, read back by omr_png_t3_probe (tools/png_batch_probe.py).
+#ifdef OMR_PNG_T3_PROBE
+__device__ unsigned long long g_t3[16];
+#define T3MARK(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_t3[i] = __builtin_amdgcn_s_memtime(); } while (0)
+extern "C" int omr_png_t3_probe(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t3), sizeof(g_t3)) == hipSuccess ? 0 : 1;
+}
+#else
+#define T3MARK(i) do {} while (0)
+#endif
+
 // The table block D4/D5 read: codes, lengths and the block header bits.
 struct DflTables {
     uint16_t lcode[286];
@@ -796,10 +835,11 @@ struct DflTables {
 };
 
 constexpr int kHuffMaxSym = 288;
+constexpr int kHuffNodes = kHuffMaxSym + 2;   // W.wt index of node m (the first merged node)
 constexpr int kHuffThreads = 320;       // one symbol per thread (286 + 30 + 19 symbols: <= 286)
 struct HuffWork {                       // LDS scratch of one tree
     alignas(16) uint32_t f[kHuffMaxSym];   // symbol frequencies
-    uint32_t wt[2 * kHuffMaxSym];       // leaf weights (sorted), then merged nodes
+    uint32_t wt[2 * kHuffMaxSym + 8];   // leaf weights (sorted) + 2 x INF; merged nodes from kHuffNodes
     int16_t ord[kHuffMaxSym];           // used symbols by (frequency, symbol)
     int16_t parent[2 * kHuffMaxSym];
     uint8_t len[kHuffMaxSym];
@@ -808,6 +848,8 @@ struct HuffWork {                       // LDS scratch of one tree
     int wcnt[kHuffThreads / 64][16];    // per wave: symbols of each code length
     int m;
 };
+static_assert(sizeof(HuffWork::wt) >= 8 * (kHuffMaxSym + 1) && offsetof(HuffWork, wt) % 16 == 0,
+              "the rank keys (u64, n + 1) fit W.wt, 16-byte aligned");
 
 // Code lengths (<= maxbits) of the n symbols in W.f -> W.len, by the two-queue Huffman
 // construction (leaves sorted by (freq, symbol)), then miniz's tdefl_huffman_enforce_max_code_size:
@@ -819,24 +861,27 @@ __device__ void huff_lengths_dev(HuffWork& W, int n, int maxbits) {
     if (tid == 0) W.m = 0;
     if (tid < 17) W.bl[tid] = 0;
     __syncthreads();
+    if (n == 286) T3MARK(8);
+    // rank among the used symbols in (frequency, symbol) order: with key = f << 9 | symbol (all
+    // ones for an unused symbol) a rank is one 64-bit compare per symbol, two keys per broadcast
+    // read (round 6: a third of the compares-and-selects of the (f, j < i) test)
+    uint64_t* key = reinterpret_cast<uint64_t*>(W.wt);          // free until the merge
+    for (int i = tid; i < n + 1; i += nt) {
+        const uint32_t fi = i < n ? W.f[i] : 0u;
+        key[i] = fi ? ((uint64_t)fi << 9) | (uint32_t)i : ~0ull;
+    }
+    __syncthreads();
     for (int i = tid; i < n; i += nt) {
-        const uint32_t fi = W.f[i];
+        const uint64_t ki = key[i];
         W.len[i] = 0;
-        if (fi) {                                   // rank among the used symbols (stable order)
+        if (ki != ~0ull) {
             int r = 0;
-            const int n4 = n & ~3;
-            const uint4* f4 = reinterpret_cast<const uint4*>(W.f);
+            const uint4* k2 = reinterpret_cast<const uint4*>(key);
 #pragma unroll 4
-            for (int j = 0; j < n4; j += 4) {       // four broadcast reads per LDS access
-                const uint4 v = f4[j >> 2];
-                r += (v.x != 0u && (v.x < fi || (v.x == fi && j < i))) ? 1 : 0;
-                r += (v.y != 0u && (v.y < fi || (v.y == fi && j + 1 < i))) ? 1 : 0;
-                r += (v.z != 0u && (v.z < fi || (v.z == fi && j + 2 < i))) ? 1 : 0;
-                r += (v.w != 0u && (v.w < fi || (v.w == fi && j + 3 < i))) ? 1 : 0;
-            }
-            for (int j = n4; j < n; ++j) {
-                const uint32_t fj = W.f[j];
-                r += (fj != 0u && (fj < fi || (fj == fi && j < i))) ? 1 : 0;
+            for (int j = 0; j < n; j += 2) {        // keys j, j + 1 (key[n] is all ones)
+                const uint4 v = k2[j >> 1];
+                r += (((uint64_t)v.y << 32) | v.x) < ki ? 1 : 0;
+                r += (((uint64_t)v.w << 32) | v.z) < ki ? 1 : 0;
             }
             W.ord[r] = (int16_t)i;
             atomicAdd(&W.m, 1);
@@ -853,33 +898,36 @@ __device__ void huff_lengths_dev(HuffWork& W, int n, int maxbits) {
         __syncthreads();
         return;
     }
-    for (int k = tid; k < m; k += nt) W.wt[k] = W.f[W.ord[k]];
+    // leaves, two INF entries after them, and INF in every node slot (a node not yet merged)
+    for (int k = tid; k < kHuffNodes + m + 1; k += nt)
+        W.wt[k] = k < m ? W.f[W.ord[k]] : 0xFFFFFFFFu;
     __syncthreads();
+    if (n == 286) T3MARK(9);
     if (tid == 0) {                                 // two queues: sorted leaves, merged nodes
-        // the two heads of each queue are read together (one LDS round trip per merge); a leaf
-        // wins ties, as wt[li] <= wt[qi] does
-        constexpr uint32_t kInf = 0xFFFFFFFFu;       // weights stay below it (< 2^31 bytes)
+        // Serial: each merge reads the two queue heads as two adjacent pairs -- leaves past m and
+        // nodes not yet merged read INF, so the reads are unconditional and go out together --
+        // and selects without branches.  A leaf wins ties, as wt[li] <= wt[qi] does.
         int li = 0, qi = m, qn = m;
+        const uint32_t* nodes = W.wt + kHuffNodes - m;   // nodes[q]: node q (q >= m)
         for (int c = 0; c < m - 1; ++c) {
-            const uint32_t a = li < m ? W.wt[li] : kInf, b = li + 1 < m ? W.wt[li + 1] : kInf;
-            const uint32_t q0 = qi < qn ? W.wt[qi] : kInf, q1 = qi + 1 < qn ? W.wt[qi + 1] : kInf;
-            int p0, p1;
-            uint32_t w0, w1;
-            if (a <= q0) {                          // first: leaf li; second: leaf li+1 or node qi
-                p0 = li; w0 = a;
-                if (b <= q0) { p1 = li + 1; w1 = b; li += 2; }
-                else { p1 = qi; w1 = q0; li += 1; qi += 1; }
-            } else {                                // first: node qi; second: leaf li or node qi+1
-                p0 = qi; w0 = q0;
-                if (a <= q1) { p1 = li; w1 = a; li += 1; qi += 1; }
-                else { p1 = qi + 1; w1 = q1; qi += 2; }
-            }
-            W.wt[qn] = w0 + w1;
+            const uint32_t a = W.wt[li], b = W.wt[li + 1];
+            const uint32_t q0 = nodes[qi], q1 = nodes[qi + 1];
+            const bool la = a <= q0;                 // first: leaf li, else node qi
+            const int p0 = la ? li : qi;
+            const uint32_t w0 = la ? a : q0;
+            const uint32_t c1 = la ? b : a, c2 = la ? q0 : q1;   // the second's two candidates
+            const bool lb = c1 <= c2;                // second: a leaf, else a node
+            const int p1 = la ? (lb ? li + 1 : qi) : (lb ? li : qi + 1);
+            const uint32_t w1 = lb ? c1 : c2;
+            li += (la ? 1 : 0) + (lb ? 1 : 0);
+            qi += (la ? 0 : 1) + (lb ? 0 : 1);
+            W.wt[kHuffNodes + qn - m] = w0 + w1;
             W.parent[p0] = W.parent[p1] = (int16_t)qn;
             ++qn;
         }
     }
     __syncthreads();
+    if (n == 286) T3MARK(10);
     const int root = 2 * m - 2;
     for (int k = tid; k < m; k += nt) {             // leaf depth: walk up to the root
         int d = 0;
@@ -887,6 +935,7 @@ __device__ void huff_lengths_dev(HuffWork& W, int n, int maxbits) {
         atomicAdd(&W.bl[min(d, maxbits)], 1);
     }
     __syncthreads();
+    if (n == 286) T3MARK(11);
     if (tid == 0) {                                 // Kraft repair after the clamp (in registers)
         int bl[16];
 #pragma unroll
@@ -918,6 +967,7 @@ __device__ void huff_lengths_dev(HuffWork& W, int n, int maxbits) {
         W.len[W.ord[k]] = (uint8_t)b;
     }
     __syncthreads();
+    if (n == 286) T3MARK(12);
 }
 
 // Canonical codes of W.len (RFC 1951 3.2.2), bit-reversed for LSB-first packing; every thread
@@ -965,86 +1015,121 @@ __device__ void png_build_tables(const uint32_t* __restrict__ hist, DflTables* _
     __shared__ uint8_t rs[286 + 30], rx[286 + 30];   // run-length symbols and their extra bits
     __shared__ int s_nr, s_hlit, s_hdist;
     const int tid = threadIdx.x;
+    T3MARK(0);
     for (int i = tid; i < 286; i += kHuffThreads) W.f[i] = hist[i] + (i == 256 ? 1u : 0u);   // + EOB
     huff_lengths_dev(W, 286, kMaxBits);
+    T3MARK(1);
     for (int i = tid; i < 286; i += kHuffThreads) t.llen[i] = W.len[i];
     huff_canon_dev(W, 286, t.lcode);
+    T3MARK(2);
     if (tid < 30) W.f[tid] = hist[286 + tid];
     huff_lengths_dev(W, 30, kMaxBits);
     if (tid < 30) t.dlen[tid] = W.len[tid];
     huff_canon_dev(W, 30, t.dcode);
-    if (tid == 0) {                                 // zlib trees.c scan_tree over the lengths
+    T3MARK(3);
+    // zlib trees.c scan_tree over the lengths, one thread per run of equal lengths (round 6; the
+    // serial walk on lane 0 took ~107k cycles): runs found by a neighbour compare and compacted by
+    // a scan, each run's entries counted, scanned and written at their positions -- the same
+    // entries in the same order as the walk (a zero run: chunks of min(rest, 138) while >= 3
+    // remain; a non-zero run: the length, then 16 for min(rest - 1, 6) more, while >= 4 remain;
+    // single entries for the rest).  Entries <= ns <= 316 < kHuffThreads.
+    __shared__ uint32_t s_wave[kHuffThreads / 64];
+    __shared__ int16_t run_at[286 + 30 + 1];
+    __shared__ int s_hclen;
+    if (tid == 0) {
         int hlit = 286, hdist = 30;
         while (hlit > 257 && t.llen[hlit - 1] == 0) --hlit;
         while (hdist > 1 && t.dlen[hdist - 1] == 0) --hdist;
-        for (int i = 0; i < hlit; ++i) seq[i] = t.llen[i];
-        for (int i = 0; i < hdist; ++i) seq[hlit + i] = t.dlen[i];
-        const int ns = hlit + hdist;
-        int nr = 0;
-        for (int i = 0; i < ns;) {
-            const int v = seq[i];
-            int r = 1;
-            while (i + r < ns && seq[i + r] == v) ++r;
-            if (v == 0 && r >= 3) {
-                const int k = min(r, 138);
-                rs[nr] = k >= 11 ? 18 : 17;
-                rx[nr++] = (uint8_t)(k >= 11 ? k - 11 : k - 3);
-                i += k;
-            } else if (v != 0 && r >= 4) {
-                const int k = min(r - 1, 6);
-                rs[nr] = (uint8_t)v; rx[nr++] = 0;
-                rs[nr] = 16; rx[nr++] = (uint8_t)(k - 3);
-                i += 1 + k;
+        s_hlit = hlit; s_hdist = hdist;
+    }
+    __syncthreads();
+    const int ns = s_hlit + s_hdist;
+    if (tid < ns) seq[tid] = tid < s_hlit ? t.llen[tid] : t.dlen[tid - s_hlit];
+    __syncthreads();
+    {
+        const bool st = tid < ns && (tid == 0 || seq[tid] != seq[tid - 1]);
+        uint32_t nruns;
+        const uint32_t ri = pngb_block_excl_scan(st ? 1u : 0u, s_wave, nruns);
+        if (st) run_at[ri] = (int16_t)tid;
+        if (tid == 0) run_at[nruns] = (int16_t)ns;
+        __syncthreads();
+        const bool own = tid < (int)nruns;
+        const int r0 = own ? run_at[tid] : 0, len = own ? run_at[tid + 1] - r0 : 0;
+        const int v = own ? seq[r0] : 0;
+        auto walk = [&](auto&& emit) {               // the run's entries, in the walk's order
+            int rem = len;
+            if (v == 0) {
+                while (rem >= 3) {
+                    const int k = min(rem, 138);
+                    emit(k >= 11 ? 18 : 17, k >= 11 ? k - 11 : k - 3);
+                    rem -= k;
+                }
             } else {
-                rs[nr] = (uint8_t)v; rx[nr++] = 0;
-                ++i;
+                while (rem >= 4) {
+                    const int k = min(rem - 1, 6);
+                    emit(v, 0);
+                    emit(16, k - 3);
+                    rem -= 1 + k;
+                }
             }
-        }
-        s_nr = nr; s_hlit = hlit; s_hdist = hdist;
+            for (; rem > 0; --rem) emit(v, 0);
+        };
+        uint32_t cnt = 0;
+        walk([&](int, int) { ++cnt; });
+        uint32_t nr_all;
+        uint32_t at = pngb_block_excl_scan(cnt, s_wave, nr_all);
+        walk([&](int sym, int x) { rs[at] = (uint8_t)sym; rx[at] = (uint8_t)x; ++at; });
+        if (tid == 0) s_nr = (int)nr_all;
     }
     if (tid < 19) W.f[tid] = 0;
     __syncthreads();
+    T3MARK(4);
     const int nr = s_nr;
     for (int i = tid; i < nr; i += kHuffThreads) atomicAdd(&W.f[rs[i]], 1u);
     huff_lengths_dev(W, 19, 7);
     __shared__ uint16_t ccode[19];
     huff_canon_dev(W, 19, ccode);
+    T3MARK(5);
+    // The block header, LSB-first: BFINAL, BTYPE, HLIT, HDIST, HCLEN (17 bits), HCLEN 3-bit
+    // code-length-code lengths, then every run-length entry's code + extra bits at its scanned bit
+    // offset -- each field ORed into its (at most two) words in parallel.
+    static constexpr uint8_t kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
     for (int i = tid; i < 96; i += kHuffThreads) t.hdr[i] = 0;
-    // each run-length entry's code + extra bits (LSB-first: the code, then the extra), in parallel
-    __shared__ uint16_t ev[286 + 30];
-    __shared__ uint8_t en[286 + 30];
-    for (int i = tid; i < nr; i += kHuffThreads) {
-        const int sym = rs[i];
-        const int xb = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
-        ev[i] = (uint16_t)(ccode[sym] | ((uint32_t)rx[i] << W.len[sym]));
-        en[i] = (uint8_t)(W.len[sym] + xb);
-    }
-    __syncthreads();
-    if (tid == 0) {                                 // block header, LSB-first
-        static constexpr uint8_t kOrd[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    if (tid == 0) {
         int hclen = 19;
         while (hclen > 4 && W.len[kOrd[hclen - 1]] == 0) --hclen;
-        uint32_t nb = 0;
-        uint64_t acc = 0;                           // pending bits, LSB-first; whole words out
-        auto put = [&](uint32_t v, int n) {
-            acc |= (uint64_t)(v & ((1u << n) - 1u)) << (nb & 31);   // n <= 14
-            nb += n;
-            if ((nb >> 5) != ((nb - n) >> 5)) { t.hdr[(nb - n) >> 5] = (uint32_t)acc; acc >>= 32; }
-        };
-        put(1, 1);                                  // BFINAL
-        put(2, 2);                                  // BTYPE = 10 (dynamic)
-        put((uint32_t)(s_hlit - 257), 5);
-        put((uint32_t)(s_hdist - 1), 5);
-        put((uint32_t)(hclen - 4), 4);
-        for (int i = 0; i < hclen; ++i) put(W.len[kOrd[i]], 3);
-        for (int i = 0; i < nr; ++i) put(ev[i], en[i]);
-        if (nb & 31) t.hdr[nb >> 5] = (uint32_t)acc;
-        t.hdr[95] = nb;
+        s_hclen = hclen;
     }
     __syncthreads();
+    const int hclen = s_hclen;
+    const uint32_t hbits = 17 + 3 * (uint32_t)hclen;
+    auto put_at = [&](uint32_t pos, uint32_t v) {    // v < 2^17
+        const uint64_t sh = (uint64_t)v << (pos & 31);
+        atomicOr(&t.hdr[pos >> 5], (uint32_t)sh);
+        if ((uint32_t)(sh >> 32)) atomicOr(&t.hdr[(pos >> 5) + 1], (uint32_t)(sh >> 32));
+    };
+    uint32_t ev = 0, en = 0;
+    if (tid < nr) {
+        const int sym = rs[tid];
+        const int xb = sym == 16 ? 2 : sym == 17 ? 3 : sym == 18 ? 7 : 0;
+        ev = ccode[sym] | ((uint32_t)rx[tid] << W.len[sym]);
+        en = (uint32_t)(W.len[sym] + xb);
+    }
+    uint32_t ebits;
+    const uint32_t eoff = hbits + pngb_block_excl_scan(en, s_wave, ebits);
+    if (en) put_at(eoff, ev);
+    if (tid < hclen) put_at(17 + 3 * (uint32_t)tid, W.len[kOrd[tid]]);
+    if (tid == 0) {
+        put_at(0, 1u | (2u << 1) | ((uint32_t)(s_hlit - 257) << 3) | ((uint32_t)(s_hdist - 1) << 8) |
+                      ((uint32_t)(hclen - 4) << 13));
+        t.hdr[95] = hbits + ebits;
+    }
+    __syncthreads();
+    T3MARK(6);
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&t);
     uint32_t* dst = reinterpret_cast<uint32_t*>(T);
     for (int i = tid; i < (int)(sizeof(DflTables) / 4); i += kHuffThreads) dst[i] = src[i];
+    T3MARK(7);
 }
 
 __global__ void __launch_bounds__(kHuffThreads) k_png_tables(const uint32_t* __restrict__ hist, DflTables* __restrict__ T) {
@@ -1840,32 +1925,6 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
     }
     unsigned long long* rs = B.row_sums + 2 * ((int64_t)I.row0 + y0);
     if (lane < 2 * (y1 - y0)) rs[lane] = lane == 0 ? s1 : lane == 1 ? s2 : 0ull;
-}
-
-__device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wave[wid] = x;
-    __syncthreads();
-    if (wid == 0) {
-        uint32_t w = lane < nw ? s_wave[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(w, o, 64);
-            if (lane >= o) w += y;
-        }
-        if (lane < nw) s_wave[lane] = w;
-    }
-    __syncthreads();
-    const uint32_t off = wid ? s_wave[wid - 1] : 0;
-    total = s_wave[nw - 1];
-    __syncthreads();
-    return off + x - v;
 }
 
 // P2: the parse of one block: the image's symbol histograms (eight LDS copies, lane & 7, two
