@@ -2209,6 +2209,65 @@ __device__ __forceinline__ void trace_codes(uint32_t S, uint32_t M, uint32_t D, 
     }
 }
 
+// P4's pass-1 walk without branches (round 6; OMR_PNG_ENC_FLAT=0 builds the trace_codes form):
+// every step takes one token -- a match, or one or two literals -- and puts its whole code at
+// once.  A match's code comes from one 8-byte table entry per (distance candidate, length) --
+// the four candidate distances are the image's, a length is <= 32 (tokens stay inside their
+// segment) -- holding the length code + extra bits, then the distance code + extra bits (<= 48
+// bits), and the bit count in bits 58-63.  The literal and match values are both formed and one
+// selected, so a wave with literals in some lanes and matches in others runs one path instead of
+// both under masks (the branchy walk ran ~140 instructions per step).
+constexpr int kMcLen = 33;                       // match table: [candidate][length 0..32]
+template <typename Byte, typename Put>
+__device__ __forceinline__ void trace_codes_flat(uint32_t S, uint32_t M, uint32_t D, int n, Byte&& seg,
+                                                 const uint64_t* mc, const uint32_t* lc, Put& put) {
+    while (S) {
+        const int p = __builtin_ctz(S);
+        S &= S - 1;
+        const int q = S ? __builtin_ctz(S) : n;
+        const bool ism = (M >> p) & 1u;
+        const uint64_t me = mc[(D & 3u) * kMcLen + (uint32_t)(q - p)];
+        const uint32_t e1 = lc[seg(p)];
+        // a literal followed by a literal (the next byte starts a token that is no match)
+        const bool pair = !ism && q < n && !((M >> q) & 1u);
+        const uint32_t e2 = lc[seg(pair ? q : p)];
+        const uint32_t n1 = e1 >> 16, n2 = pair ? e2 >> 16 : 0u;
+        const uint64_t lv = (e1 & 0xFFFFu) | (pair ? (e2 & 0xFFFFu) << n1 : 0u);
+        put(ism ? me & 0xFFFFFFFFFFFFull : lv, ism ? (uint32_t)(me >> 58) : n1 + n2);
+        S = pair ? S & (S - 1) : S;
+        D = ism ? D >> 2 : D;
+    }
+}
+
+// The same walk taking up to four literals in a row per step (OMR_PNG_ENC_FLAT=2, the default):
+// the four bytes from p come out of the lane's stream column as one word (two reads and an
+// alignbyte), their four codes are read, and those past the run of literals get length 0 -- a
+// literal-heavy segment (most of a photographic tile) takes 8 steps instead of 16.  Codes of a
+// step: up to 4 x 15 bits, or a match's <= 48.
+template <typename Word4, typename Put>
+__device__ __forceinline__ void trace_codes_quad(uint32_t S, uint32_t M, uint32_t D, int n, Word4&& seg4,
+                                                 const uint64_t* mc, const uint32_t* lc, Put& put) {
+    const uint32_t L = S & ~M;                      // literal starts
+    while (S) {
+        const int p = __builtin_ctz(S);
+        const bool ism = (M >> p) & 1u;
+        // literals in a row from p, at most 4 (L holds no bit at or past n)
+        const int k = ism ? 1 : min(4, (int)__builtin_ctz(~(L >> p) | 0x10u));
+        const uint32_t Sn = S & ~(((2u << (k - 1)) - 1u) << p);   // the next tokens
+        const int q = Sn ? __builtin_ctz(Sn) : n;
+        const uint64_t me = mc[(D & 3u) * kMcLen + (uint32_t)(q - p)];
+        const uint32_t b4 = seg4(p);
+        const uint32_t e0 = lc[b4 & 255u], e1 = lc[(b4 >> 8) & 255u], e2 = lc[(b4 >> 16) & 255u], e3 = lc[b4 >> 24];
+        const uint32_t n0 = e0 >> 16, n1 = k > 1 ? e1 >> 16 : 0u, n2 = k > 2 ? e2 >> 16 : 0u, n3 = k > 3 ? e3 >> 16 : 0u;
+        const uint32_t p01 = (e0 & 0xFFFFu) | (k > 1 ? (e1 & 0xFFFFu) << n0 : 0u);
+        const uint32_t p23 = (k > 2 ? e2 & 0xFFFFu : 0u) | (k > 3 ? (e3 & 0xFFFFu) << n2 : 0u);
+        const uint64_t lv = (uint64_t)p01 | ((uint64_t)p23 << (n0 + n1));
+        put(ism ? me & 0xFFFFFFFFFFFFull : lv, ism ? (uint32_t)(me >> 58) : n0 + n1 + n2 + n3);
+        S = Sn;
+        D = ism ? D >> 2 : D;
+    }
+}
+
 __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
     png_build_tables(B.hist + (size_t)blockIdx.x * 316, B.tab + blockIdx.x);
 }
@@ -2219,6 +2278,9 @@ __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
 // high-entropy data) ORs its interior words straight into memory (the slow path).
 constexpr int kEncWords = kPngbGroup * kSeg * 8 / 32 + 96 + 4;
 constexpr int kEncScr = 8;                       // words of codes a lane keeps in LDS (256 bits)
+#ifndef OMR_PNG_ENC_FLAT
+#define OMR_PNG_ENC_FLAT 2
+#endif
 static_assert(kPngbGroup == 2 * kParseLanes, "P4 groups are two parse blocks");
 
 // The codes of one packed token through put(value, bits), with the code tables packed as
@@ -2247,6 +2309,9 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     __shared__ uint32_t scr[kEncScr * kPngbGroup];              // [word][lane]: each lane's codes from bit 0
     __shared__ uint32_t s_end[2];                               // slow path: the group's first / last word
     __shared__ uint32_t s_wave[kPngbGroup / 64];
+#if OMR_PNG_ENC_FLAT
+    __shared__ uint64_t mc[4 * kMcLen];                         // match codes (trace_codes_flat)
+#endif
     const int i = pngb_image(B, B.grp0, B.grp_per, blockIdx.x);
     const PngImg& I = B.img[i];
     const int64_t gfirst = B.uniform ? (int64_t)i * B.grp_per : I.grp0;
@@ -2305,6 +2370,56 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
                             (uint32_t)I.rowlen};               // lz_seg_prepare's candidates
     auto seg_byte = [&](int p) { return (s_buf[(p >> 2) * kPngbGroup + threadIdx.x] >> (8 * (p & 3))) & 0xFFu; };
     uint32_t nb = 0;
+#if OMR_PNG_ENC_FLAT
+    if (threadIdx.x < 4 * kMcLen) {                             // (lc, dc, T are staged: barrier above)
+        const int k = threadIdx.x / kMcLen, l = threadIdx.x % kMcLen;
+        uint64_t e = 0;
+        if (l >= 3) {
+            const uint32_t t = pack_match(T, (uint32_t)l, dl[k]);
+            const int ls = (int)(t & 31), ds = (int)((t >> 5) & 31);
+            const uint32_t le = lc[257 + ls], de = dc[ds];
+            const uint32_t lb = (le >> 16) + (uint32_t)len_xbits_of(ls), db = (de >> 16) + (uint32_t)dist_xbits_of(ds);
+            const uint64_t lv = (le & 0xFFFFu) | (((t >> 10) & 31u) << (le >> 16));
+            const uint64_t dv = (de & 0xFFFFu) | (((t >> 15) & 0x1FFFu) << (de >> 16));
+            e = lv | (dv << lb) | ((uint64_t)(lb + db) << 58);
+        }
+        mc[threadIdx.x] = e;
+    }
+    __syncthreads();
+    // pass 1: the lane's codes from bit 0 into its scratch column (a lane whose codes pass
+    // kEncScr words only counts them and codes again in pass 2); codes of up to 48 bits, the
+    // pending bits (< 32) in a 64-bit accumulator, at most two words out per put
+    if (live) {
+        n = (int)min((int64_t)kSeg, I.raw - s * kSeg);
+        uint64_t acc = 0;
+        uint32_t nacc = 0, nw = 0;
+        auto put = [&](uint64_t v, uint32_t bits) {
+            const uint64_t lo = acc | (v << nacc);
+            const uint32_t hi = nacc ? (uint32_t)(v >> (64 - nacc)) : 0u;
+            const uint32_t tot = nacc + bits;
+            if (tot >= 32 && nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)lo;
+            if (tot >= 64 && nw + 1 < (uint32_t)kEncScr) scr[(nw + 1) * kPngbGroup + threadIdx.x] = (uint32_t)(lo >> 32);
+            acc = tot >= 64 ? (uint64_t)hi : tot >= 32 ? (lo >> 32) | ((uint64_t)hi << 32) : lo;
+            nw += (tot >= 32 ? 1u : 0u) + (tot >= 64 ? 1u : 0u);
+            nacc = tot & 31u;
+        };
+#if OMR_PNG_ENC_FLAT == 2
+        auto seg4 = [&](int p) {                                // stream bytes p .. p + 3 of the lane
+            const int d = p >> 2;
+            const uint32_t lo = s_buf[d * kPngbGroup + threadIdx.x];
+            const uint32_t hi = s_buf[min(d + 1, kSeg / 4 - 1) * kPngbGroup + threadIdx.x];   // (past the segment: unused)
+            return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(p & 3));
+        };
+        trace_codes_quad(S, M, D, n, seg4, mc, lc, put);
+        (void)seg_byte;
+#else
+        trace_codes_flat(S, M, D, n, seg_byte, mc, lc, put);
+#endif
+        if (last) put(lc[256] & 0xFFFFu, lc[256] >> 16);
+        if (nacc > 0 && nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)acc;
+        nb = 32 * nw + nacc;
+    }
+#else
     // pass 1: the lane's codes from bit 0 into its scratch column (a lane whose codes pass
     // kEncScr words only counts them and codes again in pass 2)
     if (live) {
@@ -2327,6 +2442,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         if (nacc > 0 && nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)acc;
         nb = 32 * nw + (uint32_t)nacc;
     }
+#endif
     // a lane whose codes passed its scratch column codes them again in pass 2, from its stream
     // bytes kept in that column (the stream buffer becomes the word buffer; the scan's barriers
     // order these copies before it is zeroed)

@@ -55,6 +55,13 @@ def main():
         ln = lens[:n].cpu().numpy()
         res[f"batch{n}"] = {"ms_per_call": round(1e3 * el / iters, 4), "tiles_per_s": round(n * iters / el, 1),
                             "mean_file_bytes": int(ln.mean()), "status_ok": int((stat[:n] == 0).sum().item())}
+        if os.environ.get("PNG_PROBE_HASH"):               # the files' bytes, for same-output A/Bs
+            import hashlib
+            ob, oo = out.cpu().numpy(), offs[:n].cpu().numpy()
+            h = hashlib.sha256()
+            for k in range(n):
+                h.update(ob[oo[k]:oo[k] + ln[k].astype("uint32")].tobytes())
+            res[f"batch{n}"]["sha256"] = h.hexdigest()
         ctx.kernel_timings()                            # per-stage HIP events (kinds 20-26)
         ctx.enable_kernel_timing(True)
         for _ in range(4):
