@@ -816,13 +816,16 @@ __device__ __forceinline__ uint32_t pngb_block_excl_scan(uint32_t v, uint32_t* s
 // Measurement build only (tools/ab_build.sh <name> -DOMR_PNG_T3_PROBE): block 0's shader-clock
 // stamps at the phases of the table build, read back by omr_png_t3_probe (tools/png_batch_probe.py).
 #ifdef OMR_PNG_T3_PROBE
-__device__ unsigned long long g_t3[16];
+__device__ unsigned long long g_t3[32];
 #define T3MARK(i) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_t3[i] = __builtin_amdgcn_s_memtime(); } while (0)
+// P4 phases of one workgroup in the middle of the grid, in g_t3[16 + i]
+#define T4MARK(i) do { if (blockIdx.x == gridDim.x / 2 && threadIdx.x == 0) g_t3[16 + (i)] = __builtin_amdgcn_s_memtime(); } while (0)
 extern "C" int omr_png_t3_probe(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_t3), sizeof(g_t3)) == hipSuccess ? 0 : 1;
 }
 #else
 #define T3MARK(i) do {} while (0)
+#define T4MARK(i) do {} while (0)
 #endif
 
 // The table block D4/D5 read: codes, lengths and the block header bits.
@@ -2277,7 +2280,14 @@ __global__ void __launch_bounds__(kHuffThreads) k_pngb_tables(PngBatch B) {
 // LDS for 8 bits per stream byte + header; a group whose codes need more (<= 16 bits per byte:
 // high-entropy data) ORs its interior words straight into memory (the slow path).
 constexpr int kEncWords = kPngbGroup * kSeg * 8 / 32 + 96 + 4;
-constexpr int kEncScr = 8;                       // words of codes a lane keeps in LDS (256 bits)
+#ifndef OMR_PNG_ENC_SCR
+#define OMR_PNG_ENC_SCR 10
+#endif
+// Words of codes a lane keeps in LDS: 10 (320 bits, 10 bits per stream byte; round 6).  A lane
+// past them codes its tokens again in pass 2 with a word-by-word atomic put, and its wave (and
+// the workgroup's barrier) waits for it: at 8 words (256 bits) enough C2 segments passed that P4
+// ran 1.03 ms per 256 tiles, at 10 or 12 words 0.73-0.75 (profiles/r06/ab_png_encode_scr.txt).
+constexpr int kEncScr = OMR_PNG_ENC_SCR;
 #ifndef OMR_PNG_ENC_FLAT
 #define OMR_PNG_ENC_FLAT 2
 #endif
@@ -2306,7 +2316,8 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     static_assert(kEncWords * 4 >= kPngbGroup * kSeg, "stream bytes fit the word buffer");
     __shared__ DeflateTabs T;
     __shared__ uint32_t lc[286], dc[30];                        // code | length << 16
-    __shared__ uint32_t scr[kEncScr * kPngbGroup];              // [word][lane]: each lane's codes from bit 0
+    __shared__ uint32_t scr[(kEncScr + 2) * kPngbGroup];        // [word][lane]: each lane's codes from bit 0
+                                                                // (+2 rows: pass 1's spill, see put)
     __shared__ uint32_t s_end[2];                               // slow path: the group's first / last word
     __shared__ uint32_t s_wave[kPngbGroup / 64];
 #if OMR_PNG_ENC_FLAT
@@ -2318,6 +2329,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     const int64_t blk = (int64_t)blockIdx.x - gfirst;
     const int64_t g = blockIdx.x;                               // this workgroup's group
     const DflTables* Tb = B.tab + i;
+    T4MARK(0);
     // the group's bit range from P3b: its first parse block's offset (the header opens group 0)
     // to the next group's (or the stream's end)
     const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
@@ -2364,6 +2376,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         for (int k = 0; k < kSeg / 4; ++k) s_buf[k * kPngbGroup + threadIdx.x] = x[k];
     }
     __syncthreads();
+    T4MARK(1);
     const bool last = s == I.nseg - 1;                          // the EOB code follows its tokens
     int n = 0;
     const uint32_t dl[4] = {1u, I.bpp == 1 ? (uint32_t)I.rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
@@ -2393,14 +2406,22 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         n = (int)min((int64_t)kSeg, I.raw - s * kSeg);
         uint64_t acc = 0;
         uint32_t nacc = 0, nw = 0;
+        // every put stores the three words its bits can reach, unconditionally (a partial word
+        // is stored again, more complete, by the next put; rows past the lane's last word hold
+        // zeros or nothing pass 2 reads).  From word kEncScr - 1 on the stores stay at rows 7-9:
+        // such a lane passes kEncScr words, and pass 2 codes it again from its stream bytes.
         auto put = [&](uint64_t v, uint32_t bits) {
             const uint64_t lo = acc | (v << nacc);
-            const uint32_t hi = nacc ? (uint32_t)(v >> (64 - nacc)) : 0u;
-            const uint32_t tot = nacc + bits;
-            if (tot >= 32 && nw < (uint32_t)kEncScr) scr[nw * kPngbGroup + threadIdx.x] = (uint32_t)lo;
-            if (tot >= 64 && nw + 1 < (uint32_t)kEncScr) scr[(nw + 1) * kPngbGroup + threadIdx.x] = (uint32_t)(lo >> 32);
-            acc = tot >= 64 ? (uint64_t)hi : tot >= 32 ? (lo >> 32) | ((uint64_t)hi << 32) : lo;
-            nw += (tot >= 32 ? 1u : 0u) + (tot >= 64 ? 1u : 0u);
+            const uint32_t hi = (uint32_t)((v >> 1) >> (63 - nacc));          // bits past 64 (0 when nacc = 0)
+            const uint32_t tot = nacc + bits, wn = tot >> 5;                  // whole words done: 0 .. 2
+            uint32_t* col = scr + min(nw, (uint32_t)kEncScr - 1) * kPngbGroup + threadIdx.x;
+            col[0] = (uint32_t)lo;
+            col[kPngbGroup] = (uint32_t)(lo >> 32);
+            col[2 * kPngbGroup] = hi;
+            const uint32_t a0 = wn == 0 ? (uint32_t)lo : wn == 1 ? (uint32_t)(lo >> 32) : hi;
+            const uint32_t a1 = wn == 0 ? (uint32_t)(lo >> 32) : wn == 1 ? hi : 0u;
+            acc = ((uint64_t)a1 << 32) | a0;
+            nw += wn;
             nacc = tot & 31u;
         };
 #if OMR_PNG_ENC_FLAT == 2
@@ -2450,6 +2471,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
 #pragma unroll
         for (int k = 0; k < kSeg / 4; ++k) scr[k * kPngbGroup + threadIdx.x] = x[k];
     }
+    T4MARK(2);
     uint32_t total;
     const uint32_t ex = pngb_block_excl_scan(nb, s_wave, total);
     const uint32_t hb = Tb->hdr[95];
@@ -2464,6 +2486,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         __threadfence_block();                                  // the zeroed words before any OR
     }
     __syncthreads();
+    T4MARK(3);
     if (blk == 0 && threadIdx.x == 0)
         for (uint32_t k = 0; k < (hb + 31) / 32; ++k) orw(k, Tb->hdr[k]);
     if (live && nb) {
@@ -2502,6 +2525,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         }
     }
     __syncthreads();
+    T4MARK(4);
     // whole words inside [b0, b1) go out; the first and last (shared with the neighbouring
     // blocks) are kept for P5
     const uint32_t cf = big ? s_end[0] : sw[0], cl = nwl ? (big ? s_end[1] : sw[nwl]) : 0u;
@@ -2518,6 +2542,7 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         B.blk_cf[g] = cf;
         B.blk_cl[g] = cl;
     }
+    T4MARK(5);
 }
 
 // P5: the words two or more blocks share.  Block g handles the partial word its stream ends in,

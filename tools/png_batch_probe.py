@@ -74,12 +74,14 @@ def main():
         res[f"batch{n}"]["stage_ms"] = {k: round(sum(v) / len(v), 4) for k, v in sorted(acc.items())}
     if hasattr(_lib.lib, "omr_png_t3_probe"):            # a -DOMR_PNG_T3_PROBE build: P3 phase clocks
         import ctypes
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 32)()
         if _lib.lib.omr_png_t3_probe(buf) == 0:
             t = list(buf)
             res["t3_phase_cycles"] = {f"{a}-{b}": int(t[b] - t[a]) for a, b in
                                       ((0, 1), (1, 2), (2, 3), (3, 4), (4, 5), (5, 6), (6, 7),
                                        (8, 9), (9, 10), (10, 11), (11, 12))}
+            res["t4_phase_cycles"] = {f"{a}-{b}": int(t[16 + b] - t[16 + a]) for a, b in
+                                      ((0, 1), (1, 2), (2, 3), (3, 4), (4, 5))}
     # single-tile path (host D3, one sync per tile)
     t0 = time.perf_counter()
     k = 32
