@@ -1627,7 +1627,15 @@ constexpr int kPngbEmitBytes = 16 * 256;        // output bytes per P8 workgroup
 #endif
 constexpr int kPngbEmitCrcStrip = OMR_PNG_CRC_STRIP_KIB * 1024;   // bytes a wave emits and CRCs (steps of 1 KiB)
 constexpr int kPngbEmitCrcBytes = 4 * kPngbEmitCrcStrip;   // file bytes per workgroup (4 waves)
-// env OMR_PNG_CRC_P9=1: the round-5 form (P8 4 KiB per workgroup, then the separate P9 pass)
+// Direct mode (round 6, the default; env OMR_PNG_DIRECT=0 for the forms below): P5b / P6 run before
+// P4, which codes into the files in place; P8 then stores only the bytes around the streams and
+// P9 CRCs the files (k_pngb_crc).
+static bool png_direct() {
+    static const bool v = [] { const char* e = std::getenv("OMR_PNG_DIRECT"); return !(e && std::atoi(e) == 0); }();
+    return v;
+}
+// env OMR_PNG_CRC_P9=1 (with OMR_PNG_DIRECT=0): the round-5 form (P8 4 KiB per workgroup, then
+// the separate P9 pass); otherwise P8 with the CRC fused (k_pngb_emit_crc)
 static bool png_crc_separate() {
     static const bool v = [] { const char* e = std::getenv("OMR_PNG_CRC_P9"); return e && std::atoi(e) != 0; }();
     return v;
@@ -1689,6 +1697,7 @@ struct PngBatch {
     int32_t* d_status;
     const uint32_t* crc_pow;                    // [kCrcPowAll] (k_png_crc_pow)
     uint32_t* strip_crc;                        // [P8 workgroups][4] raw CRC of each P8+P9 strip at its end
+    int32_t direct, pad4;                       // P4 codes straight into the files (png_direct())
 };
 
 // Image owning global item `x` of a stage whose per-image first items are `first` (sorted).
@@ -1700,6 +1709,22 @@ __device__ __forceinline__ int pngb_image(const PngBatch& B, const int32_t* firs
         if (first[mid] <= x) lo = mid; else hi = mid - 1;
     }
     return lo;
+}
+
+// Where P4 / P5 put image I's deflate words, and the bit offset of the stream in them: the words
+// buffer (bit 0), or -- direct mode (round 6) -- the file itself: the stream starts at file byte
+// pre_len + 10 (after the IDAT length and type and the zlib header), so the words are the file's
+// aligned dwords from a = (pre_len + 10) mod 4 bytes before it, and bit 8a is the stream's bit 0.
+// The file offsets (P5b, P6) are known before P4: they follow from P3b's stream lengths.
+__device__ __forceinline__ uint32_t* pngb_stream_words(const PngBatch& B, const PngImg& I, const PngMeta& M,
+                                                       uint32_t& bo) {
+    if (!B.direct) {
+        bo = 0;
+        return B.words + I.words;
+    }
+    const int a = (I.pre_len + 10) & 3;
+    bo = 8u * (uint32_t)a;
+    return reinterpret_cast<uint32_t*>(B.out + M.off + I.pre_len + 10 - a);
 }
 
 __device__ __forceinline__ PngArgs pngb_args(const PngImg& I) {
@@ -2334,13 +2359,17 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     // to the next group's (or the stream's end)
     const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
     const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
-    const uint32_t c0 = B.poff[p0 + 2 * blk];                   // first code bit of the group
-    const uint32_t b0 = blk == 0 ? 0u : c0;
-    const uint32_t b1 = 2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i];
-    const uint32_t w0 = b0 >> 5, w1 = (b1 - 1) >> 5, nwl = w1 - w0;
-    // stored blocks win for this image (P5b decides the same from the same bits): nothing to code
+    // stored blocks win for this image (P5b decides the same from the same bits): nothing to code;
+    // direct mode: nor for a file without a slot in the output
     if (2 + ((int64_t)B.img_bits[i] + 7) / 8 + 4 >= 2 + 5 * I.nblk + I.raw + 4) return;
-    uint32_t* w = B.words + I.words;
+    if (B.direct && B.meta[i].off < 0) return;
+    uint32_t bo;                                                // the stream's bit 0 in the words
+    uint32_t* w = pngb_stream_words(B, I, B.meta[i], bo);
+    // (group 0 owns the bits below bo too: zero here, the zlib header's bytes are stored by P8)
+    const uint32_t c0 = B.poff[p0 + 2 * blk] + bo;              // first code bit of the group
+    const uint32_t b0 = blk == 0 ? 0u : c0;
+    const uint32_t b1 = (2 * blk + 2 < npb ? B.poff[p0 + 2 * blk + 2] : B.img_bits[i]) + bo;
+    const uint32_t w0 = b0 >> 5, w1 = (b1 - 1) >> 5, nwl = w1 - w0;
     uint32_t* const sw = s_buf;
     for (int k = threadIdx.x; k < 286; k += kPngbGroup) lc[k] = (uint32_t)Tb->lcode[k] | (uint32_t)Tb->llen[k] << 16;
     if (threadIdx.x < 30) dc[threadIdx.x] = (uint32_t)Tb->dcode[threadIdx.x] | (uint32_t)Tb->dlen[threadIdx.x] << 16;
@@ -2487,8 +2516,15 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     }
     __syncthreads();
     T4MARK(3);
-    if (blk == 0 && threadIdx.x == 0)
-        for (uint32_t k = 0; k < (hb + 31) / 32; ++k) orw(k, Tb->hdr[k]);
+    if (blk == 0 && threadIdx.x == 0) {                         // the block header, from bit bo
+        const uint32_t nh = (hb + 31) / 32;
+        uint32_t prev = 0;
+        for (uint32_t k = 0; k < (hb + bo + 31) / 32; ++k) {
+            const uint32_t v = k < nh ? Tb->hdr[k] : 0u;
+            orw(k, bo ? (v << bo) | (prev >> (32 - bo)) : v);
+            prev = v;
+        }
+    }
     if (live && nb) {
         const uint32_t pos = c0 + ex - 32 * w0;                 // bit position in sw
         const uint32_t sh = pos & 31, wb = pos >> 5;
@@ -2557,9 +2593,11 @@ __global__ void __launch_bounds__(256) k_pngb_fixup(PngBatch B) {
     if (2 + ((int64_t)B.img_bits[i] + 7) / 8 + 4 >= 2 + 5 * I.nblk + I.raw + 4) return;   // stored: P4 skipped
     const uint32_t b0 = B.blk_b0[g], b1 = B.blk_b1[g], w0 = b0 >> 5, w1 = (b1 - 1) >> 5;
     if ((b1 & 31) == 0 || !(w1 > w0 || (b0 & 31) == 0)) return;
+    if (B.direct && B.meta[i].off < 0) return;
     uint32_t v = w1 == w0 ? B.blk_cf[g] : B.blk_cl[g];
     for (int64_t j = g + 1; j < gend && B.blk_b0[j] < 32 * (w1 + 1); ++j) v |= B.blk_cf[j];
-    B.words[I.words + w1] = v;
+    uint32_t bo;
+    pngb_stream_words(B, I, B.meta[i], bo)[w1] = v;
 }
 
 // P5b: one workgroup per image: stream length, stored vs dynamic, Adler-32.
@@ -2721,6 +2759,29 @@ __global__ void __launch_bounds__(256) k_pngb_emit(PngBatch B) {
     const int64_t k0 = (lb * 256 + threadIdx.x) * 16;
     if (M.off < 0 || k0 >= M.file_len) return;
     *reinterpret_cast<uint4*>(B.out + M.off + k0) = pngb_file_chunk(B, I, M, k0);
+}
+
+// P8 in direct mode: the file's bytes around the stream P4 / P5 already coded in place -- the prefix
+// chunks, IDAT length and type, zlib header, Adler-32, IEND (the CRC is P10's) -- by byte stores
+// from each image's first workgroup; a stored-blocks file whole, 16 bytes per lane, as k_pngb_emit,
+// over the image's kEmitDirectWgs workgroups (grid: images x kEmitDirectWgs -- a grid of every
+// file's 4 KiB pieces, nearly all idle here, cost 0.06 ms of dispatch per 256 tiles).
+constexpr int kEmitDirectWgs = 16;
+__global__ void __launch_bounds__(256) k_pngb_emit_direct(PngBatch B) {
+    const int i = blockIdx.x / kEmitDirectWgs, lb = blockIdx.x % kEmitDirectWgs;
+    const PngImg& I = B.img[i];
+    const PngMeta& M = B.meta[i];
+    if (M.off < 0) return;
+    if (M.stored) {
+        for (int64_t k0 = ((int64_t)lb * 256 + threadIdx.x) * 16; k0 < M.file_len; k0 += kEmitDirectWgs * 256 * 16)
+            *reinterpret_cast<uint4*>(B.out + M.off + k0) = pngb_file_chunk(B, I, M, k0);
+        return;
+    }
+    if (lb != 0) return;
+    uint8_t* f = B.out + M.off;
+    const int64_t head = I.pre_len + 10, tail = I.pre_len + 8 + M.zlen - 4;   // Adler on
+    for (int64_t k = threadIdx.x; k < head; k += 256) f[k] = (uint8_t)pngb_file_byte(B, I, M, k);
+    for (int64_t k = tail + threadIdx.x; k < M.file_len; k += 256) f[k] = (uint8_t)pngb_file_byte(B, I, M, k);
 }
 
 // P9 tables (round 5): braid[b][v] = raw CRC of byte v at position b of a 4-byte word followed
@@ -3072,7 +3133,7 @@ static omr_status plan_png_batch(Ctx* ctx, const PngImgHost* im, int n, PngBatch
         d.pre_len = png_prefix(h.kind, h.W, h.H, h.rgba, d.pre);
         const int64_t npb = (d.nseg + kParseLanes - 1) / kParseLanes, ng = (d.nseg + kPngbGroup - 1) / kPngbGroup;
         const int64_t max_file = d.pre_len + 8 + P.zlen + 4 + 12;
-        const int64_t eb = png_crc_separate() ? kPngbEmitBytes : kPngbEmitCrcBytes;
+        const int64_t eb = png_direct() || png_crc_separate() ? kPngbEmitBytes : kPngbEmitCrcBytes;
         const int64_t ne = (max_file + eb - 1) / eb;
         const int64_t nc = (4 + P.zlen + kPngbCrcBytes - 1) / kPngbCrcBytes;
         if (L.rows + h.H > INT32_MAX || L.pblk + npb > INT32_MAX || L.grp + ng > INT32_MAX ||
@@ -3186,6 +3247,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     Bt.d_status = d_status;
     Bt.crc_pow = ctx->d_crc_pow;
     Bt.strip_crc = reinterpret_cast<uint32_t*>(ws + o_scrc);
+    Bt.direct = png_direct() ? 1 : 0;
     st = stage_h2d2(ctx, ws + o_img, I.data(), sizeof(PngImg) * n, ws + o_first, firsts.data(),
                     sizeof(int32_t) * 5 * n);
     if (st) return st;
@@ -3230,6 +3292,31 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
         KernelTimer t(ctx, 22);
         hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
         hipLaunchKernelGGL(k_pngb_block_offsets, dim3((unsigned)n), dim3(256), 0, s, Bt);
+    }
+    if (Bt.direct) {
+        // P5b, P6 (the files' lengths and offsets), P4 into the files, P5, P8 around the
+        // streams, P9, P10 (timer kinds: 24 meta + offsets, 23 encode, 25 fixup + emit, 26 CRC)
+        {
+            KernelTimer t(ctx, 24);
+            hipLaunchKernelGGL(k_pngb_meta, dim3((unsigned)n), dim3(256), 0, s, Bt);
+            hipLaunchKernelGGL(k_pngb_offsets, dim3(1), dim3(1024), 0, s, Bt);
+        }
+        {
+            KernelTimer t(ctx, 23);
+            hipLaunchKernelGGL(k_pngb_encode, dim3((unsigned)grp), dim3(kPngbGroup), 0, s, Bt);
+        }
+        {
+            KernelTimer t(ctx, 25);
+            hipLaunchKernelGGL(k_pngb_fixup, dim3((unsigned)((grp + 255) / 256)), dim3(256), 0, s, Bt);
+            hipLaunchKernelGGL(k_pngb_emit_direct, dim3((unsigned)(n * kEmitDirectWgs)), dim3(256), 0, s, Bt);
+        }
+        {
+            KernelTimer t(ctx, 26);
+            hipLaunchKernelGGL(k_pngb_crc, dim3((unsigned)cblk), dim3(256), 0, s, Bt);
+            hipLaunchKernelGGL(k_pngb_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Bt);
+        }
+        OMR_HIP(ctx, hipGetLastError());
+        return OMR_OK;
     }
     {
         KernelTimer t(ctx, 23);
