@@ -348,9 +348,10 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
 
 PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "png_sq.json")
 # batched PNG stages (omr_png.hip launch_png_batch timer kinds) -> the kernels they launch
+# (direct mode, the default since round 6: P5b/P6 before P4, which codes into the files)
 PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse", "k_pngb_hist"),
                      22: ("k_pngb_tables", "k_pngb_block_offsets"), 23: ("k_pngb_encode",),
-                     24: ("k_pngb_fixup", "k_pngb_meta", "k_pngb_offsets"), 25: ("k_pngb_emit",),
+                     24: ("k_pngb_meta", "k_pngb_offsets"), 25: ("k_pngb_fixup", "k_pngb_emit_direct"),
                      26: ("k_pngb_crc", "k_pngb_finish")}
 
 
@@ -865,17 +866,17 @@ def png_section(torch, ctx, data):
         ms = el * 1e3 / reps
         leg = {"tiles_per_s": round(n * reps / el, 1), "ms_per_call": round(ms, 4), "mean_png_bytes": int(ln.mean())}
         # Per-stage roofline from HIP events around each stage's launches (kinds 20-26,
-        # omr_png.hip launch_png_batch).  Algorithmic bytes per call: the filter reads the ARGB
-        # tiles and writes the filtered streams; the parse and the encoder read the streams (the
-        # encoder also writes the deflate words, ~ the files); emit reads the words and writes the
-        # files; CRC reads the files.  HBM-bound stages against 8 TB/s.
+        # omr_png.hip launch_png_batch; direct mode).  Algorithmic bytes per call: the filter reads
+        # the ARGB tiles and writes the filtered streams; the parse and the encoder read the streams
+        # (the encoder also writes the deflate stream into the files in place); P8 stores only the
+        # bytes around the streams; CRC reads the files.  HBM-bound stages against 8 TB/s.
         stages = {20: ("filter (P1)", n * TILE * TILE * 4 + n * raw),
                   21: ("LZ77 parse + histograms (P2)", n * raw),
                   22: ("huffman tables + block offsets (P3, P3b)", 0),
-                  23: ("encode (P4: codes from the parse traces)", n * raw + files),
-                  24: ("fixup + meta + offsets", 0),
-                  25: ("emit (P8)", 2 * files),
-                  26: ("crc (P9)", files)}
+                  23: ("encode (P4: codes from the parse traces, into the files)", n * raw + files),
+                  24: ("meta + file offsets (P5b, P6)", 0),
+                  25: ("fixup + bytes around the streams (P5, P8)", 0),
+                  26: ("IDAT CRC (P9, P10)", files)}
         per = {}
         for k, (name, alg) in stages.items():
             if k not in avg:
