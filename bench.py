@@ -903,6 +903,37 @@ def png_section(torch, ctx, data):
             if mt:
                 leg["roofline"]["measured_traffic"] = mt
         batched[f"tiles_per_call_{n}"] = leg
+    # 256 per call on two contexts taking alternate batches (as the batcher's two dispatch lanes
+    # do): one batch's latency-bound stages (P3: one workgroup per image; the small P5b/P6/P10
+    # launches) overlap the other's filter / parse / encode
+    if "tiles_per_call_256" in batched:
+        import omr
+        ctx2 = omr.Context(ctx.device, torch_order=False)
+        try:
+            n = 256
+            bufs = [(d_out, offs, lens, stat),
+                    (torch.empty(cap, dtype=torch.uint8, device=data.device),
+                     torch.empty(B, dtype=torch.int64, device=data.device),
+                     torch.empty(B, dtype=torch.int32, device=data.device),
+                     torch.empty(B, dtype=torch.int32, device=data.device))]
+            ctxs = [ctx, ctx2]
+            reps = 8
+            for k in range(4):
+                ctxs[k & 1].encode_png_batch_device(argb, n, TILE, TILE, *bufs[k & 1])
+            ctx.synchronize()
+            ctx2.synchronize()
+            t0 = time.perf_counter()
+            for k in range(2 * reps):
+                ctxs[k & 1].encode_png_batch_device(argb, n, TILE, TILE, *bufs[k & 1])
+            ctx.synchronize()
+            ctx2.synchronize()
+            el2 = time.perf_counter() - t0
+            ok = all(int((b[3][:n] != 0).sum().item()) == 0 for b in bufs)
+            assert ok, "PNG batch status (two contexts)"
+            assert torch.equal(bufs[0][2][:n], bufs[1][2][:n]), "two contexts' files differ in length"
+            batched["tiles_per_call_256"]["tiles_per_s_two_streams"] = round(2 * reps * n / el2, 1)
+        finally:
+            ctx2.close()
     res["batched"] = batched
     if "tiles_per_call_256" in batched:
         res["batched_vs_single"] = round(batched["tiles_per_call_256"]["tiles_per_s"] / res["single_tile_per_s"], 2)
@@ -1315,6 +1346,7 @@ def sections_summary(line):
     p = _get(line, "png", "batched", "tiles_per_call_256")
     if p:
         s["png_batched_256"] = {"tiles_per_s": p.get("tiles_per_s"), "ms_per_call": p.get("ms_per_call"),
+                                "tiles_per_s_two_streams": p.get("tiles_per_s_two_streams"),
                                 "hbm_frac": _get(p, "roofline", "frac"),
                                 "traffic_ratio": _get(p, "roofline", "measured_traffic", "ratio")}
     for alg in ("max", "mean"):
