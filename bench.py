@@ -336,7 +336,7 @@ def profile_provenance(doc, path):
     return out
 
 
-VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "jpeg_valu_pmc.json")
+VALU_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "jpeg_valu_pmc.json")
 VALU_PEAK_ISSUE_CYCLES_PER_S = 256 * 4 * 2.4e9   # 1,024 SIMD-32s at 2.4 GHz
 # issue cycles of one wave64 VALU instruction: 2 on a SIMD-32; f64 add / mul / fma issue at half
 # the f32 rate and transcendentals (v_exp / v_log / v_sqrt / v_rcp ...) at half the issue rate
@@ -346,7 +346,7 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
                       "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_TRANS_F32")
 
 
-PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "png_sq.json")
+PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "png_sq.json")
 # batched PNG stages (omr_png.hip launch_png_batch timer kinds) -> the kernels they launch
 # (direct mode, the default since round 6: P5b/P6 before P4, which codes into the files)
 PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse", "k_pngb_hist"),
@@ -357,7 +357,7 @@ PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse", "k_png
 
 def png_valu_roofline(stage_ms):
     """VALU issue of each batched PNG stage (256 C2 tiles per call): SQ_INSTS_VALU per launch from
-    the committed SQ passes (tools/gpu.sh sq=png -> tools/sq_json.py -> profiles/r05/png_sq.json,
+    the committed SQ passes (tools/gpu.sh sq=png -> tools/sq_json.py -> profiles/r06/png_sq.json,
     the same probe workload) x 2 issue cycles, over the stage's measured time; peak = every SIMD
     issuing every cycle.  Next to the stage's HBM frac it says which bound the stage is nearer."""
     try:
@@ -384,7 +384,7 @@ def png_valu_roofline(stage_ms):
     return out
 
 
-PNG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r05", "f2_pmc_traffic_png.json")
+PNG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "pmc_traffic_png.json")
 
 
 def png_measured_traffic(alg_bytes):
@@ -416,7 +416,7 @@ def png_measured_traffic(alg_bytes):
     return out
 
 
-JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r04", "pmc_traffic_jpeg_r04u2.json")
+JPEG_PMC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "pmc_traffic_jpeg.json")
 JPEG_FUSED_KERNELS = ("k_jpeg_render_fdct", "k_jpeg_block_bits", "k_jpeg_group_scan", "k_jpeg_huff_thread",
                       "k_jpeg_tile_scan", "k_jpeg_stuff_count", "k_jpeg_stuff_batch")
 
@@ -717,6 +717,11 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
                                     "off): the kernel duration a rocprofv3 trace reports",
                           "working_set": f"{C3_SETS} request stack sets x {C * Z * S * S * 2 >> 20} MiB in turn "
                                          "(beyond the 256 MiB Infinity Cache)"}}
+        if os.environ.get("OMR_K3R", "0") in ("", "0"):
+            tr = c3_trace_frac(0 if name == "max" else 1, alg_bytes)
+            if tr:
+                r["roofline"]["trace"] = tr
+                r["roofline"]["trace_consistent_frac"] = tr["frac"]
         if burst:
             r["roofline"]["burst_throughput_frac"] = round(alg_bytes / (burst * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             r["roofline"]["burst_timing"] = ("200 launches queued behind a spin kernel, two events around the "
@@ -744,6 +749,30 @@ def c3_section(torch, ctx, steps, warmup, cpu_seconds, threads, with_cpu):
         res[name] = r
     ctx2.close()
     return res
+
+
+C3_TRACE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "all_sections_kernels.json")
+
+
+def c3_trace_frac(alg, alg_bytes):
+    """The C3 K3 roofline from the committed all-sections rocprofv3 trace (tools/gpu.sh trace ->
+    tools/trace_kernels.py -> profiles/r06/all_sections_kernels.json): the median traced duration
+    of the bench's K3 launches (k_project_v, this projection, three 512^2 x 64 stacks), beside the
+    frac the bench's own per-launch events give."""
+    try:
+        with open(C3_TRACE) as fh:
+            doc = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    rows = [r for r in doc.get("kernels", []) if f"k_project_v<unsigned short, true, false, {alg}," in r["kernel"]
+            and r["grid_size"] == 393216]
+    if not rows:
+        return None
+    r = max(rows, key=lambda r: r["launches"])
+    out = profile_provenance(doc, C3_TRACE)
+    out.update({"launches": r["launches"], "median_ns": r["median_ns"], "avg_ns": r["avg_ns"],
+                "frac": round(alg_bytes / (r["median_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)})
+    return out
 
 
 def c5_section(torch, ctx, B, steps, warmup, cpu_seconds, threads, with_cpu):

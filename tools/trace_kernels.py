@@ -4,6 +4,7 @@ that the bench line's roofline fractions can be recomputed from (duration = End 
 
 Usage: trace_kernels.py TRACE.csv OUT.csv
 Columns: kernel, grid_size, workgroup_size, lds_bytes, launches, avg_ns, median_ns, min_ns, max_ns.
+Also writes OUT.json: the rows with the kernel-source build id (bench.kernel_build_id).
 """
 import csv
 import sys
@@ -31,6 +32,20 @@ def main():
             d = sorted(groups[key])
             w.writerow([key[0], key[1], meta[key][0], meta[key][1], len(d), round(sum(d) / len(d), 1),
                         d[len(d) // 2], d[0], d[-1]])
+    # the same rows as JSON with the kernel-source fingerprint of this tree (bench.py reads the
+    # committed all-sections trace through it: profile_provenance)
+    import json
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    rows = []
+    for key in sorted(groups, key=lambda k: -sum(groups[k])):
+        d = sorted(groups[key])
+        rows.append({"kernel": key[0], "grid_size": key[1], "launches": len(d), "avg_ns": round(sum(d) / len(d), 1),
+                     "median_ns": d[len(d) // 2], "min_ns": d[0], "max_ns": d[-1]})
+    with open(os.path.splitext(sys.argv[2])[0] + ".json", "w") as fh:
+        json.dump({"build_id": bench.kernel_build_id(), "source_trace": os.path.basename(sys.argv[1]),
+                   "kernels": rows}, fh, indent=0)
 
 
 if __name__ == "__main__":
