@@ -349,3 +349,44 @@ def test_png_batch_sparse_noisy_segments(ctx):
         assert not idat_is_stored(png)
         np.testing.assert_array_equal(np.asarray(decode(png)), rgb_of(argb[i]))
         assert png == ctx.encode_png(argb[i], w, h)
+
+
+_MODES_SCRIPT = r"""
+import hashlib, os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(os.environ["OMR_REPO"], "omero-ms-image-region_amd"))
+sys.path.insert(0, os.path.join(os.environ["OMR_REPO"], "tests"))
+import omr, torch
+from test_png_batch_gpu import tiles, encode_batch
+h = hashlib.sha256()
+with omr.Context(0) as ctx:
+    for kind, n, w, h_, seed in (("image", 5, 256, 200, 1), ("noise", 3, 130, 70, 2), ("flat", 2, 64, 8, 3),
+                                 ("image", 3, 1, 1, 4), ("image", 2, 1023, 33, 5)):
+        for st, off, png in encode_batch(ctx, tiles(kind, n, w, h_, seed)):
+            assert st == 0
+            h.update(png)
+        h.update(ctx.encode_png(tiles(kind, 1, w, h_, seed + 7)[0], w, h_))
+    rng = np.random.default_rng(6)
+    for w, h_ in ((333, 77), (64, 48)):
+        h.update(ctx.render_shape_mask_png(np.packbits(rng.integers(0, 2, w * h_)).tobytes(), w, h_, (9, 8, 7, 6)))
+print(h.hexdigest())
+"""
+
+
+def test_png_direct_mode_matches_words_buffer_forms():
+    """Direct mode (the default since round 6: P4 codes into the files in place, P8 stores only the
+    bytes around the streams) writes the same bytes as the words-buffer forms it replaced -- P8
+    with the CRC fused (OMR_PNG_DIRECT=0) and P8 + a separate P9 (OMR_PNG_CRC_P9=1).  The modes
+    are read once per process, so each runs in a child process, one after another."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    digests = {}
+    for name, env in (("direct", {}), ("fused", {"OMR_PNG_DIRECT": "0"}),
+                      ("separate", {"OMR_PNG_DIRECT": "0", "OMR_PNG_CRC_P9": "1"})):
+        e = dict(os.environ, OMR_REPO=repo, **env)
+        r = subprocess.run([sys.executable, "-c", _MODES_SCRIPT], env=e, capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, f"{name}: {r.stderr[-2000:]}"
+        digests[name] = r.stdout.strip().splitlines()[-1]
+    assert digests["direct"] == digests["fused"] == digests["separate"], digests
