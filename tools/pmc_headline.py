@@ -25,7 +25,7 @@ def main():
            "hbm_bytes_per_tile": (rd + wr) / TILES, "algorithmic_bytes_per_tile": ALG,
            "traffic_over_algorithmic": round((rd + wr) / TILES / ALG, 4),
            "note": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB->B; one counter per pass",
-           "source": tag}
+           "source": tag, "build_id": d.get("build_id")}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
