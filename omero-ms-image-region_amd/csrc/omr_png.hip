@@ -1786,6 +1786,19 @@ __global__ void __launch_bounds__(256) k_pngb_filter(PngBatch B) {
                     B.row_sums + 2 * ((int64_t)I.row0 + y0), s_rows);
 }
 
+// XCD-aware order of a grid's blocks (round 6): workgroup g runs on XCD g mod 8, so handing XCD x
+// the x-th contiguous eighth of the blocks puts a block and the one before it -- whose bytes its
+// look-back windows re-read -- on the same XCD, in the same L2.
+#ifndef OMR_PNG_XCD_ORDER
+#define OMR_PNG_XCD_ORDER 1
+#endif
+__device__ __forceinline__ int64_t xcd_block(int64_t g, int64_t total) {
+    if (!OMR_PNG_XCD_ORDER) return g;
+    constexpr int64_t X = 8;
+    const int64_t q = total / X, r = total % X, x = g % X, k = g / X;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 // D1, wave form (round 5): for a uniform batch of RGB images with W % 4 == 0 and W <= 1024 (the
 // rendered tiles), one wave filters a band of kFilterBandRows rows.  Lane l holds pixel quads
 // q = l + 64 m (4 px = 3 dwords of RGB, one coalesced 16-byte load), the row above stays in
@@ -1824,7 +1837,7 @@ template <int M>
 __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_fw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t wid = (int64_t)blockIdx.x * 4 + wv;
+    const int64_t wid = xcd_block(blockIdx.x, gridDim.x) * 4 + wv;   // (XCD order: the band above on the same L2)
     const int i = (int)(wid / B.fw_bands);
     if (i >= B.n) return;
     const PngImg& I = B.img[i];
@@ -1997,9 +2010,10 @@ __device__ __forceinline__ void lds_barrier() {
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     __shared__ uint32_t lh[kHistRows * 32];                 // u8 counters [bin / 4][copy]
     __shared__ DeflateTabs T;
-    const int i = pngb_image(B, B.pblk0, B.pblk_per, blockIdx.x);
+    const int64_t gblk = xcd_block(blockIdx.x, B.total_pblk);
+    const int i = pngb_image(B, B.pblk0, B.pblk_per, gblk);
     const PngImg& I = B.img[i];
-    const int64_t blk = (int64_t)blockIdx.x - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
+    const int64_t blk = gblk - (B.uniform ? (int64_t)i * B.pblk_per : I.pblk0);
     const int64_t s = blk * kParseLanes + threadIdx.x;
     const bool live = s < I.nseg;
     const uint8_t* f = B.flt + I.flt;                       // 16-byte aligned, >= 64 bytes of slack after
@@ -2106,7 +2120,7 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     lds_barrier();
     // per-block counts: bins 4r..4r+3 summed over the 32 copies of row r (u16 pairs: <= 32 x 128);
     // the image histogram is summed from them by k_pngb_hist (no per-block global atomics)
-    uint16_t* bh = B.bh + (size_t)blockIdx.x * 316;         // <= 4096 symbols per block: u16
+    uint16_t* bh = B.bh + (size_t)gblk * 316;               // <= 4096 symbols per block: u16
     for (int r = threadIdx.x; r < kHistRows; r += kParseLanes) {
         uint32_t ev = 0, od = 0;
 #pragma unroll 8
