@@ -349,7 +349,7 @@ VALU_SLOW_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INST
 PNG_SQ = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", "png_sq.json")
 # batched PNG stages (omr_png.hip launch_png_batch timer kinds) -> the kernels they launch
 # (direct mode, the default since round 6: P5b/P6 before P4, which codes into the files)
-PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4>",), 21: ("k_pngb_parse", "k_pngb_hist"),
+PNG_STAGE_KERNELS = {20: ("k_pngb_filter_wave<4, true>",), 21: ("k_pngb_parse", "k_pngb_hist"),
                      22: ("k_pngb_tables", "k_pngb_block_offsets"), 23: ("k_pngb_encode",),
                      24: ("k_pngb_meta", "k_pngb_offsets"), 25: ("k_pngb_fixup", "k_pngb_emit_direct"),
                      26: ("k_pngb_crc", "k_pngb_finish")}

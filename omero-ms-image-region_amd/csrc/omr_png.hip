@@ -361,8 +361,11 @@ __device__ __forceinline__ uint32_t paeth_pairs(uint32_t a, uint32_t b, uint32_t
     const omr_s16x2 pa = __builtin_elementwise_abs(d1), pb = __builtin_elementwise_abs(d2),
                     pc = __builtin_elementwise_abs(d1 + d2);
     const omr_s16x2 m = __builtin_elementwise_min(pb, pc);
-    const uint32_t na = __builtin_bit_cast(uint32_t, (omr_s16x2)((m - pa) >> 15));   // ~0: not a
-    const uint32_t nb = __builtin_bit_cast(uint32_t, (omr_s16x2)((pc - pb) >> 15));  // ~0: c over b
+    uint32_t na = __builtin_bit_cast(uint32_t, (omr_s16x2)((m - pa) >> 15));   // ~0: not a
+    uint32_t nb = __builtin_bit_cast(uint32_t, (omr_s16x2)((pc - pb) >> 15));  // ~0: c over b
+    // opaque masks: otherwise the selects below become a compare + v_cndmask per 16-bit half
+    // (plus the extracts and a v_perm to rejoin them) instead of one v_bitop3 each
+    asm("" : "+v"(na), "+v"(nb));
     const uint32_t bc = (nb & c) | (~nb & b);
     return (na & bc) | (~na & a);
 }
@@ -1822,6 +1825,19 @@ __device__ __forceinline__ uint32_t png_residual(int f, uint32_t X, uint32_t A, 
     }
 }
 
+// Sum over the wave's 64 lanes, returned in a scalar register (every lane active): sums of 16 by
+// four DPP adds (quad swaps, half-row and row mirrors), then the four rows' lanes read out.
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);   // row_mirror
+    return (uint32_t)(__builtin_amdgcn_readlane((int)v, 0) + __builtin_amdgcn_readlane((int)v, 16) +
+                      __builtin_amdgcn_readlane((int)v, 32) + __builtin_amdgcn_readlane((int)v, 48));
+}
+
+template <int V> struct FltIdx { static constexpr int value = V; };
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1833,8 +1849,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 template <int M> __host__ __device__ constexpr int fw_row_dwords() { return 3 * 64 * M + 1; }
 template <int M> __host__ __device__ constexpr size_t fw_lds_bytes() { return (size_t)4 * 2 * fw_row_dwords<M>() * 4; }
 
-template <int M>
-__global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
+#ifndef OMR_PNG_FW_WAVES
+#define OMR_PNG_FW_WAVES 5
+#endif
+// FULL: W == 256 * M (the 1024-wide tiles at M = 4), so every lane's quads and dwords lie inside
+// the row: no per-dword guards, and the compiler keeps the sums in v_sad_u8's accumulator and
+// batches the LDS reads across dwords.
+template <int M, bool FULL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OMR_PNG_FW_WAVES))) k_pngb_filter_wave(PngBatch B) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_fw[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t wid = xcd_block(blockIdx.x, gridDim.x) * 4 + wv;   // (XCD order: the band above on the same L2)
@@ -1856,14 +1878,14 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
         for (int m = 0; m < M; ++m) {
             const int q = lane + 64 * m;
             v[m] = make_uint4(0, 0, 0, 0);
-            if (y >= 0 && q < nq) v[m] = reinterpret_cast<const uint4*>(argb + (int64_t)y * W)[q];
+            if (y >= 0 && (FULL || q < nq)) v[m] = reinterpret_cast<const uint4*>(argb + (int64_t)y * W)[q];
         }
     };
     auto put_row = [&](const uint4 (&v)[M], uint32_t* row) {   // RGB dwords of the row at row[1 + j]
 #pragma unroll
         for (int m = 0; m < M; ++m) {
             const int q = lane + 64 * m;
-            if (q < nq) {
+            if (FULL || q < nq) {
                 row[1 + 3 * q] = __builtin_amdgcn_perm(v[m].y, v[m].x, 0x06000102u);       // r0 g0 b0 r1
                 row[2 + 3 * q] = __builtin_amdgcn_perm(v[m].z, v[m].y, 0x05060001u);       // g1 b1 r2 g2
                 row[3 + 3 * q] = __builtin_amdgcn_perm(v[m].w, v[m].z, 0x04050600u);       // b2 r3 g3 b3
@@ -1886,7 +1908,7 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
 #pragma unroll
         for (int t = 0; t < 3 * M; ++t) {
             const int j = lane + 64 * t;
-            if (j < nd) {
+            if (FULL || j < nd) {
                 const uint32_t X = cur[1 + j], Bv = prev[1 + j];
                 const uint32_t Av = __builtin_amdgcn_alignbyte(X, cur[j], 1);
                 const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, prev[j], 1);
@@ -1895,28 +1917,36 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
 #pragma unroll
                 for (int f = 0; f < 5; ++f) sm[f] = abs_sum8(r[f], sm[f]);
             }
+            if (FULL) __builtin_amdgcn_sched_barrier(0);      // one dword's reads at a time (VGPRs)
         }
-        int f = 0;
+        int f = 0;                                             // scalar: sums by DPP, read out
         uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
-            uint32_t v = sm[k];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            if (v < best) { best = v; f = k; }                 // wave-uniform; lowest filter on ties
+            const uint32_t v = wave_sum_dpp(sm[k]);
+            if (v < best) { best = v; f = k; }                 // lowest filter on ties
         }
-        // pass 2: the chosen residual row
+        // pass 2: the chosen residual row (one straight-line copy per filter, picked once per row)
         uint32_t c[3 * M];
+        auto pass2 = [&](auto F) {
 #pragma unroll
-        for (int t = 0; t < 3 * M; ++t) {
-            const int j = lane + 64 * t;
-            c[t] = 0u;
-            if (j < nd) {
-                const uint32_t X = cur[1 + j], Bv = prev[1 + j];
-                const uint32_t Av = __builtin_amdgcn_alignbyte(X, cur[j], 1);
-                const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, prev[j], 1);
-                c[t] = png_residual(f, X, Av, Bv, Cv);
+            for (int t = 0; t < 3 * M; ++t) {
+                const int j = lane + 64 * t;
+                c[t] = 0u;
+                if (FULL || j < nd) {
+                    const uint32_t X = cur[1 + j], Bv = prev[1 + j];
+                    const uint32_t Av = __builtin_amdgcn_alignbyte(X, cur[j], 1);
+                    const uint32_t Cv = __builtin_amdgcn_alignbyte(Bv, prev[j], 1);
+                    c[t] = png_residual(decltype(F)::value, X, Av, Bv, Cv);
+                }
             }
+        };
+        switch (f) {
+        case 0: pass2(FltIdx<0>{}); break;
+        case 1: pass2(FltIdx<1>{}); break;
+        case 2: pass2(FltIdx<2>{}); break;
+        case 3: pass2(FltIdx<3>{}); break;
+        default: pass2(FltIdx<4>{}); break;
         }
         const int64_t ypos = (int64_t)y * rowlen;              // the row's offset in the stream
         const int64_t row0 = I.flt + ypos;                     // ... and in B.flt (16-aligned base)
@@ -1928,18 +1958,20 @@ __global__ void __launch_bounds__(256) k_pngb_filter_wave(PngBatch B) {
 #pragma unroll
         for (int t = 0; t < 3 * M; ++t) {
             const int j = lane + 64 * t;
-            const uint32_t dn = __shfl_down(c[t], 1, 64);        // residual dword j + 1
-            const uint32_t wn = t + 1 < 3 * M ? __shfl(c[t + 1], 0, 64) : 0u;
+            // residual dword j + 1: lane l + 1's (DPP wave_shl:1), lane 63 takes lane 0's of t + 1
+            const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[t], 0x130, 0xF, 0xF, false);
+            const uint32_t wn = t + 1 < 3 * M ? (uint32_t)__builtin_amdgcn_readlane((int)c[t + 1], 0) : 0u;
             const uint32_t hi = lane == 63 ? wn : dn;
-            if (j < nd) {
+            if (FULL || j < nd) {
                 const uint32_t w = c[t];
-                if (j < jfull) gw[j] = __builtin_amdgcn_alignbyte(hi, w, u);
+                if ((FULL && t < 3 * M - 1) || j < jfull) gw[j] = __builtin_amdgcn_alignbyte(hi, w, u);
                 const uint32_t sv = __builtin_amdgcn_sad_u8(w, 0u, 0u);
                 a1 += sv;
                 aj += (uint32_t)j * sv;                        // <= 767 * 12 * 1020 per lane and row
                 ad = __builtin_amdgcn_udot4(w, 0x03020100u, ad, false);
                 // bytes outside the whole out dwords: the row's first u, its last (rb - u) & 3
-                if (4 * j < u || 4 * j + 3 >= u + 4 * jfull) {
+                // (FULL: only dword 0 and the row's last dword can hold such bytes)
+                if ((!FULL || t == 0 || t == 3 * M - 1) && (4 * j < u || 4 * j + 3 >= u + 4 * jfull)) {
                     for (int b = 0; b < 4; ++b) {
                         const int tt = 4 * j + b;
                         if (tt < u || tt >= u + 4 * jfull) flt[ypos + 1 + tt] = (uint8_t)byte_at(w, b);
@@ -3287,11 +3319,16 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
         if (wave_filter && uniform && im[0].kind == kRgb && W0 % 4 == 0 && W0 <= 1024) {
             Bt.fw_bands = (H0 + kFilterBandRows - 1) / kFilterBandRows;
             const unsigned blocks = (unsigned)(((int64_t)n * Bt.fw_bands + 3) / 4);
-            switch (fw_m) {
-            case 1: hipLaunchKernelGGL(k_pngb_filter_wave<1>, dim3(blocks), dim3(256), fw_lds_bytes<1>(), s, Bt); break;
-            case 2: hipLaunchKernelGGL(k_pngb_filter_wave<2>, dim3(blocks), dim3(256), fw_lds_bytes<2>(), s, Bt); break;
-            case 3: hipLaunchKernelGGL(k_pngb_filter_wave<3>, dim3(blocks), dim3(256), fw_lds_bytes<3>(), s, Bt); break;
-            default: hipLaunchKernelGGL(k_pngb_filter_wave<4>, dim3(blocks), dim3(256), fw_lds_bytes<4>(), s, Bt); break;
+            const bool full = W0 == 256 * fw_m;                // every lane's quads inside the row
+            switch (fw_m * 2 + (full ? 1 : 0)) {
+            case 2: hipLaunchKernelGGL((k_pngb_filter_wave<1, false>), dim3(blocks), dim3(256), fw_lds_bytes<1>(), s, Bt); break;
+            case 3: hipLaunchKernelGGL((k_pngb_filter_wave<1, true>), dim3(blocks), dim3(256), fw_lds_bytes<1>(), s, Bt); break;
+            case 4: hipLaunchKernelGGL((k_pngb_filter_wave<2, false>), dim3(blocks), dim3(256), fw_lds_bytes<2>(), s, Bt); break;
+            case 5: hipLaunchKernelGGL((k_pngb_filter_wave<2, true>), dim3(blocks), dim3(256), fw_lds_bytes<2>(), s, Bt); break;
+            case 6: hipLaunchKernelGGL((k_pngb_filter_wave<3, false>), dim3(blocks), dim3(256), fw_lds_bytes<3>(), s, Bt); break;
+            case 7: hipLaunchKernelGGL((k_pngb_filter_wave<3, true>), dim3(blocks), dim3(256), fw_lds_bytes<3>(), s, Bt); break;
+            case 8: hipLaunchKernelGGL((k_pngb_filter_wave<4, false>), dim3(blocks), dim3(256), fw_lds_bytes<4>(), s, Bt); break;
+            default: hipLaunchKernelGGL((k_pngb_filter_wave<4, true>), dim3(blocks), dim3(256), fw_lds_bytes<4>(), s, Bt); break;
             }
         } else {
             hipLaunchKernelGGL(k_pngb_filter, dim3((unsigned)L.rblk), dim3(256), rows_lds, s, Bt);
