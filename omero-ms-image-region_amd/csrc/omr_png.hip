@@ -1825,6 +1825,16 @@ __device__ __forceinline__ uint32_t png_residual(int f, uint32_t X, uint32_t A, 
     }
 }
 
+// v_writelane_b32: the uniform value v into lane `lane` of old (LLVM's intrinsic).
+__device__ int png_lane_write(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// Dword j + 1 of a row held as w[t] = dword lane + 64 t: lane l + 1's w (DPP wave_shl:1), lane 63
+// lane 0's of the next step (`nxt`, read out to a scalar and written into lane 63).
+__device__ __forceinline__ uint32_t next_lane_dword(uint32_t w, uint32_t nxt) {
+    const int dn = __builtin_amdgcn_mov_dpp((int)w, 0x130, 0xF, 0xF, true);
+    return (uint32_t)png_lane_write(__builtin_amdgcn_readlane((int)nxt, 0), 63, dn);
+}
+
 // Sum over the wave's 64 lanes, returned in a scalar register (every lane active): sums of 16 by
 // four DPP adds (quad swaps, half-row and row mirrors), then the four rows' lanes read out.
 __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
@@ -1958,10 +1968,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OMR_PN
 #pragma unroll
         for (int t = 0; t < 3 * M; ++t) {
             const int j = lane + 64 * t;
-            // residual dword j + 1: lane l + 1's (DPP wave_shl:1), lane 63 takes lane 0's of t + 1
-            const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[t], 0x130, 0xF, 0xF, false);
-            const uint32_t wn = t + 1 < 3 * M ? (uint32_t)__builtin_amdgcn_readlane((int)c[t + 1], 0) : 0u;
-            const uint32_t hi = lane == 63 ? wn : dn;
+            const uint32_t hi = next_lane_dword(c[t], t + 1 < 3 * M ? c[t + 1] : 0u);   // residual dword j + 1
             if (FULL || j < nd) {
                 const uint32_t w = c[t];
                 if ((FULL && t < 3 * M - 1) || j < jfull) gw[j] = __builtin_amdgcn_alignbyte(hi, w, u);
@@ -2012,6 +2019,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OMR_PN
 // counted by a static walk over the 32 bytes.  Symbol counts go to lane-private u8 counters in
 // LDS -- [bin / 4][lane & 31]: a lane's adds hit its own bank, no conflicts; at most 4 lanes x 32
 // symbols share a counter, so u8 never wraps.
+#ifndef OMR_PNG_LIT_FLAT
+#define OMR_PNG_LIT_FLAT 1
+#endif
 constexpr int kHistRows = 316 / 4 + 1;          // dwords of four u8 counters per copy
 
 __device__ __forceinline__ uint32_t eq_mask_q(const uint32_t (&x)[8], const uint32_t (&q)[9], int sh) {
@@ -2145,9 +2155,18 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
         }
         const uint32_t lit = nmask & ~cov;
         S |= lit;
+#if OMR_PNG_LIT_FLAT
+        // every byte's add issued, a non-literal's with 0: no exec-mask branch per byte
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+            const uint32_t b = (x[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            atomicAdd(hl + ((b >> 2) << 5), ((lit >> q) & 1u) << ((b << 3) & 31u));
+        }
+#else
 #pragma unroll
         for (int q = 0; q < 32; ++q)
             if (lit & (1u << q)) count((x[q >> 2] >> (8 * (q & 3))) & 0xFFu);
+#endif
     }
     lds_barrier();
     // per-block counts: bins 4r..4r+3 summed over the 32 copies of row r (u16 pairs: <= 32 x 128);
@@ -2916,29 +2935,36 @@ __global__ void __launch_bounds__(256) k_pngb_crc(PngBatch B) {
     const int sh = (int)(sa & 3);
     const int64_t arel = s0 - sh;                         // range offset of aw[0]
     uint32_t q = 0;
+    // an inner strip (s0 >= 0, not the last: every byte its 17 x 4 loads reach lies in the range)
+    // runs without the range tests (round 6: one wave-uniform branch per strip)
+    auto walk = [&](auto inner_c) {
+        constexpr bool kInner = decltype(inner_c)::value;
 #pragma unroll 1
-    for (int j0 = 0; j0 < 64; j0 += 16) {
-        uint32_t cw[17];
+        for (int j0 = 0; j0 < 64; j0 += 16) {
+            uint32_t cw[17];
 #pragma unroll
-        for (int t = 0; t < 17; ++t) {                    // 17 loads in flight; bytes outside the range read 0
-            const int64_t r = arel + 256 * (j0 + t) + 4 * lane;
-            cw[t] = (r > -4 && r < n) ? aw[64 * (j0 + t) + lane] : 0u;
-        }
+            for (int t = 0; t < 17; ++t) {                // 17 loads in flight; bytes outside the range read 0
+                const int64_t r = arel + 256 * (j0 + t) + 4 * lane;
+                cw[t] = (kInner || (r > -4 && r < n)) ? aw[64 * (j0 + t) + lane] : 0u;
+            }
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t dn = __shfl_down(cw[t], 1, 64);
-            const uint32_t wn = __shfl(cw[t + 1], 0, 64);
-            uint32_t w = __builtin_amdgcn_alignbyte(lane == 63 ? wn : dn, cw[t], sh);
-            const int64_t rel = s0 + 256 * (j0 + t) + 4 * lane;   // range offset of the word
-            if (rel < 0) w = rel <= -4 ? 0u : w & (0xFFFFFFFFu << (8 * (int)(-rel)));   // bytes before the range: 0
-            const uint32_t x = q ^ w;
-            if (j0 + t < 63) {
-                q = sb[0][x & 255] ^ sb[1][(x >> 8) & 255] ^ sb[2][(x >> 16) & 255] ^ sb[3][x >> 24];
-            } else {
-                q = sl[0][x & 255] ^ sl[1][(x >> 8) & 255] ^ sl[2][(x >> 16) & 255] ^ sl[3][x >> 24];
+            for (int t = 0; t < 16; ++t) {
+                uint32_t w = __builtin_amdgcn_alignbyte(next_lane_dword(cw[t], cw[t + 1]), cw[t], sh);
+                if (!kInner) {
+                    const int64_t rel = s0 + 256 * (j0 + t) + 4 * lane;   // range offset of the word
+                    if (rel < 0) w = rel <= -4 ? 0u : w & (0xFFFFFFFFu << (8 * (int)(-rel)));   // bytes before the range: 0
+                }
+                const uint32_t x = q ^ w;
+                if (j0 + t < 63) {
+                    q = sb[0][x & 255] ^ sb[1][(x >> 8) & 255] ^ sb[2][(x >> 16) & 255] ^ sb[3][x >> 24];
+                } else {
+                    q = sl[0][x & 255] ^ sl[1][(x >> 8) & 255] ^ sl[2][(x >> 16) & 255] ^ sl[3][x >> 24];
+                }
             }
         }
-    }
+    };
+    if (s0 >= 0 && g > 0) walk(FltIdx<1>{});
+    else walk(FltIdx<0>{});
     uint32_t v = q ? multmodp(c_braid.lane[lane], q) : 0u;
     for (int o = 32; o > 0; o >>= 1) v ^= __shfl_xor(v, o, 64);
     if (lane == 0) {
