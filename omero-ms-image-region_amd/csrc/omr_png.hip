@@ -2019,6 +2019,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OMR_PN
 // counted by a static walk over the 32 bytes.  Symbol counts go to lane-private u8 counters in
 // LDS -- [bin / 4][lane & 31]: a lane's adds hit its own bank, no conflicts; at most 4 lanes x 32
 // symbols share a counter, so u8 never wraps.
+// P2 match symbols from a per-workgroup (candidate, length) table instead of pack_match's four
+// table reads and the per-lane candidate distance select (round 6)
+#ifndef OMR_PNG_PARSE_PM
+#define OMR_PNG_PARSE_PM 1
+#endif
+constexpr int kPmLen = 33;
+#ifndef OMR_PNG_HIST_B128
+#define OMR_PNG_HIST_B128 1
+#endif                      // lengths 0..32 (tokens stay inside their segment)
 #ifndef OMR_PNG_LIT_FLAT
 #define OMR_PNG_LIT_FLAT 1
 #endif
@@ -2050,8 +2059,12 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
-    __shared__ uint32_t lh[kHistRows * 32];                 // u8 counters [bin / 4][copy]
+    __shared__ __attribute__((aligned(16))) uint32_t lh[kHistRows * 32];                 // u8 counters [bin / 4][copy]
+#if OMR_PNG_PARSE_PM
+    __shared__ uint32_t pm[4 * kPmLen];     // (candidate, length) -> the match's two symbols
+#else
     __shared__ DeflateTabs T;
+#endif
     const int64_t gblk = xcd_block(blockIdx.x, B.total_pblk);
     const int i = pngb_image(B, B.pblk0, B.pblk_per, gblk);
     const PngImg& I = B.img[i];
@@ -2081,7 +2094,23 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
         }
     }
     for (int k = threadIdx.x; k < kHistRows * 32; k += kParseLanes) lh[k] = 0;
+#if OMR_PNG_PARSE_PM
+    {   // 257 + length symbol | (286 + distance symbol) << 16 of every (candidate, length <= 32)
+        const uint32_t dl0[4] = {1u, I.bpp == 1 ? (uint32_t)rowlen : (uint32_t)I.bpp, (uint32_t)(2 * I.bpp),
+                                 (uint32_t)rowlen};
+        for (int e = threadIdx.x; e < 4 * kPmLen; e += kParseLanes) {
+            const int k = e / kPmLen, l = e % kPmLen;
+            uint32_t v = 0;
+            if (l >= 3) {
+                const uint32_t t = pack_match(c_dfl, (uint32_t)l, dl0[k]);
+                v = (257u + (t & 31u)) | ((286u + ((t >> 5) & 31u)) << 16);
+            }
+            pm[e] = v;
+        }
+    }
+#else
     lz_load_tabs(T);
+#endif
     uint32_t* const hl = lh + (threadIdx.x & 31);
     auto count = [&](uint32_t t) {                          // one symbol into this lane's counters
         atomicAdd(hl + ((t >> 2) << 5), 1u << ((t << 3) & 31u));
@@ -2144,13 +2173,19 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
                 const int l = v == 0xFFFFFFFFu ? 32 : __builtin_ctz(~v);   // run of equal bytes from p
                 if (l > best) { best = l; bk = k; }
             }
-            const uint32_t t = pack_match(T, (uint32_t)best, dl[bk]);
             S |= 1u << p;
             M |= 1u << p;
             D |= (uint32_t)bk << (2 * nm++);
             cov |= (best >= 32 ? 0xFFFFFFFFu : ((1u << best) - 1u)) << p;
+#if OMR_PNG_PARSE_PM
+            const uint32_t sy = pm[bk * kPmLen + best];     // one LDS read: both symbols
+            count(sy & 0xFFFFu);
+            count(sy >> 16);
+#else
+            const uint32_t t = pack_match(T, (uint32_t)best, dl[bk]);
             count(257 + (t & 31));
             count(286 + ((t >> 5) & 31));
+#endif
             p += best;
         }
         const uint32_t lit = nmask & ~cov;
@@ -2174,12 +2209,26 @@ __global__ void __launch_bounds__(kParseLanes) k_pngb_parse(PngBatch B) {
     uint16_t* bh = B.bh + (size_t)gblk * 316;               // <= 4096 symbols per block: u16
     for (int r = threadIdx.x; r < kHistRows; r += kParseLanes) {
         uint32_t ev = 0, od = 0;
+#if OMR_PNG_HIST_B128
+        // four copies per 16-byte read (rotated by the row: 8 lanes cover the 32 banks); even bytes
+        // by a mask, odd ones by a v_perm, two dwords per v_add3
+        const uint4* row4 = reinterpret_cast<const uint4*>(lh + r * 32);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint4 v = row4[(c + r) & 7];
+            ev += (v.x & 0x00FF00FFu) + (v.y & 0x00FF00FFu);
+            ev += (v.z & 0x00FF00FFu) + (v.w & 0x00FF00FFu);
+            od += __builtin_amdgcn_perm(0u, v.x, 0x0C030C01u) + __builtin_amdgcn_perm(0u, v.y, 0x0C030C01u);
+            od += __builtin_amdgcn_perm(0u, v.z, 0x0C030C01u) + __builtin_amdgcn_perm(0u, v.w, 0x0C030C01u);
+        }
+#else
 #pragma unroll 8
         for (int c = 0; c < 32; ++c) {
             const uint32_t v = lh[r * 32 + ((c + r) & 31)];  // rotated start: rows spread over banks
             ev += v & 0x00FF00FFu;
             od += (v >> 8) & 0x00FF00FFu;
         }
+#endif
         const uint32_t cnt[4] = {ev & 0xFFFFu, od & 0xFFFFu, ev >> 16, od >> 16};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
