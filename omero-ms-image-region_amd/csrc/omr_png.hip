@@ -2266,6 +2266,75 @@ __global__ void __launch_bounds__(320) k_pngb_hist(PngBatch B) {
 // symbol counts times the code lengths (extra bits included), an exclusive scan over the image's
 // blocks from the header's end gives every block's first bit -- so P4 needs no inter-block
 // communication at all.
+#ifndef OMR_PNG_BOFF_WAVE
+#define OMR_PNG_BOFF_WAVE 1
+#endif
+#if OMR_PNG_BOFF_WAVE
+// (round 6) A wave per parse block: the lanes read the block's 632-byte count row together (three
+// coalesced loads instead of 158 row-strided ones per lane), multiply by the code lengths held in
+// registers and sum by DPP; four blocks' loads in flight per wave, 16 waves, chunks of 1024 blocks
+// scanned by the workgroup.
+constexpr int kBoffThreads = 1024, kBoffChunk = 1024;
+__global__ void __launch_bounds__(kBoffThreads) k_pngb_block_offsets(PngBatch B) {
+    __shared__ uint32_t s_bits[kBoffChunk];
+    __shared__ uint32_t s_wave[kBoffThreads / 64];
+    __shared__ uint32_t s_carry;
+    const int i = blockIdx.x;
+    const PngImg& I = B.img[i];
+    const DflTables* T = B.tab + i;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int kWaves = kBoffThreads / 64;
+    auto cost_of = [&](int k) -> uint32_t {                    // code bits of symbol k (extra bits included)
+        if (k >= 316) return 0u;
+        if (k < 257) return T->llen[k];
+        if (k < 286) return T->llen[k] + len_xbits_of(k - 257);
+        return T->dlen[k - 286] + dist_xbits_of(k - 286);
+    };
+    uint32_t ce[3], co[3];                                    // lane's dwords lane + 64 m: symbols 2d, 2d + 1
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+        const int d = lane + 64 * m;
+        ce[m] = cost_of(2 * d);
+        co[m] = cost_of(2 * d + 1);
+    }
+    const uint32_t hb = T->hdr[95];
+    if (threadIdx.x == 0) s_carry = hb;
+    const int64_t p0 = B.uniform ? (int64_t)i * B.pblk_per : I.pblk0;
+    const int npb = (int)((I.nseg + kParseLanes - 1) / kParseLanes);
+    for (int j0 = 0; j0 < npb; j0 += kBoffChunk) {
+        const int nj = min(kBoffChunk, npb - j0);
+        for (int b = wv * 4; b < nj; b += 4 * kWaves) {        // four blocks per wave step
+            uint32_t v[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t* c2 = reinterpret_cast<const uint32_t*>(B.bh + (size_t)(p0 + j0 + min(b + u, nj - 1)) * 316);
+#pragma unroll
+                for (int m = 0; m < 3; ++m) v[u][m] = (m < 2 || lane < 158 - 128) ? c2[lane + 64 * m] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                uint32_t acc = 0;
+#pragma unroll
+                for (int m = 0; m < 3; ++m) acc += (v[u][m] & 0xFFFFu) * ce[m] + (v[u][m] >> 16) * co[m];
+                const uint32_t tot = wave_sum_dpp(acc);
+                if (lane == 0 && b + u < nj) s_bits[b + u] = tot;
+            }
+        }
+        __syncthreads();
+        const int j = j0 + (int)threadIdx.x;
+        const uint32_t bits = (int)threadIdx.x < nj ? s_bits[threadIdx.x] : 0u;
+        uint32_t tot;
+        const uint32_t ex = pngb_block_excl_scan(bits, s_wave, tot);
+        const uint32_t base = s_carry;
+        if (j < npb) B.poff[p0 + j] = base + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = base + tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) B.img_bits[i] = s_carry + T->llen[256];   // + EOB
+}
+#else
+constexpr int kBoffThreads = 256;
 __global__ void __launch_bounds__(256) k_pngb_block_offsets(PngBatch B) {
     __shared__ uint32_t cost[316];
     __shared__ uint32_t s_wave[4];
@@ -2305,6 +2374,8 @@ __global__ void __launch_bounds__(256) k_pngb_block_offsets(PngBatch B) {
     }
     if (threadIdx.x == 0) B.img_bits[i] = s_carry + T->llen[256];   // + EOB
 }
+
+#endif
 
 // The tokens of a segment from its parse trace (P2): t as lz_seg_tokens produced them.
 template <typename Byte, typename Tok>
@@ -3417,7 +3488,7 @@ static omr_status launch_png_batch(Ctx* ctx, PngBatchPlan& L, const PngImgHost* 
     {
         KernelTimer t(ctx, 22);
         hipLaunchKernelGGL(k_pngb_tables, dim3((unsigned)n), dim3(kHuffThreads), 0, s, Bt);
-        hipLaunchKernelGGL(k_pngb_block_offsets, dim3((unsigned)n), dim3(256), 0, s, Bt);
+        hipLaunchKernelGGL(k_pngb_block_offsets, dim3((unsigned)n), dim3(kBoffThreads), 0, s, Bt);
     }
     if (Bt.direct) {
         // P5b, P6 (the files' lengths and offsets), P4 into the files, P5, P8 around the
