@@ -249,11 +249,15 @@ def test_mask_batch_capacity(pixel_flip):
 
 
 @pytest.mark.parametrize("kind,n,w,h", [("image", 3, 1024, 40), ("noise", 2, 1024, 9), ("image", 5, 512, 33),
-                                        ("image", 4, 100, 17), ("image", 2, 764, 21), ("flat", 3, 8, 5)])
+                                        ("image", 4, 100, 17), ("image", 2, 764, 21), ("flat", 3, 8, 5),
+                                        ("noise", 3, 256, 19), ("image", 2, 768, 26), ("noise", 2, 768, 11),
+                                        ("image", 2, 260, 9)])
 def test_png_batch_wave_filter_matches_workgroup_filter(ctx, kind, n, w, h, monkeypatch):
     """D1's wave form (uniform RGB batches, W % 4 == 0, W <= 1024) writes the same filtered rows,
     the same filter bytes and the same Adler partials as the workgroup form: the files are
-    byte-identical (OMR_PNG_FILTER_WAVE=0 selects the workgroup form, read per call)."""
+    byte-identical (OMR_PNG_FILTER_WAVE=0 selects the workgroup form, read per call).  Widths
+    256 / 512 / 768 / 1024 run the guard-free FULL instantiations (M = 1..4), the others the
+    guarded ones."""
     argb = tiles(kind, n, w, h, 7 * w + h + n)
     monkeypatch.setenv("OMR_PNG_FILTER_WAVE", "0")
     ref = encode_batch(ctx, argb)
