@@ -2498,6 +2498,9 @@ constexpr int kEncWords = kPngbGroup * kSeg * 8 / 32 + 96 + 4;
 // the workgroup's barrier) waits for it: at 8 words (256 bits) enough C2 segments passed that P4
 // ran 1.03 ms per 256 tiles, at 10 or 12 words 0.73-0.75 (profiles/r06/ab_png_encode_scr.txt).
 constexpr int kEncScr = OMR_PNG_ENC_SCR;
+#ifndef OMR_PNG_ENC_LDS_T
+#define OMR_PNG_ENC_LDS_T 0
+#endif
 #ifndef OMR_PNG_ENC_FLAT
 #define OMR_PNG_ENC_FLAT 2
 #endif
@@ -2524,7 +2527,14 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
     // read on its own bank), then in the same LDS the group's code words (pass 2)
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kEncWords];
     static_assert(kEncWords * 4 >= kPngbGroup * kSeg, "stream bytes fit the word buffer");
+#if OMR_PNG_ENC_LDS_T
     __shared__ DeflateTabs T;
+#else
+    // (round 6) the deflate tables from constant memory: they serve only the (candidate, length)
+    // table build and the rare long-lane re-code, and their 1.2 KiB of LDS lets a seventh
+    // workgroup onto the CU
+    const DeflateTabs& T = c_dfl;
+#endif
     __shared__ uint32_t lc[286], dc[30];                        // code | length << 16
     __shared__ uint32_t scr[(kEncScr + 2) * kPngbGroup];        // [word][lane]: each lane's codes from bit 0
                                                                 // (+2 rows: pass 1's spill, see put)
@@ -2572,7 +2582,9 @@ __global__ void __launch_bounds__(kPngbGroup) k_pngb_encode(PngBatch B) {
         else if (li == 0 || li == nwl) orw(li, v);
         else w[w0 + li] = v;
     };
+#if OMR_PNG_ENC_LDS_T
     lz_load_tabs(T);
+#endif
     const int64_t s = blk * kPngbGroup + threadIdx.x;
     const bool live = s < I.nseg;
     uint32_t x[kSeg / 4] = {};                                  // the lane's 32 stream bytes
